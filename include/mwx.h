@@ -1,0 +1,239 @@
+/*
+ * mwx.h — C ABI of the MI355X-native Whisper engine.
+ *
+ * This is the drop-in boundary for the hot path of sentiric-stt-whisper-service.
+ * The service's SttEngine (src/stt_engine.cpp) binds the whisper.h subset listed
+ * below; every entry point here replaces exactly one of those symbols with the
+ * same argument meaning, ownership and error behaviour. Reference call sites
+ * (paths relative to the reference repository):
+ *
+ *   mwx_context_default_params            <- whisper_context_default_params      src/stt_engine.cpp:28
+ *   mwx_init_from_file_with_params        <- whisper_init_from_file_with_params  src/stt_engine.cpp:33
+ *   mwx_init_state                        <- whisper_init_state                  src/stt_engine.cpp:39
+ *   mwx_free_state / mwx_free             <- whisper_free_state / whisper_free   src/stt_engine.cpp:56-57
+ *   mwx_full_default_params               <- whisper_full_default_params         src/stt_engine.cpp:214
+ *   mwx_full_with_state                   <- whisper_full_with_state             src/stt_engine.cpp:245-246
+ *   mwx_full_n_segments_from_state        <- whisper_full_n_segments_from_state  src/stt_engine.cpp:261
+ *   mwx_full_get_segment_text_from_state  <- whisper_full_get_segment_text_from_state   :267
+ *   mwx_full_get_segment_t0/t1_from_state <- whisper_full_get_segment_t0/t1_from_state  :278-279
+ *   mwx_full_get_segment_speaker_turn_next_from_state <- whisper_..._speaker_turn_next  :280-281
+ *   mwx_full_n_tokens_from_state          <- whisper_full_n_tokens_from_state    src/stt_engine.cpp:284
+ *   mwx_full_get_token_data_from_state    <- whisper_full_get_token_data_from_state :288
+ *   mwx_token_to_str                      <- whisper_token_to_str                src/stt_engine.cpp:289
+ *   mwx_token_eot                         <- whisper_token_eot                   src/stt_engine.cpp:290
+ *   mwx_log_set                           <- whisper_log_set                     src/main.cpp:71
+ *
+ * New (no whisper.h counterpart): mwx_full_batch runs B independent clips in one
+ * batched GPU pass (the data-parallel unit of this engine), and
+ * mwx_write_synthetic_model writes a seeded model in the ggml .bin layout that
+ * src/model_manager.cpp provisions (no real checkpoints exist offline).
+ *
+ * Conventions: plain C, no exceptions cross this boundary, all functions return
+ * NULL / negative on failure (0 = success), strings returned by getters stay
+ * valid until the next mwx_full* call on the same state.
+ */
+#ifndef MWX_H
+#define MWX_H
+
+#include <stdbool.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MWX_SAMPLE_RATE 16000
+#define MWX_N_FFT 400
+#define MWX_HOP_LENGTH 160
+#define MWX_CHUNK_SIZE 30
+#define MWX_MAX_DECODERS 8
+
+typedef int32_t mwx_token;
+struct mwx_context;
+struct mwx_state;
+
+/* ggml_log_level-compatible levels (src/main.cpp:37-55 switches on these). */
+enum mwx_log_level {
+  MWX_LOG_LEVEL_NONE = 0,
+  MWX_LOG_LEVEL_DEBUG = 1,
+  MWX_LOG_LEVEL_INFO = 2,
+  MWX_LOG_LEVEL_WARN = 3,
+  MWX_LOG_LEVEL_ERROR = 4,
+  MWX_LOG_LEVEL_CONT = 5,
+};
+typedef void (*mwx_log_callback)(enum mwx_log_level level, const char* text,
+                                 void* user_data);
+
+struct mwx_context_params {
+  bool use_gpu;     /* must be true: the engine has no CPU path */
+  bool flash_attn;  /* accepted for API parity; attention is always fused */
+  int gpu_device;   /* HIP device ordinal */
+};
+
+enum mwx_sampling_strategy {
+  MWX_SAMPLING_GREEDY = 0,
+  MWX_SAMPLING_BEAM_SEARCH = 1,
+};
+
+typedef bool (*mwx_abort_callback)(void* user_data);
+
+/* Same fields and meaning as whisper_token_data. */
+typedef struct mwx_token_data {
+  mwx_token id;  /* token id */
+  mwx_token tid; /* forced timestamp token id */
+  float p;       /* probability of the token */
+  float plog;    /* log probability of the token */
+  float pt;      /* probability of the timestamp token */
+  float ptsum;   /* sum of probabilities of all timestamp tokens */
+  int64_t t0;    /* token-level timestamps (10 ms units), -1 if unset */
+  int64_t t1;
+  int64_t t_dtw;
+  float vlen; /* voice length of the token */
+} mwx_token_data;
+
+/* Mirrors the whisper_full_params fields the service sets or relies on
+ * (src/stt_engine.cpp:214-243) plus the upstream defaults it inherits. */
+struct mwx_full_params {
+  int strategy;
+  int n_threads;
+  int n_max_text_ctx;
+  int offset_ms;
+  int duration_ms;
+
+  bool translate;
+  bool no_context;
+  bool no_timestamps;
+  bool single_segment;
+  bool print_special;
+  bool print_progress;
+  bool print_realtime;
+  bool print_timestamps;
+
+  bool token_timestamps;
+  float thold_pt;
+  float thold_ptsum;
+  int max_len;
+  bool split_on_word;
+  int max_tokens;
+
+  int audio_ctx;
+  bool tdrz_enable;
+
+  const char* initial_prompt;
+  const mwx_token* prompt_tokens;
+  int prompt_n_tokens;
+
+  const char* language;
+  bool detect_language;
+
+  bool suppress_blank;
+  bool suppress_nst;
+
+  float temperature;
+  float max_initial_ts;
+  float length_penalty;
+  float temperature_inc;
+  float entropy_thold;
+  float logprob_thold;
+  float no_speech_thold;
+
+  struct {
+    int best_of;
+  } greedy;
+  struct {
+    int beam_size;
+    float patience;
+  } beam_search;
+
+  mwx_abort_callback abort_callback;
+  void* abort_callback_user_data;
+
+  /* Engine extension (benchmark workload only): when > 0 every clip is decoded
+   * as exactly one 30-s window of greedy steps with EOT and timestamp tokens
+   * suppressed, so each clip costs the same fixed number of decode steps. */
+  int bench_fixed_steps;
+};
+
+/* --- lifecycle --------------------------------------------------------- */
+struct mwx_context_params mwx_context_default_params(void);
+struct mwx_context* mwx_init_from_file_with_params(
+    const char* path_model, struct mwx_context_params params);
+struct mwx_state* mwx_init_state(struct mwx_context* ctx);
+void mwx_free_state(struct mwx_state* state);
+void mwx_free(struct mwx_context* ctx);
+
+/* --- inference --------------------------------------------------------- */
+struct mwx_full_params mwx_full_default_params(int strategy);
+
+/* Returns 0 on success, <0 on failure (same codes as whisper_full_with_state). */
+int mwx_full_with_state(struct mwx_context* ctx, struct mwx_state* state,
+                        struct mwx_full_params params, const float* samples,
+                        int n_samples);
+
+/* Batched variant: clip b (f32 PCM @16 kHz, n_samples[b] samples) is decoded
+ * into states[b]. All clips share params. Returns 0 or the first error. */
+int mwx_full_batch(struct mwx_context* ctx, struct mwx_state* const* states,
+                   struct mwx_full_params params,
+                   const float* const* samples, const int* n_samples,
+                   int n_clips);
+
+/* --- results ------------------------------------------------------------ */
+int mwx_full_n_segments_from_state(struct mwx_state* state);
+const char* mwx_full_get_segment_text_from_state(struct mwx_state* state,
+                                                 int i_segment);
+int64_t mwx_full_get_segment_t0_from_state(struct mwx_state* state,
+                                           int i_segment);
+int64_t mwx_full_get_segment_t1_from_state(struct mwx_state* state,
+                                           int i_segment);
+bool mwx_full_get_segment_speaker_turn_next_from_state(struct mwx_state* state,
+                                                       int i_segment);
+float mwx_full_get_segment_no_speech_prob_from_state(struct mwx_state* state,
+                                                     int i_segment);
+int mwx_full_n_tokens_from_state(struct mwx_state* state, int i_segment);
+mwx_token_data mwx_full_get_token_data_from_state(struct mwx_state* state,
+                                                  int i_segment, int i_token);
+int mwx_full_lang_id_from_state(struct mwx_state* state);
+
+/* --- vocabulary / model ------------------------------------------------- */
+const char* mwx_token_to_str(struct mwx_context* ctx, mwx_token token);
+mwx_token mwx_token_eot(struct mwx_context* ctx);
+mwx_token mwx_token_sot(struct mwx_context* ctx);
+mwx_token mwx_token_beg(struct mwx_context* ctx);
+mwx_token mwx_token_not(struct mwx_context* ctx);
+mwx_token mwx_token_nosp(struct mwx_context* ctx);
+mwx_token mwx_token_transcribe(struct mwx_context* ctx);
+mwx_token mwx_token_translate(struct mwx_context* ctx);
+mwx_token mwx_token_lang(struct mwx_context* ctx, int lang_id);
+int mwx_n_vocab(struct mwx_context* ctx);
+int mwx_n_text_ctx(struct mwx_context* ctx);
+int mwx_n_audio_ctx(struct mwx_context* ctx);
+int mwx_n_mels(struct mwx_context* ctx);
+int mwx_is_multilingual(struct mwx_context* ctx);
+int mwx_model_wtype(struct mwx_context* ctx); /* 1 = f16, 30 = bf16 */
+int mwx_lang_id(const char* lang);
+const char* mwx_lang_str(int id);
+int mwx_lang_max_id(void);
+/* Greedy longest-match tokenizer (whisper_tokenize semantics). Returns the
+ * number of tokens, or -(needed) if n_max_tokens is too small. */
+int mwx_tokenize(struct mwx_context* ctx, const char* text, mwx_token* tokens,
+                 int n_max_tokens);
+
+void mwx_log_set(mwx_log_callback log_callback, void* user_data);
+
+/* --- model tooling --------------------------------------------------------
+ * Writes a model in the ggml .bin layout read by whisper.cpp and by
+ * mwx_init_from_file_with_params: magic, 11 hparams, mel filterbank, vocab,
+ * tensors. Weights are splitmix64-seeded; wtype 1 = f16, 30 = bf16 for the 2-D
+ * tensors (1-D tensors, conv biases and positional embeddings are f32, as in
+ * the upstream converter). arch: "tiny.en", "tiny", "base.en", "base",
+ * "small", "medium", "large-v3", or "micro" (test-sized).
+ * Returns 0 on success. */
+int mwx_write_synthetic_model(const char* path, const char* arch, int wtype,
+                              uint64_t seed);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MWX_H */

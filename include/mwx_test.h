@@ -1,0 +1,38 @@
+/*
+ * mwx_test.h — per-stage entry points of the mwx engine used by the parity
+ * tests (tests/test_gpu_parity.py). They run one stage of the device hot path
+ * for a single clip and copy the result back to the host as f32, so each stage
+ * can be compared with the CPU oracle (oracle/) in isolation. Not used by the
+ * service path.
+ */
+#ifndef MWX_TEST_H
+#define MWX_TEST_H
+
+#include "mwx.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Device log-mel of one clip. out receives [n_mels][n_len] (if out_cap is
+ * large enough); returns n_len, or <0 on error. */
+int mwx_test_mel(struct mwx_context* ctx, struct mwx_state* state, const float* pcm, int n,
+                 float* out, long out_cap);
+
+/* mel + conv stem + encoder + cross K/V of one clip at `seek`. enc_out:
+ * [n_audio_ctx][n_audio_state] (encoder output after ln_post, as stored on the
+ * device); k_out / v_out (nullable): [n_text_layer][n_audio_ctx][n_text_state]
+ * cross K/V. The cross K/V stay resident in `state` for mwx_test_decode. */
+int mwx_test_encode(struct mwx_context* ctx, struct mwx_state* state, const float* pcm, int n,
+                    int seek, float* enc_out, float* k_out, float* v_out);
+
+/* Teacher-forced decoder run against the cross K/V left by mwx_test_encode:
+ * token i at position i, logits_out [n][n_vocab] (raw logits). */
+int mwx_test_decode(struct mwx_context* ctx, struct mwx_state* state, const int* tokens, int n,
+                    float* logits_out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MWX_TEST_H */

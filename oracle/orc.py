@@ -1,0 +1,249 @@
+"""ctypes binding of the CPU oracle (liborc.so) — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module, and only as the checker. See oracle/mwx_oracle.cpp for what the
+oracle restates (whisper.cpp v1.8.2 semantics; parity with whisper.cpp itself
+is unpinned because the reference ships no fixtures and whisper.cpp is not
+available offline).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liborc.so")
+ORC_EXACT = 1
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        build()
+    L = C.CDLL(LIB_PATH)
+    P = C.c_void_p
+    fp = C.POINTER(C.c_float)
+    L.orc_load.restype = P
+    L.orc_load.argtypes = [C.c_char_p, C.c_int]
+    L.orc_free.argtypes = [P]
+    L.orc_set_threads.argtypes = [C.c_int]
+    L.orc_hparams.argtypes = [P, C.POINTER(C.c_int)]
+    L.orc_wtype.restype = C.c_int
+    L.orc_wtype.argtypes = [P]
+    L.orc_special.argtypes = [P, C.POINTER(C.c_int)]
+    L.orc_token_str.restype = C.c_char_p
+    L.orc_token_str.argtypes = [P, C.c_int]
+    L.orc_filters.restype = fp
+    L.orc_filters.argtypes = [P]
+    L.orc_mel.restype = C.c_int
+    L.orc_mel.argtypes = [P, fp, C.c_int, fp, C.c_int, C.POINTER(C.c_int)]
+    L.orc_encode.argtypes = [P, fp, C.c_int, C.c_int, fp]
+    L.orc_cross.argtypes = [P, fp, fp, fp]
+    L.orc_decode_seq.argtypes = [P, fp, fp, C.POINTER(C.c_int), C.c_int, fp]
+    L.orc_full.restype = P
+    L.orc_full.argtypes = [P, C.POINTER(C.c_int), fp, C.c_char_p, C.c_char_p, fp, C.c_int,
+                           C.POINTER(C.c_int)]
+    L.orc_full_free.argtypes = [P]
+    L.orc_full_n_segments.restype = C.c_int
+    L.orc_full_n_segments.argtypes = [P]
+    L.orc_full_segment_text.restype = C.c_char_p
+    L.orc_full_segment_text.argtypes = [P, C.c_int]
+    L.orc_full_segment_times.argtypes = [P, C.c_int, C.POINTER(C.c_int64)]
+    L.orc_full_n_tokens.restype = C.c_int
+    L.orc_full_n_tokens.argtypes = [P, C.c_int]
+    L.orc_full_token.argtypes = [P, C.c_int, C.c_int, C.POINTER(C.c_int), fp,
+                                 C.POINTER(C.c_int64)]
+    L.orc_full_lang_id.restype = C.c_int
+    L.orc_full_lang_id.argtypes = [P]
+    L.orc_full_n_windows.restype = C.c_int
+    L.orc_full_n_windows.argtypes = [P]
+    L.orc_full_window_tokens.restype = C.c_int
+    L.orc_full_window_tokens.argtypes = [P, C.c_int, C.POINTER(C.c_int), C.c_int]
+    _lib = L
+    return L
+
+
+def _fp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+@dataclass
+class OToken:
+    id: int
+    tid: int
+    p: float
+    plog: float
+    pt: float
+    ptsum: float
+    t0: int
+    t1: int
+
+
+@dataclass
+class OSegment:
+    t0: int
+    t1: int
+    text: str
+    tokens: List[OToken] = field(default_factory=list)
+
+
+@dataclass
+class FullOptions:
+    strategy: int = 0
+    best_of: int = 5
+    beam_size: int = 5
+    translate: bool = False
+    no_timestamps: bool = False
+    token_timestamps: bool = False
+    suppress_nst: bool = False
+    suppress_blank: bool = True
+    tdrz: bool = False
+    bench_fixed_steps: int = 0
+    no_context: bool = True
+    temperature: float = 0.0
+    temperature_inc: float = 0.2
+    entropy_thold: float = 2.4
+    logprob_thold: float = -1.0
+    no_speech_thold: float = 0.6
+    max_initial_ts: float = 1.0
+    length_penalty: float = -1.0
+    thold_pt: float = 0.01
+    thold_ptsum: float = 0.01
+    language: str = "en"
+    initial_prompt: Optional[str] = None
+
+    @classmethod
+    def service_defaults(cls, beam_size: int = 1) -> "FullOptions":
+        """Parameters SttEngine::transcribe sets (src/stt_engine.cpp:204-243)
+        with the Settings defaults of src/config.h (greedy when beam_size=1)."""
+        return cls(strategy=0 if beam_size <= 1 else 1, best_of=5, beam_size=beam_size,
+                   token_timestamps=True, suppress_nst=True, no_speech_thold=0.85,
+                   entropy_thold=2.40, logprob_thold=-0.7, temperature=0.0, language="auto")
+
+
+class Oracle:
+    def __init__(self, path: str, exact: bool = False, threads: Optional[int] = None):
+        L = lib()
+        if threads:
+            L.orc_set_threads(threads)
+        self.h = L.orc_load(path.encode(), ORC_EXACT if exact else 0)
+        if not self.h:
+            raise RuntimeError(f"oracle failed to load {path}")
+        hp = (C.c_int * 11)()
+        L.orc_hparams(self.h, hp)
+        self.hp = list(hp)
+        sp = (C.c_int * 9)()
+        L.orc_special(self.h, sp)
+        (self.eot, self.sot, self.translate, self.transcribe, self.solm, self.prev, self.nosp,
+         self.not_, self.beg) = list(sp)
+
+    def close(self):
+        if self.h:
+            lib().orc_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def n_vocab(self):
+        return self.hp[0]
+
+    @property
+    def n_mels(self):
+        return self.hp[9]
+
+    @property
+    def d(self):
+        return self.hp[2]
+
+    @property
+    def n_text_layer(self):
+        return self.hp[8]
+
+    def filters(self) -> np.ndarray:
+        p = lib().orc_filters(self.h)
+        return np.ctypeslib.as_array(p, shape=(self.n_mels * 201,)).reshape(self.n_mels, 201).copy()
+
+    def token_str(self, i: int) -> str:
+        return lib().orc_token_str(self.h, i).decode("utf-8", "replace")
+
+    def mel(self, pcm: np.ndarray):
+        pcm = np.ascontiguousarray(pcm, dtype=np.float32)
+        n_len = (len(pcm) + 480000) // 160
+        out = np.empty((self.n_mels, n_len), dtype=np.float32)
+        org = C.c_int()
+        r = lib().orc_mel(self.h, _fp(pcm), len(pcm), _fp(out), out.size, C.byref(org))
+        assert r == n_len
+        return out, org.value
+
+    def encode(self, mel: np.ndarray, seek: int = 0) -> np.ndarray:
+        mel = np.ascontiguousarray(mel, dtype=np.float32)
+        out = np.empty((self.hp[1], self.d), dtype=np.float32)
+        lib().orc_encode(self.h, _fp(mel), mel.shape[1], seek, _fp(out))
+        return out
+
+    def cross(self, enc: np.ndarray):
+        enc = np.ascontiguousarray(enc, dtype=np.float32)
+        k = np.empty((self.n_text_layer, self.hp[1], self.d), dtype=np.float32)
+        v = np.empty_like(k)
+        lib().orc_cross(self.h, _fp(enc), _fp(k), _fp(v))
+        return k, v
+
+    def decode_seq(self, k, v, tokens) -> np.ndarray:
+        toks = np.ascontiguousarray(tokens, dtype=np.int32)
+        out = np.empty((len(toks), self.n_vocab), dtype=np.float32)
+        lib().orc_decode_seq(self.h, _fp(np.ascontiguousarray(k)), _fp(np.ascontiguousarray(v)),
+                             toks.ctypes.data_as(C.POINTER(C.c_int)), len(toks), _fp(out))
+        return out
+
+    def full(self, pcm: np.ndarray, opt: FullOptions):
+        pcm = np.ascontiguousarray(pcm, dtype=np.float32)
+        ip = (C.c_int * 11)(opt.strategy, opt.best_of, opt.beam_size, int(opt.translate),
+                            int(opt.no_timestamps), int(opt.token_timestamps),
+                            int(opt.suppress_nst), int(opt.suppress_blank), int(opt.tdrz),
+                            opt.bench_fixed_steps, int(opt.no_context))
+        fpv = (C.c_float * 9)(opt.temperature, opt.temperature_inc, opt.entropy_thold,
+                              opt.logprob_thold, opt.no_speech_thold, opt.max_initial_ts,
+                              opt.length_penalty, opt.thold_pt, opt.thold_ptsum)
+        rc = C.c_int()
+        L = lib()
+        r = L.orc_full(self.h, ip, fpv, opt.language.encode(),
+                       opt.initial_prompt.encode() if opt.initial_prompt else None, _fp(pcm),
+                       len(pcm), C.byref(rc))
+        segs = []
+        for i in range(L.orc_full_n_segments(r)):
+            t = (C.c_int64 * 2)()
+            L.orc_full_segment_times(r, i, t)
+            seg = OSegment(t[0], t[1], L.orc_full_segment_text(r, i).decode("utf-8", "replace"))
+            for j in range(L.orc_full_n_tokens(r, i)):
+                ids = (C.c_int * 2)()
+                f = (C.c_float * 4)()
+                tt = (C.c_int64 * 2)()
+                L.orc_full_token(r, i, j, ids, f, tt)
+                seg.tokens.append(OToken(ids[0], ids[1], f[0], f[1], f[2], f[3], tt[0], tt[1]))
+            segs.append(seg)
+        lang = L.orc_full_lang_id(r)
+        windows = []
+        for w in range(L.orc_full_n_windows(r)):
+            buf = (C.c_int * 1024)()
+            n = L.orc_full_window_tokens(r, w, buf, 1024)
+            windows.append(list(buf)[:n])
+        L.orc_full_free(r)
+        return rc.value, segs, lang, windows

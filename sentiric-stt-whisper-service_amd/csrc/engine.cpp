@@ -1,0 +1,685 @@
+// mwx engine: context / state lifecycle, weight upload and the batched
+// whisper_full driver (the reference's L1 hot path), exposed
+// through the C ABI of include/mwx.h.
+//
+// Work split:
+//   device (HIP, gfx950): log-mel, conv stem, encoder, cross K/V, every decoder
+//     step (embedding -> layers -> logits -> logits processing + greedy pick);
+//   host: the whisper_full control flow — seek windows, prompt handling,
+//     temperature fallback, decoder state machine, sequence scoring, segment
+//     and token-timestamp construction — restated from whisper.cpp v1.8.2.
+//     Per decode step only a 32-byte record per row comes back to the host.
+//
+// Batching: mwx_full_batch runs B clips through every device stage together
+// (rows = clips x decoders); each clip keeps its own host state machine.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "kernels.h"
+
+#define HIPC(x)                                                                        \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess) {                                                            \
+      MWX_LOG_ERROR("mwx: HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, \
+                    __LINE__);                                                         \
+      throw std::runtime_error("hip");                                                 \
+    }                                                                                  \
+  } while (0)
+
+namespace mwx {
+
+static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// grow-only device buffer
+struct DBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  void* get(size_t bytes, bool zero = false) {
+    if (bytes > n) {
+      if (p) (void)hipFree(p);
+      p = nullptr;
+      n = 0;
+      HIPC(hipMalloc(&p, bytes));
+      n = bytes;
+      if (zero) HIPC(hipMemset(p, 0, bytes));
+    }
+    return p;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+struct EncLayerW {
+  const float *ln1_w, *ln1_b, *ln2_w, *ln2_b;
+  const void *qkv_w, *o_w, *fc1_w, *fc2_w;
+  const float *qkv_b, *o_b, *fc1_b, *fc2_b;
+};
+struct DecLayerW {
+  const float *ln1_w, *ln1_b, *lnc_w, *lnc_b, *ln2_w, *ln2_b;
+  const void *qkv_w, *o_w, *cq_w, *co_w, *fc1_w, *fc2_w;
+  const float *qkv_b, *o_b, *cq_b, *co_b, *fc1_b, *fc2_b;
+};
+
+struct Context {
+  Hparams hp;
+  Vocab vocab;
+  std::vector<float> filters;
+  int wtype = GGML_F16;
+  int device = 0;
+  int cpad = 128;  // conv1 input channels padded (3*cpad % 64 == 0)
+  void* arena = nullptr;
+  const float* d_filters = nullptr;
+  const float* d_tables = nullptr;  // hann[400], cos[400], sin[400]
+  const _Float16* conv1_w = nullptr;
+  const float* conv1_b = nullptr;
+  const _Float16* conv2_w = nullptr;
+  const float* conv2_b = nullptr;
+  const float* enc_pe = nullptr;
+  std::vector<EncLayerW> enc;
+  const float *enc_ln_w = nullptr, *enc_ln_b = nullptr;
+  const void* tok_emb = nullptr;
+  const float* dec_pe = nullptr;
+  std::vector<DecLayerW> dec;
+  const void* cross_w = nullptr;
+  const float* cross_b = nullptr;
+  const float *dec_ln_w = nullptr, *dec_ln_b = nullptr;
+  int space_id = -1;
+  std::vector<int> nst_ids;  // suppress_nst token ids
+};
+
+struct Segment {
+  int64_t t0, t1;
+  std::string text;
+  float no_speech_prob;
+  std::vector<mwx_token_data> tokens;
+  bool speaker_turn_next;
+};
+
+struct State {
+  Context* ctx = nullptr;
+  hipStream_t stream = nullptr;
+  // encoder workspace (clip-batched)
+  DBuf pcm, mel, melmax, melT, h1p, x, h, q, k, vt, o, ff, enc, cross_k, cross_v;
+  DBuf energy;
+  DBuf ibuf;  // small int arrays (slot maps)
+  // decoder workspace (row-batched)
+  DBuf xd, hd, qd, od, ffd, logits, kself, vself, stepin, ctl, tokout, probs, logprobs, smask;
+  int cross_cap = 0;  // cross cache slots
+  int row_cap = 0;    // self cache rows
+  std::vector<Segment> result_all;
+  int lang_id = 0;
+  std::mt19937 rng0 = std::mt19937(0);  // decoders[0].rng persists per state
+  std::vector<float> probs_h, logprobs_h;
+};
+
+// ---------------------------------------------------------------------------
+// model upload
+// ---------------------------------------------------------------------------
+static const FileTensor* find_t(const ModelFile& mf, const std::string& n) {
+  auto it = mf.tensors.find(n);
+  return it == mf.tensors.end() ? nullptr : &it->second;
+}
+
+static float elem_f32(const FileTensor& t, size_t i) {
+  switch (t.type) {
+    case GGML_F32: {
+      float f;
+      memcpy(&f, t.data.data() + i * 4, 4);
+      return f;
+    }
+    case GGML_F16: {
+      uint16_t h;
+      memcpy(&h, t.data.data() + i * 2, 2);
+      return f16_to_f32(h);
+    }
+    default: {
+      uint16_t h;
+      memcpy(&h, t.data.data() + i * 2, 2);
+      return bf16_to_f32(h);
+    }
+  }
+}
+
+namespace {
+struct Arena {
+  std::vector<uint8_t> host;
+  std::vector<std::pair<size_t, const void**>> fixups;
+  size_t add(const void* src, size_t bytes, const void** slot) {
+    const size_t off = align_up(host.size(), 256);
+    host.resize(off + bytes);
+    if (src) memcpy(host.data() + off, src, bytes);
+    fixups.emplace_back(off, slot);
+    return off;
+  }
+  uint8_t* at(size_t off) { return host.data() + off; }
+};
+}  // namespace
+
+static bool upload_model(Context& C, const ModelFile& mf) {
+  const Hparams& hp = C.hp;
+  const int d = hp.n_audio_state, dt = hp.n_text_state;
+  if (d != dt || d % 128 != 0 || d / hp.n_audio_head != 64 || dt / hp.n_text_head != 64) {
+    MWX_LOG_ERROR("mwx: unsupported dims (state %d/%d heads %d/%d)\n", d, dt, hp.n_audio_head,
+                  hp.n_text_head);
+    return false;
+  }
+  const FileTensor* te = find_t(mf, "decoder.token_embedding.weight");
+  if (!te) return false;
+  C.wtype = te->type == GGML_BF16 ? GGML_BF16 : GGML_F16;
+  const bool bf = C.wtype == GGML_BF16;
+  C.cpad = hp.n_mels <= 64 ? 64 : 128;
+  if (hp.n_mels > 128) return false;
+  Arena A;
+  bool ok = true;
+  auto need = [&](const std::string& n) -> const FileTensor* {
+    const FileTensor* t = find_t(mf, n);
+    if (!t) {
+      MWX_LOG_ERROR("mwx: missing tensor '%s'\n", n.c_str());
+      ok = false;
+    }
+    return t;
+  };
+  auto f32v = [&](const std::string& n, const float** slot, int64_t expect) {
+    const FileTensor* t = need(n);
+    if (!t) return;
+    if (t->nelements() != expect) {
+      MWX_LOG_ERROR("mwx: tensor '%s' has %lld elements, expected %lld\n", n.c_str(),
+                    (long long)t->nelements(), (long long)expect);
+      ok = false;
+      return;
+    }
+    std::vector<float> v(expect);
+    for (int64_t i = 0; i < expect; ++i) v[i] = elem_f32(*t, i);
+    A.add(v.data(), v.size() * 4, (const void**)slot);
+  };
+  // 16-bit weight in the model type, rows concatenated from several tensors
+  auto w16 = [&](const std::vector<std::string>& names, int64_t K, const void** slot) {
+    std::vector<const FileTensor*> ts;
+    int64_t rows = 0;
+    for (const auto& n : names) {
+      const FileTensor* t = need(n);
+      if (!t) return;
+      if (t->ne[0] != K) {
+        MWX_LOG_ERROR("mwx: tensor '%s' inner dim %lld != %lld\n", n.c_str(), (long long)t->ne[0],
+                      (long long)K);
+        ok = false;
+        return;
+      }
+      ts.push_back(t);
+      rows += t->nelements() / K;
+    }
+    const size_t off = A.add(nullptr, (size_t)rows * K * 2, slot);
+    uint16_t* dst = (uint16_t*)A.at(off);
+    for (const FileTensor* t : ts) {
+      const int64_t n = t->nelements();
+      const int want = bf ? GGML_BF16 : GGML_F16;
+      if (t->type == want) {
+        memcpy(dst, t->data.data(), n * 2);
+      } else {
+        for (int64_t i = 0; i < n; ++i) {
+          const float f = elem_f32(*t, i);
+          dst[i] = bf ? f32_to_bf16(f) : f32_to_f16(f);
+        }
+      }
+      dst += n;
+    }
+  };
+  // filters + mel tables
+  A.add(mf.filters.data(), mf.filters.size() * 4, (const void**)&C.d_filters);
+  {
+    std::vector<float> tab(1200);
+    for (int i = 0; i < 400; ++i) {
+      tab[i] = (float)(0.5 * (1.0 - cosf((float)((2.0 * M_PI * i) / 400))));
+      const double theta = (2 * M_PI * i) / 400;
+      tab[400 + i] = cosf((float)theta);
+      tab[800 + i] = sinf((float)theta);
+    }
+    A.add(tab.data(), tab.size() * 4, (const void**)&C.d_tables);
+  }
+  // conv stem: repack [D][C][3] -> [D][3][Cpad] / [D][3][D], always f16 (im2col type)
+  {
+    const FileTensor* c1 = need("encoder.conv1.weight");
+    const FileTensor* c2 = need("encoder.conv2.weight");
+    if (!c1 || !c2) return false;
+    const int nm = hp.n_mels, cp = C.cpad;
+    std::vector<uint16_t> w1((size_t)d * 3 * cp, 0), w2((size_t)d * 3 * d);
+    for (int o = 0; o < d; ++o)
+      for (int c = 0; c < nm; ++c)
+        for (int kk = 0; kk < 3; ++kk)
+          w1[((size_t)o * 3 + kk) * cp + c] = f32_to_f16(elem_f32(*c1, ((size_t)o * nm + c) * 3 + kk));
+    for (int o = 0; o < d; ++o)
+      for (int c = 0; c < d; ++c)
+        for (int kk = 0; kk < 3; ++kk)
+          w2[((size_t)o * 3 + kk) * d + c] = f32_to_f16(elem_f32(*c2, ((size_t)o * d + c) * 3 + kk));
+    A.add(w1.data(), w1.size() * 2, (const void**)&C.conv1_w);
+    A.add(w2.data(), w2.size() * 2, (const void**)&C.conv2_w);
+  }
+  f32v("encoder.conv1.bias", &C.conv1_b, d);
+  f32v("encoder.conv2.bias", &C.conv2_b, d);
+  f32v("encoder.positional_embedding", &C.enc_pe, (int64_t)hp.n_audio_ctx * d);
+  C.enc.resize(hp.n_audio_layer);
+  for (int l = 0; l < hp.n_audio_layer; ++l) {
+    const std::string p = "encoder.blocks." + std::to_string(l);
+    EncLayerW& L = C.enc[l];
+    f32v(p + ".attn_ln.weight", &L.ln1_w, d);
+    f32v(p + ".attn_ln.bias", &L.ln1_b, d);
+    f32v(p + ".mlp_ln.weight", &L.ln2_w, d);
+    f32v(p + ".mlp_ln.bias", &L.ln2_b, d);
+    w16({p + ".attn.query.weight", p + ".attn.key.weight", p + ".attn.value.weight"}, d, &L.qkv_w);
+    {
+      const FileTensor* qb = need(p + ".attn.query.bias");
+      const FileTensor* vb = need(p + ".attn.value.bias");
+      if (!qb || !vb) return false;
+      std::vector<float> b(3 * d, 0.0f);
+      for (int i = 0; i < d; ++i) {
+        b[i] = elem_f32(*qb, i);
+        b[2 * d + i] = elem_f32(*vb, i);
+      }
+      A.add(b.data(), b.size() * 4, (const void**)&L.qkv_b);
+    }
+    w16({p + ".attn.out.weight"}, d, &L.o_w);
+    f32v(p + ".attn.out.bias", &L.o_b, d);
+    w16({p + ".mlp.0.weight"}, d, &L.fc1_w);
+    f32v(p + ".mlp.0.bias", &L.fc1_b, 4 * d);
+    w16({p + ".mlp.2.weight"}, 4 * d, &L.fc2_w);
+    f32v(p + ".mlp.2.bias", &L.fc2_b, d);
+  }
+  f32v("encoder.ln_post.weight", &C.enc_ln_w, d);
+  f32v("encoder.ln_post.bias", &C.enc_ln_b, d);
+  w16({"decoder.token_embedding.weight"}, dt, &C.tok_emb);
+  f32v("decoder.positional_embedding", &C.dec_pe, (int64_t)hp.n_text_ctx * dt);
+  C.dec.resize(hp.n_text_layer);
+  std::vector<std::string> cross_names;
+  std::vector<float> cross_b;
+  for (int l = 0; l < hp.n_text_layer; ++l) {
+    const std::string p = "decoder.blocks." + std::to_string(l);
+    DecLayerW& L = C.dec[l];
+    f32v(p + ".attn_ln.weight", &L.ln1_w, dt);
+    f32v(p + ".attn_ln.bias", &L.ln1_b, dt);
+    f32v(p + ".cross_attn_ln.weight", &L.lnc_w, dt);
+    f32v(p + ".cross_attn_ln.bias", &L.lnc_b, dt);
+    f32v(p + ".mlp_ln.weight", &L.ln2_w, dt);
+    f32v(p + ".mlp_ln.bias", &L.ln2_b, dt);
+    w16({p + ".attn.query.weight", p + ".attn.key.weight", p + ".attn.value.weight"}, dt, &L.qkv_w);
+    {
+      const FileTensor* qb = need(p + ".attn.query.bias");
+      const FileTensor* vb = need(p + ".attn.value.bias");
+      if (!qb || !vb) return false;
+      std::vector<float> b(3 * dt, 0.0f);
+      for (int i = 0; i < dt; ++i) {
+        b[i] = elem_f32(*qb, i);
+        b[2 * dt + i] = elem_f32(*vb, i);
+      }
+      A.add(b.data(), b.size() * 4, (const void**)&L.qkv_b);
+    }
+    w16({p + ".attn.out.weight"}, dt, &L.o_w);
+    f32v(p + ".attn.out.bias", &L.o_b, dt);
+    w16({p + ".cross_attn.query.weight"}, dt, &L.cq_w);
+    f32v(p + ".cross_attn.query.bias", &L.cq_b, dt);
+    w16({p + ".cross_attn.out.weight"}, dt, &L.co_w);
+    f32v(p + ".cross_attn.out.bias", &L.co_b, dt);
+    w16({p + ".mlp.0.weight"}, dt, &L.fc1_w);
+    f32v(p + ".mlp.0.bias", &L.fc1_b, 4 * dt);
+    w16({p + ".mlp.2.weight"}, 4 * dt, &L.fc2_w);
+    f32v(p + ".mlp.2.bias", &L.fc2_b, dt);
+    cross_names.push_back(p + ".cross_attn.key.weight");
+    cross_names.push_back(p + ".cross_attn.value.weight");
+    const FileTensor* vb = need(p + ".cross_attn.value.bias");
+    if (!vb) return false;
+    for (int i = 0; i < dt; ++i) cross_b.push_back(0.0f);
+    for (int i = 0; i < dt; ++i) cross_b.push_back(elem_f32(*vb, i));
+  }
+  w16(cross_names, d, &C.cross_w);
+  A.add(cross_b.data(), cross_b.size() * 4, (const void**)&C.cross_b);
+  f32v("decoder.ln.weight", &C.dec_ln_w, dt);
+  f32v("decoder.ln.bias", &C.dec_ln_b, dt);
+  if (!ok) return false;
+  HIPC(hipMalloc(&C.arena, A.host.size()));
+  HIPC(hipMemcpy(C.arena, A.host.data(), A.host.size(), hipMemcpyHostToDevice));
+  for (auto& f : A.fixups) *f.second = (const uint8_t*)C.arena + f.first;
+  MWX_LOG_INFO("mwx: uploaded %.1f MB of weights to device %d\n", A.host.size() / 1048576.0,
+               C.device);
+  return true;
+}
+
+static const std::vector<std::string>& non_speech_tokens() {
+  static const std::vector<std::string> v = {
+      "\"", "#", "(", ")", "*", "+", "/", ":", ";", "<", "=", ">", "@", "[", "\\", "]", "^",
+      "_", "`", "{", "|", "}", "~", "「", "」", "『", "』", "<<", ">>", "<<<", ">>>", "--",
+      "---", "-(", "-[", "('", "(\"", "((", "))", "(((", ")))", "[[", "]]", "{{", "}}", "♪♪",
+      "♪♪♪", "♩", "♪", "♫", "♬", "♭", "♮", "♯"};
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// batched driver
+// ---------------------------------------------------------------------------
+struct TsState {
+  int64_t t_beg = 0, t_last = 0;
+  int tid_last = 0;
+  std::vector<float> energy;
+};
+
+struct ClipRun {
+  State* st = nullptr;
+  const float* pcm = nullptr;
+  int n = 0;
+  int n_len = 0, n_len_org = 0, n_fft_frames = 0;
+  size_t mel_off = 0;  // element offset of this clip's mel
+  int seek = 0, seek_start = 0, seek_end = 0;
+  bool finished = false;
+  std::vector<int> prompt_past, prompt_init, prompt;
+  int lang_id = 0;
+  TsState ts;
+  int enc_seek = -1;
+  std::vector<std::mt19937> rng;  // per decoder j (j = 0 aliases st->rng0)
+  float no_speech_prob = 0.0f;
+};
+
+struct Row {
+  int clip = 0, dec = 0;
+  int fed = 0;
+  bool stopped = false, failed = false, completed = false, has_ts = false;
+  int seek_delta = 3000, result_len = 0;
+  double sum_logprobs_all = 0.0, sum_logprobs = -INFINITY, avg_logprobs = -INFINITY,
+         entropy = 0.0, score = -INFINITY;
+  std::vector<mwx_token_data> tokens;
+};
+
+template <typename T>
+struct Driver {
+  Context& C;
+  State& S;
+  hipStream_t st;
+  const mwx_full_params& P;
+  const Hparams& hp;
+  int d, H, L_enc, L_dec, V, Tctx, Lp;
+  LogitsConst LC;
+
+  Driver(Context& c, State& s, const mwx_full_params& p)
+      : C(c), S(s), st(s.stream), P(p), hp(c.hp) {
+    d = hp.n_audio_state;
+    H = hp.n_audio_head;
+    L_enc = hp.n_audio_layer;
+    L_dec = hp.n_text_layer;
+    V = hp.n_vocab;
+    Tctx = hp.n_text_ctx;
+    Lp = (hp.n_audio_ctx + 7) & ~7;
+    LC.n_vocab = V;
+    LC.eot = C.vocab.token_eot;
+    LC.beg = C.vocab.token_beg;
+    LC.space_id = C.space_id;
+    LC.suppress_blank = P.suppress_blank ? 1 : 0;
+    LC.nosp_id = C.vocab.token_nosp;
+    if (P.max_initial_ts > 0.0f) {
+      const float precision = float(MWX_CHUNK_SIZE) / hp.n_audio_ctx;
+      LC.max_initial_tid = C.vocab.token_beg + (int)std::round(P.max_initial_ts / precision);
+    } else {
+      LC.max_initial_tid = -1;
+    }
+  }
+
+  const T* Wt(const void* p) const { return (const T*)p; }
+
+  // static suppression mask for this call's params
+  void build_static_mask() {
+    std::vector<float> m(V, 0.0f);
+    const Vocab& vb = C.vocab;
+    const float NI = -INFINITY;
+    m[vb.token_not] = NI;
+    if (P.no_timestamps)
+      for (int i = vb.token_beg; i < V; ++i) m[i] = NI;
+    m[vb.token_sot] = NI;
+    m[vb.token_nosp] = NI;
+    if (!P.tdrz_enable) m[vb.token_solm] = NI;
+    m[vb.token_translate] = NI;
+    m[vb.token_transcribe] = NI;
+    m[vb.token_prev] = NI;
+    for (int i = 0; i <= lang_max_id(); ++i) {
+      const int tok = vb.token_sot + 1 + i;
+      if (tok < V) m[tok] = NI;
+    }
+    if (P.suppress_nst)
+      for (int id : C.nst_ids) m[id] = NI;
+    if (P.bench_fixed_steps > 0) {
+      m[vb.token_eot] = NI;
+      for (int i = vb.token_beg; i < V; ++i) m[i] = NI;
+    }
+    float* dm = (float*)S.smask.get((size_t)V * 4);
+    HIPC(hipMemcpyAsync(dm, m.data(), (size_t)V * 4, hipMemcpyHostToDevice, st));
+  }
+
+  // ---------------- encoder: nb windows -> cross K/V slots ----------------
+  void encode(const std::vector<int>& clip_of_slot, const std::vector<int>& seek_of_slot,
+              const std::vector<int>& nlen_of_slot, const std::vector<int>& cross_slot,
+              long mel_clip_stride) {
+    const int nb = (int)clip_of_slot.size();
+    const int Lc = hp.n_audio_ctx, T2 = 2 * Lc, cp = C.cpad;
+    const int M = nb * Lc;
+    int* ib = (int*)S.ibuf.get(sizeof(int) * 4 * 4096);
+    std::vector<int> hb(4 * 4096, 0);
+    for (int i = 0; i < nb; ++i) {
+      hb[i] = clip_of_slot[i];
+      hb[4096 + i] = seek_of_slot[i];
+      hb[2 * 4096 + i] = nlen_of_slot[i];
+      hb[3 * 4096 + i] = cross_slot[i];
+    }
+    HIPC(hipMemcpyAsync(ib, hb.data(), hb.size() * 4, hipMemcpyHostToDevice, st));
+    _Float16* melT = (_Float16*)S.melT.get((size_t)nb * (T2 + 2) * cp * 2, true);
+    _Float16* h1p = (_Float16*)S.h1p.get((size_t)nb * (T2 + 2) * d * 2, true);
+    float* x = (float*)S.x.get((size_t)M * d * 4);
+    T* h = (T*)S.h.get((size_t)M * d * sizeof(T));
+    _Float16* q = (_Float16*)S.q.get((size_t)M * d * 2);
+    _Float16* k = (_Float16*)S.k.get((size_t)M * d * 2);
+    _Float16* vt = (_Float16*)S.vt.get((size_t)nb * H * 64 * Lp * 2, true);
+    T* o = (T*)S.o.get((size_t)M * d * sizeof(T));
+    T* ff = (T*)S.ff.get((size_t)M * 4 * d * sizeof(T));
+    T* enc = (T*)S.enc.get((size_t)M * d * sizeof(T));
+    launch_mel_window((const float*)S.mel.p, mel_clip_stride, ib, ib + 4096, ib + 2 * 4096,
+                      hp.n_mels, T2, cp, melT, nb, st);
+    EpiParams e;
+    // conv1 (k3 s1 p1) as a GEMM over overlapping rows of the padded window
+    e.bias = C.conv1_b;
+    e.c16 = h1p + d;
+    e.ldc = d;
+    e.c_bstride = (long)(T2 + 2) * d;
+    gemm<_Float16>(EPI_GELU, true, melT, cp, (long)(T2 + 2) * cp, C.conv1_w, 3 * cp, T2, d,
+                   3 * cp, nb, e, st);
+    // conv2 (k3 s2 p1) + GELU + positional embedding -> residual stream x
+    e = EpiParams();
+    e.bias = C.conv2_b;
+    e.c32 = x;
+    e.ldc = d;
+    e.c_bstride = (long)Lc * d;
+    e.pe = C.enc_pe;
+    gemm<_Float16>(EPI_CONV2, false, h1p, 2 * d, (long)(T2 + 2) * d, C.conv2_w, 3 * d, Lc, d,
+                   3 * d, nb, e, st);
+    const float kq_scale = 1.0f / sqrtf(64.0f);
+    for (int l = 0; l < L_enc; ++l) {
+      const EncLayerW& W = C.enc[l];
+      layer_norm<T>(x, W.ln1_w, W.ln1_b, h, M, d, nullptr, st);
+      e = EpiParams();
+      e.bias = W.qkv_b;
+      e.q = q;
+      e.k = k;
+      e.v = vt;
+      e.L = Lc;
+      e.H = H;
+      e.d = d;
+      e.ldv = Lp;  // V^T rows are padded to Lp (16-B aligned tile loads)
+      gemm<T>(EPI_ENC_QKV, false, h, d, 0, Wt(W.qkv_w), d, M, 3 * d, d, 1, e, st);
+      enc_attention<T>(q, k, vt, o, nb, H, Lc, kq_scale, st);
+      e = EpiParams();
+      e.bias = W.o_b;
+      e.c32 = x;
+      e.r32 = x;
+      e.ldc = d;
+      gemm<T>(EPI_RES, false, o, d, 0, Wt(W.o_w), d, M, d, d, 1, e, st);
+      layer_norm<T>(x, W.ln2_w, W.ln2_b, h, M, d, nullptr, st);
+      e = EpiParams();
+      e.bias = W.fc1_b;
+      e.c16 = ff;
+      e.ldc = 4 * d;
+      gemm<T>(EPI_GELU, false, h, d, 0, Wt(W.fc1_w), d, M, 4 * d, d, 1, e, st);
+      e = EpiParams();
+      e.bias = W.fc2_b;
+      e.c32 = x;
+      e.r32 = x;
+      e.ldc = d;
+      gemm<T>(EPI_RES, false, ff, 4 * d, 0, Wt(W.fc2_w), 4 * d, M, d, 4 * d, 1, e, st);
+    }
+    layer_norm<T>(x, C.enc_ln_w, C.enc_ln_b, enc, M, d, nullptr, st);
+    // cross K/V of every decoder layer in one GEMM
+    e = EpiParams();
+    e.bias = C.cross_b;
+    e.k = (_Float16*)S.cross_k.p;
+    e.v = (_Float16*)S.cross_v.p;
+    e.L = Lc;
+    e.H = H;
+    e.d = d;
+    e.ncap = S.cross_cap;
+    e.slot = ib + 3 * 4096;
+    e.kscale = powf(64.0f, -0.25f);
+    gemm<T>(EPI_CROSS_KV, false, enc, d, 0, Wt(C.cross_w), d, M, L_dec * 2 * d, d, 1, e, st);
+  }
+
+  void ensure_cross(int n_slots) {
+    const size_t per = (size_t)L_dec * hp.n_audio_ctx * d * 2;
+    if (S.cross_cap < n_slots) {
+      S.cross_k.release();
+      S.cross_v.release();
+      S.cross_k.get(per * n_slots);
+      S.cross_v.get(per * n_slots);
+      S.cross_cap = n_slots;
+    }
+  }
+
+  void ensure_rows(int R) {
+    if (S.row_cap < R) {
+      S.kself.release();
+      S.vself.release();
+      const size_t per = (size_t)L_dec * H * Tctx * 64 * 2;
+      S.kself.get(per * R);
+      S.vself.get(per * R);
+      S.row_cap = R;
+    }
+    S.xd.get((size_t)R * d * 4, true);
+    S.hd.get((size_t)R * d * sizeof(T), true);
+    S.qd.get((size_t)R * d * 2, true);
+    S.od.get((size_t)R * d * sizeof(T), true);
+    S.ffd.get((size_t)R * 4 * d * sizeof(T), true);
+    S.logits.get((size_t)R * V * 4);
+    S.stepin.get((size_t)R * 4 * 4);
+    S.ctl.get((size_t)R * sizeof(RowCtl));
+    S.tokout.get((size_t)R * sizeof(TokOut));
+  }
+
+  // one decoder step for R rows; inputs already in S.stepin / S.ctl
+  void decode_step(int R, bool want_probs) {
+    int* si = (int*)S.stepin.p;
+    const int* tok = si;
+    const int* pos = si + R;
+    const int* act = si + 2 * R;
+    const int* xidx = si + 3 * R;
+    float* xd = (float*)S.xd.p;
+    T* hd = (T*)S.hd.p;
+    _Float16* qd = (_Float16*)S.qd.p;
+    T* od = (T*)S.od.p;
+    T* ffd = (T*)S.ffd.p;
+    const float kqs = powf(64.0f, -0.25f);
+    embed<T>(Wt(C.tok_emb), C.dec_pe, tok, pos, act, xd, R, d, st);
+    const size_t layer_self = (size_t)S.row_cap * H * Tctx * 64;
+    const size_t layer_cross = (size_t)S.cross_cap * H * hp.n_audio_ctx * 64;
+    for (int l = 0; l < L_dec; ++l) {
+      const DecLayerW& W = C.dec[l];
+      _Float16* ks = (_Float16*)S.kself.p + l * layer_self;
+      _Float16* vs = (_Float16*)S.vself.p + l * layer_self;
+      layer_norm<T>(xd, W.ln1_w, W.ln1_b, hd, R, d, act, st);
+      EpiParams e;
+      e.bias = W.qkv_b;
+      e.q = qd;
+      e.k = ks;
+      e.v = vs;
+      e.L = Tctx;
+      e.H = H;
+      e.d = d;
+      e.pos = pos;
+      e.active = act;
+      e.qscale = kqs;
+      e.kscale = kqs;
+      gemm<T>(EPI_DEC_QKV, false, hd, d, 0, Wt(W.qkv_w), d, R, 3 * d, d, 1, e, st);
+      dec_attention<T>(qd, ks, vs, nullptr, pos, act, 0, Tctx, od, R, H, 1.0f, st);
+      e = EpiParams();
+      e.bias = W.o_b;
+      e.c32 = xd;
+      e.r32 = xd;
+      e.ldc = d;
+      gemm<T>(EPI_RES, false, od, d, 0, Wt(W.o_w), d, R, d, d, 1, e, st);
+      layer_norm<T>(xd, W.lnc_w, W.lnc_b, hd, R, d, act, st);
+      e = EpiParams();
+      e.bias = W.cq_b;
+      e.c16 = qd;
+      e.ldc = d;
+      gemm<T>(EPI_STORE16, false, hd, d, 0, Wt(W.cq_w), d, R, d, d, 1, e, st);
+      dec_attention<T>(qd, (_Float16*)S.cross_k.p + l * layer_cross,
+                       (_Float16*)S.cross_v.p + l * layer_cross, xidx, pos, act,
+                       hp.n_audio_ctx, hp.n_audio_ctx, od, R, H, kqs, st);
+      e = EpiParams();
+      e.bias = W.co_b;
+      e.c32 = xd;
+      e.r32 = xd;
+      e.ldc = d;
+      gemm<T>(EPI_RES, false, od, d, 0, Wt(W.co_w), d, R, d, d, 1, e, st);
+      layer_norm<T>(xd, W.ln2_w, W.ln2_b, hd, R, d, act, st);
+      e = EpiParams();
+      e.bias = W.fc1_b;
+      e.c16 = ffd;
+      e.ldc = 4 * d;
+      gemm<T>(EPI_GELU, false, hd, d, 0, Wt(W.fc1_w), d, R, 4 * d, d, 1, e, st);
+      e = EpiParams();
+      e.bias = W.fc2_b;
+      e.c32 = xd;
+      e.r32 = xd;
+      e.ldc = d;
+      gemm<T>(EPI_RES, false, ffd, 4 * d, 0, Wt(W.fc2_w), 4 * d, R, d, 4 * d, 1, e, st);
+    }
+    layer_norm<T>(xd, C.dec_ln_w, C.dec_ln_b, hd, R, d, act, st);
+    EpiParams e;
+    e.c32 = (float*)S.logits.p;
+    e.ldc = V;
+    gemm<T>(EPI_F32, false, hd, d, 0, Wt(C.tok_emb), d, R, V, d, 1, e, st);
+    float* pr = nullptr;
+    float* lp = nullptr;
+    if (want_probs) {
+      pr = (float*)S.probs.get((size_t)R * V * 4);
+      lp = (float*)S.logprobs.get((size_t)R * V * 4);
+    }
+    logits_process((float*)S.logits.p, (const float*)S.smask.p, (const RowCtl*)S.ctl.p,
+                   (TokOut*)S.tokout.p, pr, lp, LC, R, st);
+  }
+};
+
+}  // namespace mwx
+
+struct mwx_context {
+  mwx::Context c;
+};
+struct mwx_state {
+  mwx::State s;
+};
+
+// The decode-loop / window logic lives in driver.cpp (same TU via include to
+// keep templates local).
+#include "driver.inc"

@@ -1,0 +1,329 @@
+// Attention kernels for gfx950.
+//
+// enc_attn_kernel: encoder self-attention (whisper_build_graph_encoder,
+//   softmax(Q K^T / 8) V over 1500 frames). Flash-style: one workgroup = 4
+//   waves x 32 queries of one (clip, head); K and V^T tiles of 64 keys are
+//   register-prefetched and staged through double-buffered LDS (K rows XOR-
+//   swizzled, V^T rows padded to 144 B: conflict-free ds_read_b128 / _b64).
+//   S^T = K Q^T is computed with the key on the MFMA row, so every lane owns
+//   one query column: row max / row sum need two cross-lane shuffles, and the
+//   f16 P^T registers are directly the B operand of O^T = V^T P^T.
+//   Numerics: Q, K, V, P in f16 (ggml itype), f32 accumulation and softmax.
+//
+// dec_attn_kernel: one query per (row, head) against its KV rows — the
+//   decoder self-attention over the KV cache and the cross-attention over the
+//   1500 encoder frames (whisper_build_graph_decoder). Follows ggml's
+//   non-flash path exactly: f32 scores of f16 q.k, scale, max, exp, double
+//   sum, multiply by (float)(1/sum), round P to f16, then P.V in f32. K and V
+//   rows are streamed with 8 lanes per 128-B row (fully coalesced).
+#include "kcommon.h"
+#include "kernels.h"
+
+namespace mwx {
+
+constexpr int VSTR = 72;  // padded V^T tile row (elements)
+
+template <typename T>
+__global__ __launch_bounds__(256) void enc_attn_kernel(const _Float16* __restrict__ q,
+                                                       const _Float16* __restrict__ k,
+                                                       const _Float16* __restrict__ vt, T* __restrict__ o,
+                                                       int H, int L, int Lp, float scale_log2) {
+  __shared__ __attribute__((aligned(16))) _Float16 ks[2][64 * 64];
+  __shared__ __attribute__((aligned(16))) _Float16 vs[2][64 * VSTR];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int bh = blockIdx.y;
+  const int b = bh / H, h = bh - b * H;
+  const int q0 = blockIdx.x * 128 + wid * 32;
+  const _Float16* Q = q + (long)bh * L * 64;
+  const _Float16* Kh = k + (long)bh * L * 64;
+  const _Float16* VT = vt + (long)bh * 64 * Lp;
+
+  f16x8 qf[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int qr = min(q0 + u * 16 + c16, L - 1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      qf[u][s] = *reinterpret_cast<const f16x8*>(Q + (long)qr * 64 + s * 32 + g * 8);
+  }
+  f32x4 oacc[4][2];
+#pragma unroll
+  for (int te = 0; te < 4; ++te)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) oacc[te][u] = f32x4{0, 0, 0, 0};
+  float mrow[2] = {-INFINITY, -INFINITY}, lrow[2] = {0.0f, 0.0f};
+
+  uint4 rk[2], rv[2];
+  int kso[2], vso[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = tid + 256 * i;
+    const int row = c >> 3, ch = c & 7;
+    kso[i] = row * 64 + ((ch ^ (row & 7)) << 3);
+    vso[i] = row * VSTR + ch * 8;
+  }
+  auto gload = [&](int kb) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i;
+      const int row = c >> 3, ch = c & 7;
+      const int key = min(kb * 64 + row, L - 1);
+      rk[i] = *reinterpret_cast<const uint4*>(Kh + (long)key * 64 + ch * 8);
+      const int key0 = kb * 64 + ch * 8;
+      if (key0 < Lp)
+        rv[i] = *reinterpret_cast<const uint4*>(VT + (long)row * Lp + key0);
+      else
+        rv[i] = uint4{0, 0, 0, 0};
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      *reinterpret_cast<uint4*>(&ks[buf][kso[i]]) = rk[i];
+      *reinterpret_cast<uint4*>(&vs[buf][vso[i]]) = rv[i];
+    }
+  };
+
+  const int nkb = (L + 63) / 64;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int cur = kb & 1;
+    if (kb + 1 < nkb) gload(kb + 1);
+    // S^T = K Q^T : sacc[t][u] rows = keys 16t + 4g + r, col = query c16
+    f32x4 sacc[4][2];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int row = t * 16 + c16;
+      f16x8 kf[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int ch = s * 4 + g;
+        kf[s] = *reinterpret_cast<const f16x8*>(&ks[cur][row * 64 + ((ch ^ (row & 7)) << 3)]);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        f32x4 a = f32x4{0, 0, 0, 0};
+        a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[0], qf[u][0], a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[1], qf[u][1], a, 0, 0, 0);
+        sacc[t][u] = a;
+      }
+    }
+    // mask keys beyond L
+    if (kb * 64 + 64 > L) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kb * 64 + t * 16 + g * 4 + r;
+          if (key >= L) {
+            sacc[t][0][r] = -INFINITY;
+            sacc[t][1][r] = -INFINITY;
+          }
+        }
+    }
+    // online softmax per query column
+    f16x8 pf[2][2];  // [u][k-step]
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, sacc[t][u][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(mrow[u], mx * scale_log2);
+      const float alpha = exp2f(mrow[u] - mnew);
+      float ps[4][4];
+      float rs = 0.0f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = exp2f(sacc[t][u][r] * scale_log2 - mnew);
+          ps[t][r] = p;
+          rs += p;
+        }
+      rs += __shfl_xor(rs, 16, 64);
+      rs += __shfl_xor(rs, 32, 64);
+      lrow[u] = lrow[u] * alpha + rs;
+      mrow[u] = mnew;
+#pragma unroll
+      for (int te = 0; te < 4; ++te) oacc[te][u] *= alpha;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        f16x8 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = (_Float16)ps[2 * s2][r];
+          v[4 + r] = (_Float16)ps[2 * s2 + 1][r];
+        }
+        pf[u][s2] = v;
+      }
+    }
+    // O^T += V^T P^T
+#pragma unroll
+    for (int te = 0; te < 4; ++te) {
+      const int e = te * 16 + c16;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const _Float16* vp = &vs[cur][e * VSTR + s2 * 32 + g * 4];
+        const f16x4 lo = *reinterpret_cast<const f16x4*>(vp);
+        const f16x4 hi = *reinterpret_cast<const f16x4*>(vp + 16);
+        const f16x8 vf = f16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          oacc[te][u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pf[u][s2], oacc[te][u], 0, 0, 0);
+      }
+    }
+    if (kb + 1 < nkb) sstore(cur ^ 1);
+    __syncthreads();
+  }
+  const int D = H * 64;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int qi = q0 + u * 16 + c16;
+    if (qi >= L) continue;
+    const float inv = 1.0f / lrow[u];
+    T* dst = o + ((long)b * L + qi) * D + h * 64;
+#pragma unroll
+    for (int te = 0; te < 4; ++te)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dst[te * 16 + g * 4 + r] = to_t<T>(oacc[te][u][r] * inv);
+  }
+}
+
+template <typename T>
+void enc_attention(const _Float16* q, const _Float16* k, const _Float16* vt, T* o, int B, int H,
+                   int L, float scale, hipStream_t st) {
+  const int Lp = (L + 7) & ~7;
+  dim3 g((L + 127) / 128, B * H);
+  enc_attn_kernel<T><<<g, 256, 0, st>>>(q, k, vt, o, H, L, Lp, scale * 1.4426950408889634f);
+}
+
+// ---------------------------------------------------------------------------
+// decode attention
+// ---------------------------------------------------------------------------
+constexpr int DEC_MAX_KEYS = 1536;
+
+__device__ __forceinline__ float block_max_256(float v, float* red) {
+  v = wave_max(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+__device__ __forceinline__ double block_sum_256d(double v, double* red) {
+  v = wave_sum_d(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void dec_attn_kernel(
+    const _Float16* __restrict__ q, const _Float16* __restrict__ kbase,
+    const _Float16* __restrict__ vbase, const int* __restrict__ kv_index,
+    const int* __restrict__ pos, const int* __restrict__ active, int fixed_len, int cap,
+    T* __restrict__ o, int H, float scale) {
+  __shared__ float sc[DEC_MAX_KEYS];
+  __shared__ float redf[4];
+  __shared__ double redd[4];
+  __shared__ float pv[4][64][9];
+  const int row = blockIdx.y, h = blockIdx.x;
+  if (!active[row]) return;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int kg = lane >> 3, c = lane & 7;
+  const int n = fixed_len > 0 ? fixed_len : pos[row] + 1;
+  const int slot = kv_index ? kv_index[row] : row;
+  const _Float16* K = kbase + (((long)slot * H + h) * cap) * 64;
+  const _Float16* V = vbase + (((long)slot * H + h) * cap) * 64;
+  const int D = H * 64;
+  float qv[8];
+  {
+    const f16x8 qq = *reinterpret_cast<const f16x8*>(q + (long)row * D + h * 64 + c * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qv[j] = (float)qq[j];
+  }
+  // scores: 8 lanes per key row
+  for (int j0 = wid * 8; j0 < n; j0 += 32) {
+    const int j = j0 + kg;
+    float d = 0.0f;
+    if (j < n) {
+      const f16x8 kk = *reinterpret_cast<const f16x8*>(K + (long)j * 64 + c * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d += qv[e] * (float)kk[e];
+    }
+    d += __shfl_xor(d, 1, 64);
+    d += __shfl_xor(d, 2, 64);
+    d += __shfl_xor(d, 4, 64);
+    if (c == 0 && j < n) sc[j] = d * scale;
+  }
+  __syncthreads();
+  float mx = -INFINITY;
+  for (int j = tid; j < n; j += 256) mx = fmaxf(mx, sc[j]);
+  mx = block_max_256(mx, redf);
+  double sum = 0.0;
+  for (int j = tid; j < n; j += 256) {
+    const float e = expf(sc[j] - mx);
+    sc[j] = e;
+    sum += (double)e;
+  }
+  sum = block_sum_256d(sum, redd);
+  const float inv = (float)(1.0 / sum);
+  for (int j = tid; j < n; j += 256) sc[j] = (float)(_Float16)(sc[j] * inv);
+  __syncthreads();
+  float acc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0.0f;
+  for (int j = wid * 8 + kg; j < n; j += 32) {
+    const f16x8 vv = *reinterpret_cast<const f16x8*>(V + (long)j * 64 + c * 8);
+    const float p = sc[j];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += p * (float)vv[e];
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    acc[e] += __shfl_xor(acc[e], 8, 64);
+    acc[e] += __shfl_xor(acc[e], 16, 64);
+    acc[e] += __shfl_xor(acc[e], 32, 64);
+  }
+  if (kg == 0) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) pv[wid][c][e] = acc[e];
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const int cc = tid >> 3, e = tid & 7;
+    const float r = (pv[0][cc][e] + pv[1][cc][e]) + (pv[2][cc][e] + pv[3][cc][e]);
+    o[(long)row * D + h * 64 + cc * 8 + e] = to_t<T>(r);
+  }
+}
+
+template <typename T>
+void dec_attention(const _Float16* q, const _Float16* kbase, const _Float16* vbase,
+                   const int* kv_index, const int* pos, const int* active, int fixed_len,
+                   int kv_len_cap, T* o, int R, int H, float scale, hipStream_t st) {
+  dim3 g(H, R);
+  dec_attn_kernel<T><<<g, 256, 0, st>>>(q, kbase, vbase, kv_index, pos, active, fixed_len,
+                                        kv_len_cap, o, H, scale);
+}
+
+template void enc_attention<_Float16>(const _Float16*, const _Float16*, const _Float16*, _Float16*,
+                                      int, int, int, float, hipStream_t);
+template void enc_attention<__bf16>(const _Float16*, const _Float16*, const _Float16*, __bf16*, int,
+                                    int, int, float, hipStream_t);
+template void dec_attention<_Float16>(const _Float16*, const _Float16*, const _Float16*, const int*,
+                                      const int*, const int*, int, int, _Float16*, int, int, float,
+                                      hipStream_t);
+template void dec_attention<__bf16>(const _Float16*, const _Float16*, const _Float16*, const int*,
+                                    const int*, const int*, int, int, __bf16*, int, int, float,
+                                    hipStream_t);
+
+}  // namespace mwx

@@ -1,0 +1,74 @@
+// Device-side helpers shared by the gfx950 kernels of the mwx engine.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mwx {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+// Element type traits: T is _Float16 (ggml f16 files) or __bf16.
+template <typename T>
+struct Elt;
+template <>
+struct Elt<_Float16> {
+  using v8 = f16x8;
+  __device__ static inline f32x4 mfma(v8 a, v8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+};
+template <>
+struct Elt<__bf16> {
+  using v8 = bf16x8;
+  __device__ static inline f32x4 mfma(v8 a, v8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+};
+
+template <typename T>
+__device__ __forceinline__ T to_t(float x) {
+  return (T)x;  // v_cvt_f16_f32 / v_cvt_pk_bf16_f32: round to nearest even
+}
+template <typename T>
+__device__ __forceinline__ float to_f(T x) {
+  return (float)x;
+}
+
+// ggml GELU (tanh approximation) as evaluated by the ggml CPU backend with
+// GGML_GELU_FP16: the input is rounded to f16, the f32 formula is applied and
+// the result is rounded to f16 again (table lookup); saturates outside ±10.
+__device__ __forceinline__ float gelu_f32(float x) {
+  const float GELU_COEF_A = 0.044715f;
+  const float SQRT_2_OVER_PI = 0.79788456080286535587989211986876f;
+  return 0.5f * x * (1.0f + tanhf(SQRT_2_OVER_PI * x * (1.0f + GELU_COEF_A * x * x)));
+}
+__device__ __forceinline__ float gelu_ggml(float x) {
+  if (x <= -10.0f) return 0.0f;
+  if (x >= 10.0f) return x;
+  const float xh = (float)(_Float16)x;
+  return (float)(_Float16)gelu_f32(xh);
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+}  // namespace mwx

@@ -1,0 +1,116 @@
+// Host-visible launcher declarations for the gfx950 kernels of the mwx engine.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mwx {
+
+// GEMM epilogues. Every GEMM computes acc[m][n] = sum_k A[m][k] * W[n][k]
+// (W stored [N][K] as in ggml), accumulating in f32 on MFMA, and then applies
+// exactly the ops ggml applies after the matmul, at the same rounding points.
+enum Epi : int {
+  EPI_ENC_QKV = 0,  // encoder Q/K/V (+bias) -> f16 head-major Q, K and V^T
+  EPI_GELU = 1,     // out_T = gelu_ggml(acc + bias)       (FFN1, conv1)
+  EPI_RES = 2,      // out32 = (acc + bias) + res32         (out-proj, FFN2)
+  EPI_CONV2 = 3,    // out32 = pe + gelu_ggml(acc + bias)   (conv2 + pos emb)
+  EPI_F32 = 4,      // out32 = acc                          (logits)
+  EPI_CROSS_KV = 5, // cross K = f16(acc*kscale), V = f16(acc + b), all layers
+  EPI_DEC_QKV = 6,  // decoder Q (scaled) -> f16, K/V -> self KV cache at pos
+  EPI_STORE16 = 7,  // out16 = f16(acc + bias)              (cross-attn Q)
+};
+
+struct EpiParams {
+  const float* bias = nullptr;
+  float* c32 = nullptr;
+  void* c16 = nullptr;
+  long ldc = 0;
+  long c_bstride = 0;  // per grid.z batch stride of the output (elements)
+  const float* r32 = nullptr;
+  const float* pe = nullptr;
+  _Float16* q = nullptr;
+  _Float16* k = nullptr;
+  _Float16* v = nullptr;
+  int L = 0;     // sequence length (encoder / cross) or text ctx (decoder cache)
+  int H = 0;     // heads
+  int d = 0;     // model width
+  int ncap = 0;  // slots in the cross / self cache
+  int ldv = 0;   // encoder V^T row stride (padded L)
+  const int* pos = nullptr;     // decoder: position per row
+  const int* active = nullptr;  // decoder: row active flag
+  const int* slot = nullptr;    // cross: cache slot per encoder batch index
+  float kscale = 1.0f;
+  float qscale = 1.0f;
+};
+
+// T = _Float16 or __bf16 (model weight type). `OutT16` selects the 16-bit
+// output type of EPI_GELU (f16 for conv1, T for FFN1).
+template <typename T>
+void gemm(int epi, bool out_f16, const T* A, long lda, long a_bstride, const T* W, long ldw,
+          int M, int N, int K, int batch, const EpiParams& P, hipStream_t st);
+
+void launch_mel(const float* pcm, int n, int n_len, int n_fft_frames, const float* filters,
+                int n_mels, const float* tables, float* out, hipStream_t st);
+void launch_mel_norm(float* mel, long clip_stride, long count, int n_clips, float* mx,
+                     hipStream_t st);
+void launch_mel_window(const float* mel, long mel_clip_stride, const int* clip_of_slot,
+                       const int* seek_of_slot, const int* n_len_of_slot, int n_mels, int T,
+                       int cpad, _Float16* melT, int n_slots, hipStream_t st);
+void launch_signal_energy(const float* x, int n, float* out, hipStream_t st);
+
+template <typename T>
+void layer_norm(const float* x, const float* w, const float* b, T* y, int M, int N,
+                const int* active, hipStream_t st);
+template <typename T>
+void embed(const T* te, const float* pe, const int* tok, const int* pos, const int* active,
+           float* x, int R, int d, hipStream_t st);
+
+// encoder self-attention: q,k [B][H][L][64], vt [B][H][64][L] f16 -> o [B*L][H*64] (T)
+template <typename T>
+void enc_attention(const _Float16* q, const _Float16* k, const _Float16* vt, T* o, int B,
+                   int H, int L, float scale, hipStream_t st);
+
+// decode attention for R rows: q [R][H*64] f16; K/V rows [n_keys][64] per
+// (row, head). self: K = kbase + ((row*H + h)*kstride_rows)*64, n_keys =
+// pos[row] + 1. cross: K = kbase + ((clip[row]*H + h)*L)*64, n_keys = L.
+template <typename T>
+void dec_attention(const _Float16* q, const _Float16* kbase, const _Float16* vbase,
+                   const int* kv_index, const int* pos, const int* active, int fixed_len,
+                   int kv_len_cap, T* o, int R, int H, float scale, hipStream_t st);
+
+struct RowCtl {
+  int active;        // row participates in this step
+  int sample;        // logits of this step are processed (last prompt token or generated)
+  int is_initial;    // no tokens generated yet
+  int last_ts;       // last generated token is a timestamp
+  int penult_ts;     // penultimate generated token is a timestamp (or < 2 tokens)
+  int has_ts;        // decoder.has_ts
+  int seek_delta;    // decoder.seek_delta
+  int want_probs;    // write probs/logprobs rows (sampling path)
+  float temperature; // > 0: logits /= temperature
+  int want_nosp;     // compute no_speech probability from the raw logits
+  int pad[2];
+};
+struct TokOut {
+  int id;
+  int tid;
+  float p;
+  float plog;
+  float pt;
+  float ptsum;
+  float nosp;
+  int pad;
+};
+struct LogitsConst {
+  int n_vocab;
+  int eot;
+  int beg;
+  int space_id;       // token id of " " (suppress_blank)
+  int suppress_blank;
+  int max_initial_tid;  // timestamps > beg + tid0 suppressed at the first step (-1: off)
+  int nosp_id;
+};
+void logits_process(float* logits, const float* static_mask, const RowCtl* ctl, TokOut* out,
+                    float* probs, float* logprobs, const LogitsConst& C, int R, hipStream_t st);
+
+}  // namespace mwx

@@ -1,0 +1,346 @@
+"""ctypes binding of the mwx C ABI (include/mwx.h, include/mwx_test.h).
+
+Mirrors the whisper.h subset the reference service binds in
+src/stt_engine.cpp (context / state lifecycle, whisper_full_with_state, segment
+and token getters) plus the batched entry point mwx_full_batch. Used by the
+tests and by bench.py; the service itself binds the same ABI from C++
+(see INTEGRATION.md).
+
+The library is loaded from this directory (built in-tree by
+__graft_entry__.build()); a missing library raises immediately — there is no
+CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmwx.so")
+
+GGML_F16 = 1
+GGML_BF16 = 30
+SAMPLING_GREEDY = 0
+SAMPLING_BEAM_SEARCH = 1
+
+
+class ContextParams(C.Structure):
+    _fields_ = [("use_gpu", C.c_bool), ("flash_attn", C.c_bool), ("gpu_device", C.c_int)]
+
+
+class TokenData(C.Structure):
+    _fields_ = [
+        ("id", C.c_int32), ("tid", C.c_int32), ("p", C.c_float), ("plog", C.c_float),
+        ("pt", C.c_float), ("ptsum", C.c_float), ("t0", C.c_int64), ("t1", C.c_int64),
+        ("t_dtw", C.c_int64), ("vlen", C.c_float),
+    ]
+
+
+class _Greedy(C.Structure):
+    _fields_ = [("best_of", C.c_int)]
+
+
+class _Beam(C.Structure):
+    _fields_ = [("beam_size", C.c_int), ("patience", C.c_float)]
+
+
+ABORT_CB = C.CFUNCTYPE(C.c_bool, C.c_void_p)
+
+
+class FullParams(C.Structure):
+    _fields_ = [
+        ("strategy", C.c_int), ("n_threads", C.c_int), ("n_max_text_ctx", C.c_int),
+        ("offset_ms", C.c_int), ("duration_ms", C.c_int),
+        ("translate", C.c_bool), ("no_context", C.c_bool), ("no_timestamps", C.c_bool),
+        ("single_segment", C.c_bool), ("print_special", C.c_bool), ("print_progress", C.c_bool),
+        ("print_realtime", C.c_bool), ("print_timestamps", C.c_bool),
+        ("token_timestamps", C.c_bool), ("thold_pt", C.c_float), ("thold_ptsum", C.c_float),
+        ("max_len", C.c_int), ("split_on_word", C.c_bool), ("max_tokens", C.c_int),
+        ("audio_ctx", C.c_int), ("tdrz_enable", C.c_bool),
+        ("initial_prompt", C.c_char_p), ("prompt_tokens", C.POINTER(C.c_int32)),
+        ("prompt_n_tokens", C.c_int),
+        ("language", C.c_char_p), ("detect_language", C.c_bool),
+        ("suppress_blank", C.c_bool), ("suppress_nst", C.c_bool),
+        ("temperature", C.c_float), ("max_initial_ts", C.c_float), ("length_penalty", C.c_float),
+        ("temperature_inc", C.c_float), ("entropy_thold", C.c_float),
+        ("logprob_thold", C.c_float), ("no_speech_thold", C.c_float),
+        ("greedy", _Greedy), ("beam_search", _Beam),
+        ("abort_callback", ABORT_CB), ("abort_callback_user_data", C.c_void_p),
+        ("bench_fixed_steps", C.c_int),
+    ]
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Loads libmwx.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"mwx: {LIB_PATH} not built (run __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    P = C.c_void_p
+    L.mwx_context_default_params.restype = ContextParams
+    L.mwx_init_from_file_with_params.restype = P
+    L.mwx_init_from_file_with_params.argtypes = [C.c_char_p, ContextParams]
+    L.mwx_init_state.restype = P
+    L.mwx_init_state.argtypes = [P]
+    L.mwx_free_state.argtypes = [P]
+    L.mwx_free.argtypes = [P]
+    L.mwx_full_default_params.restype = FullParams
+    L.mwx_full_default_params.argtypes = [C.c_int]
+    L.mwx_full_with_state.restype = C.c_int
+    L.mwx_full_with_state.argtypes = [P, P, FullParams, C.POINTER(C.c_float), C.c_int]
+    L.mwx_full_batch.restype = C.c_int
+    L.mwx_full_batch.argtypes = [P, C.POINTER(P), FullParams, C.POINTER(C.POINTER(C.c_float)),
+                                 C.POINTER(C.c_int), C.c_int]
+    L.mwx_full_n_segments_from_state.restype = C.c_int
+    L.mwx_full_n_segments_from_state.argtypes = [P]
+    L.mwx_full_get_segment_text_from_state.restype = C.c_char_p
+    L.mwx_full_get_segment_text_from_state.argtypes = [P, C.c_int]
+    for n in ("t0", "t1"):
+        f = getattr(L, f"mwx_full_get_segment_{n}_from_state")
+        f.restype = C.c_int64
+        f.argtypes = [P, C.c_int]
+    L.mwx_full_get_segment_speaker_turn_next_from_state.restype = C.c_bool
+    L.mwx_full_get_segment_speaker_turn_next_from_state.argtypes = [P, C.c_int]
+    L.mwx_full_get_segment_no_speech_prob_from_state.restype = C.c_float
+    L.mwx_full_get_segment_no_speech_prob_from_state.argtypes = [P, C.c_int]
+    L.mwx_full_n_tokens_from_state.restype = C.c_int
+    L.mwx_full_n_tokens_from_state.argtypes = [P, C.c_int]
+    L.mwx_full_get_token_data_from_state.restype = TokenData
+    L.mwx_full_get_token_data_from_state.argtypes = [P, C.c_int, C.c_int]
+    L.mwx_full_lang_id_from_state.restype = C.c_int
+    L.mwx_full_lang_id_from_state.argtypes = [P]
+    L.mwx_token_to_str.restype = C.c_char_p
+    L.mwx_token_to_str.argtypes = [P, C.c_int32]
+    for n in ("eot", "sot", "beg", "not", "nosp", "transcribe", "translate"):
+        f = getattr(L, f"mwx_token_{n}")
+        f.restype = C.c_int32
+        f.argtypes = [P]
+    for n in ("n_vocab", "n_text_ctx", "n_audio_ctx", "n_mels", "is_multilingual", "model_wtype"):
+        f = getattr(L, f"mwx_{n}")
+        f.restype = C.c_int
+        f.argtypes = [P]
+    L.mwx_write_synthetic_model.restype = C.c_int
+    L.mwx_write_synthetic_model.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_uint64]
+    L.mwx_tokenize.restype = C.c_int
+    L.mwx_tokenize.argtypes = [P, C.c_char_p, C.POINTER(C.c_int32), C.c_int]
+    L.mwx_test_mel.restype = C.c_int
+    L.mwx_test_mel.argtypes = [P, P, C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_float), C.c_long]
+    L.mwx_test_encode.restype = C.c_int
+    L.mwx_test_encode.argtypes = [P, P, C.POINTER(C.c_float), C.c_int, C.c_int,
+                                  C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float)]
+    L.mwx_test_decode.restype = C.c_int
+    L.mwx_test_decode.argtypes = [P, P, C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_float)]
+    _lib = L
+    return L
+
+
+def fptr(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def write_synthetic_model(path: str, arch: str, wtype: int = GGML_F16, seed: int = 0) -> None:
+    rc = lib().mwx_write_synthetic_model(path.encode(), arch.encode(), wtype, seed)
+    if rc != 0:
+        raise RuntimeError(f"mwx_write_synthetic_model failed ({rc})")
+
+
+def synth_pcm16(k: int, n: int = 480000, sr: int = 16000) -> np.ndarray:
+    """Deterministic synthetic speech-like clip: 3 harmonic
+    voices (F0 90-260 Hz, 8 harmonics with 1/h amplitude), 2-6 Hz amplitude
+    modulation, white noise at -30 dBFS, peak 0.5, int16."""
+    rng = np.random.default_rng(0x5EED0000 + k)
+    t = np.arange(n, dtype=np.float64) / sr
+    sig = np.zeros(n)
+    for _ in range(3):
+        f0 = rng.uniform(90.0, 260.0)
+        rate = rng.uniform(2.0, 6.0)
+        ph = rng.uniform(0, 2 * np.pi, size=9)
+        voice = sum(np.sin(2 * np.pi * h * f0 * t + ph[h]) / h for h in range(1, 9))
+        env = 0.5 * (1.0 + np.sin(2 * np.pi * rate * t + ph[0]))
+        sig += env * voice
+    sig /= np.max(np.abs(sig))
+    sig += rng.normal(0.0, 10 ** (-30 / 20), size=n)
+    sig *= 0.5 / np.max(np.abs(sig))
+    return np.round(sig * 32767).astype(np.int16)
+
+
+def pcm16_to_f32(pcm16: np.ndarray) -> np.ndarray:
+    """SttEngine::transcribe_pcm16 conversion (src/stt_engine.cpp:123)."""
+    return (pcm16.astype(np.float32) / np.float32(32768.0)).astype(np.float32)
+
+
+@dataclass
+class Token:
+    id: int
+    tid: int
+    p: float
+    plog: float
+    pt: float
+    ptsum: float
+    t0: int
+    t1: int
+    text: str
+
+
+@dataclass
+class Segment:
+    t0: int
+    t1: int
+    text: str
+    no_speech_prob: float
+    speaker_turn_next: bool
+    tokens: List[Token] = field(default_factory=list)
+
+
+class Context:
+    """mwx_context + a pool of mwx_state objects."""
+
+    def __init__(self, model_path: str, device: int = 0):
+        L = lib()
+        cp = L.mwx_context_default_params()
+        cp.gpu_device = device
+        self.ctx = L.mwx_init_from_file_with_params(model_path.encode(), cp)
+        if not self.ctx:
+            raise RuntimeError(f"mwx_init_from_file_with_params failed for {model_path}")
+        self.states: List[int] = []
+
+    def close(self):
+        L = lib()
+        for s in self.states:
+            L.mwx_free_state(s)
+        self.states = []
+        if self.ctx:
+            L.mwx_free(self.ctx)
+            self.ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def state(self, i: int = 0) -> int:
+        while len(self.states) <= i:
+            s = lib().mwx_init_state(self.ctx)
+            if not s:
+                raise RuntimeError("mwx_init_state failed")
+            self.states.append(s)
+        return self.states[i]
+
+    @staticmethod
+    def default_params(strategy: int = SAMPLING_GREEDY) -> FullParams:
+        return lib().mwx_full_default_params(strategy)
+
+    def full(self, pcm: np.ndarray, params: FullParams, state_index: int = 0) -> int:
+        pcm = np.ascontiguousarray(pcm, dtype=np.float32)
+        return lib().mwx_full_with_state(self.ctx, self.state(state_index), params, fptr(pcm),
+                                         len(pcm))
+
+    def full_batch(self, pcms: Sequence[np.ndarray], params: FullParams) -> int:
+        n = len(pcms)
+        arrs = [np.ascontiguousarray(p, dtype=np.float32) for p in pcms]
+        states = (C.c_void_p * n)(*[self.state(i) for i in range(n)])
+        ptrs = (C.POINTER(C.c_float) * n)(*[fptr(a) for a in arrs])
+        lens = (C.c_int * n)(*[len(a) for a in arrs])
+        self._keep = arrs
+        return lib().mwx_full_batch(self.ctx, states, params, ptrs, lens, n)
+
+    def segments(self, state_index: int = 0) -> List[Segment]:
+        L = lib()
+        s = self.state(state_index)
+        out = []
+        for i in range(L.mwx_full_n_segments_from_state(s)):
+            seg = Segment(
+                t0=L.mwx_full_get_segment_t0_from_state(s, i),
+                t1=L.mwx_full_get_segment_t1_from_state(s, i),
+                text=L.mwx_full_get_segment_text_from_state(s, i).decode("utf-8", "replace"),
+                no_speech_prob=L.mwx_full_get_segment_no_speech_prob_from_state(s, i),
+                speaker_turn_next=L.mwx_full_get_segment_speaker_turn_next_from_state(s, i),
+            )
+            for j in range(L.mwx_full_n_tokens_from_state(s, i)):
+                td = L.mwx_full_get_token_data_from_state(s, i, j)
+                seg.tokens.append(Token(td.id, td.tid, td.p, td.plog, td.pt, td.ptsum, td.t0,
+                                        td.t1, L.mwx_token_to_str(self.ctx, td.id).decode(
+                                            "utf-8", "replace")))
+            out.append(seg)
+        return out
+
+    def lang_id(self, state_index: int = 0) -> int:
+        return lib().mwx_full_lang_id_from_state(self.state(state_index))
+
+    # ---- per-stage test entry points ----
+    def hparam(self, name: str) -> int:
+        return getattr(lib(), f"mwx_{name}")(self.ctx)
+
+    def test_mel(self, pcm: np.ndarray) -> np.ndarray:
+        pcm = np.ascontiguousarray(pcm, dtype=np.float32)
+        n_mels = self.hparam("n_mels")
+        n_len = (len(pcm) + 480000) // 160
+        out = np.empty((n_mels, n_len), dtype=np.float32)
+        r = lib().mwx_test_mel(self.ctx, self.state(), fptr(pcm), len(pcm), fptr(out), out.size)
+        if r != n_len:
+            raise RuntimeError(f"mwx_test_mel returned {r}")
+        return out
+
+    def test_encode(self, pcm: np.ndarray, seek: int = 0, cross: bool = True):
+        pcm = np.ascontiguousarray(pcm, dtype=np.float32)
+        L_a = self.hparam("n_audio_ctx")
+        d = self.d
+        nl = self.n_text_layer
+        enc = np.empty((L_a, d), dtype=np.float32)
+        k = np.empty((nl, L_a, d), dtype=np.float32) if cross else None
+        v = np.empty((nl, L_a, d), dtype=np.float32) if cross else None
+        null = C.POINTER(C.c_float)()
+        r = lib().mwx_test_encode(self.ctx, self.state(), fptr(pcm), len(pcm), seek, fptr(enc),
+                                  fptr(k) if cross else null, fptr(v) if cross else null)
+        if r != 0:
+            raise RuntimeError(f"mwx_test_encode returned {r}")
+        return enc, k, v
+
+    def test_decode(self, tokens: Sequence[int]) -> np.ndarray:
+        toks = np.ascontiguousarray(tokens, dtype=np.int32)
+        V = self.hparam("n_vocab")
+        out = np.empty((len(toks), V), dtype=np.float32)
+        r = lib().mwx_test_decode(self.ctx, self.state(), toks.ctypes.data_as(C.POINTER(C.c_int)),
+                                  len(toks), fptr(out))
+        if r != 0:
+            raise RuntimeError(f"mwx_test_decode returned {r}")
+        return out
+
+    @property
+    def d(self) -> int:
+        return self._hp_from_file()[2]
+
+    @property
+    def n_text_layer(self) -> int:
+        return self._hp_from_file()[8]
+
+    def _hp_from_file(self):
+        if not hasattr(self, "_hp"):
+            raise RuntimeError("hparams unknown: use Context.open()")
+        return self._hp
+
+    @classmethod
+    def open(cls, model_path: str, device: int = 0) -> "Context":
+        c = cls(model_path, device)
+        c._hp = read_hparams(model_path)
+        return c
+
+
+def read_hparams(path: str) -> List[int]:
+    with open(path, "rb") as f:
+        b = f.read(48)
+    return list(np.frombuffer(b[4:48], dtype=np.int32))
+
+
+def token_ids(segs: List[Segment]) -> List[int]:
+    return [t.id for s in segs for t in s.tokens]
