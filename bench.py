@@ -1,0 +1,274 @@
+#!/usr/bin/env python3
+"""bench.py — throughput of the MI355X Whisper hot path (BASELINE.json metric).
+
+One step = one mwx_full_batch pass over a batch of synthetic 30-s clips per GPU
+(device log-mel -> conv stem -> 32-layer encoder -> cross K/V -> KV-cached greedy
+decode with on-device logits processing -> segments) followed by the RCCL gather
+of every rank's token streams to rank 0. Workload (configs[2] of BASELINE.json):
+Whisper-large-v3 shapes, bf16 weights (synthetic, seeded), 32 clips x 30 s per
+GPU, decode length fixed at the upstream cap of 220 steps per clip (EOT and
+timestamps suppressed via bench_fixed_steps so every clip costs the same).
+
+Multi-GPU: launched with torch.distributed.run, one process per GPU; clips are
+sharded (weak scaling, 32 per GPU); RCCL is used only for the final token-stream
+gather. value = audio seconds processed by all ranks / max-over-ranks time.
+
+Also reported: a roofline object for the dominant kernel (HIP events recorded
+by the engine on its own stream during the timed region) and a CPU baseline
+(the oracle — a CPU restatement of the reference path — timed on a bounded
+sample on this host).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "sentiric-stt-whisper-service_amd"))
+
+METRIC = "audio-sec/s/GPU + RTF, Whisper-large-v3 30s chunks at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+MFMA_PEAK_TFLOPS = 2500.0  # dense bf16/f16 MFMA (spec)
+
+ARCH = {  # n_mels, d, heads, enc layers, dec layers, vocab
+    "large-v3": (128, 1280, 20, 32, 32, 51866),
+    "medium": (80, 1024, 16, 24, 24, 51865),
+    "base": (80, 512, 8, 6, 6, 51865),
+    "tiny.en": (80, 384, 6, 4, 4, 51864),
+    "micro": (80, 128, 2, 2, 3, 51864),
+}
+
+
+def kernel_model(arch, kclass, clips, rows, launches, prompt_len, steps):
+    """Algorithmic work of one launch of `kclass`, averaged over the launches of
+    one step: (bound, per-launch bytes or flops, description)."""
+    n_mels, d, H, Le, Ld, V = ARCH[arch]
+    L, T = 1500, 3000
+    if kclass == "dec_attn_cross":
+        # every active row reads its clip's cross K and V for one layer (f16)
+        b = rows * (L * d * 2 * 2 + d * 2 * 2)
+        return "hbm", b, f"{rows} rows x (K+V 1500x{d} f16 + q/o) per launch"
+    if kclass == "enc_gemm":
+        conv = 2 * T * d * 3 * n_mels + 2 * L * d * 3 * d
+        layer = 2 * L * d * (3 * d + d + 4 * d + 4 * d)
+        flops = clips * (conv + Le * layer)
+        return "mfma", flops / max(1, launches), "conv1/conv2/QKV/out/FC1/FC2 FLOPs per launch"
+    if kclass == "cross_gemm":
+        return "mfma", 2 * clips * L * d * 2 * d * Ld, "all-layer cross K/V GEMM"
+    if kclass == "enc_attn":
+        return "mfma", clips * H * 4 * L * L * 64, "QK^T + PV FLOPs per layer launch"
+    if kclass == "dec_gemm":
+        w = Ld * 2 * (3 * d * d + d * d + d * d + d * d + 8 * d * d)
+        return "hbm", w * (prompt_len + steps) / max(1, launches), "decoder weight bytes per launch"
+    if kclass == "logits_gemm":
+        return "hbm", V * d * 2 + rows * V * 4, "tied embedding bf16 + f32 logits"
+    raise ValueError(kclass)
+
+
+def cpu_baseline(model_path, arch, threads, prompt_len, steps):
+    """Times the oracle (CPU restatement of the reference path, scalar C++ +
+    OpenMP) on a bounded sample of ONE clip: full log-mel, conv stem + 1 of the
+    encoder layers, 1 of the cross K/V layers and 4 decode steps; the per-clip
+    time is extrapolated to all layers and prompt + 220 steps."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import mwx
+    import orc
+    L = orc.lib()
+    o = orc.Oracle(model_path, threads=threads)
+    n_mels, d, H, Le, Ld, V = ARCH[arch]
+    pcm = mwx.pcm16_to_f32(mwx.synth_pcm16(0))
+    t0 = time.perf_counter()
+    mel, _ = o.mel(pcm)
+    t_mel = time.perf_counter() - t0
+    L.orc_set_enc_layer_limit(0)
+    t0 = time.perf_counter()
+    o.encode(mel)
+    t_conv = time.perf_counter() - t0
+    L.orc_set_enc_layer_limit(1)
+    t0 = time.perf_counter()
+    enc = o.encode(mel)
+    t_layer = time.perf_counter() - t0 - t_conv
+    L.orc_set_enc_layer_limit(-1)
+    # cross K/V and decode against random-free stand-in: reuse one layer's cost
+    k = np.zeros((Ld, 1500, d), np.float32)
+    t0 = time.perf_counter()
+    o.decode_seq(k, k, [o.sot, 300, 301, 302])
+    t_dec = (time.perf_counter() - t0) / 4
+    # one cross layer = 2 GEMMs [1500 x d] x [d x d]: 1/4 of an encoder layer's
+    # QKV+out GEMM work -> scale the measured layer by its FLOP share
+    layer_flops = 2 * 1500 * d * 12 * d + 4 * 1500 * 1500 * d
+    t_cross = t_layer * (2 * 1500 * d * 2 * d * Ld) / layer_flops
+    t_clip = t_mel + t_conv + Le * t_layer + t_cross + (prompt_len + steps) * t_dec
+    o.close()
+    sampled = t_mel + t_conv + t_layer + 4 * t_dec
+    return {
+        "value": round(30.0 / t_clip, 4),
+        "unit": "audio-sec/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"1 clip of 30 s, {arch}: full log-mel + conv + 1/{Le} encoder layers + "
+                   f"4 decode steps measured ({sampled:.1f} s), extrapolated to {Le} layers, "
+                   f"cross K/V and {prompt_len + steps} decode steps: {t_clip:.1f} s/clip"),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--arch", default="large-v3")
+    ap.add_argument("--wtype", default="bf16", choices=["bf16", "f16"])
+    ap.add_argument("--clips", type=int, default=32, help="30-s clips per GPU")
+    ap.add_argument("--decode-steps", type=int, default=220)
+    ap.add_argument("--perf-class", default="dec_attn_cross")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    import mwx
+    wt = mwx.GGML_BF16 if args.wtype == "bf16" else mwx.GGML_F16
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"mwx_bench_{args.arch}_{args.wtype}.bin")
+    if local == 0 and not os.path.exists(path):
+        tmp = path + f".tmp{os.getpid()}"
+        mwx.write_synthetic_model(tmp, args.arch, wt, 0)
+        os.replace(tmp, path)
+    barrier()
+    ctx = mwx.Context.open(path, device=local)
+    pcms = [mwx.pcm16_to_f32(mwx.synth_pcm16(rank * args.clips + k)) for k in range(args.clips)]
+    p = ctx.default_params(mwx.SAMPLING_GREEDY)
+    p.language = b"en"
+    p.temperature = 0.0
+    p.temperature_inc = 0.0
+    p.token_timestamps = False
+    p.suppress_nst = True
+    p.bench_fixed_steps = args.decode_steps
+    prompt_len = 3 if ARCH[args.arch][5] >= 51865 else 1
+    max_tok = args.decode_steps
+    gathered = {}
+
+    def step():
+        rc = ctx.full_batch(pcms, p)
+        if rc != 0:
+            raise RuntimeError(f"mwx_full_batch rc={rc}")
+        toks = np.zeros((args.clips, max_tok), np.int32)
+        for c in range(args.clips):
+            ids = mwx.token_ids(ctx.segments(c))[:max_tok]
+            toks[c, :len(ids)] = ids
+        t = torch.from_numpy(toks).cuda()
+        if dist is not None:
+            out = torch.empty((world * args.clips, max_tok), dtype=torch.int32, device=t.device)
+            dist.all_gather_into_tensor(out, t)  # RCCL over xGMI: token streams to rank 0
+            if rank == 0:
+                gathered["tokens"] = out.cpu().numpy()
+        else:
+            gathered["tokens"] = t.cpu().numpy()
+
+    for _ in range(args.warmup):
+        step()
+    L = mwx.lib()
+    st0 = ctx.state(0)  # workspace / stream owner of the batch
+    L.mwx_perf_read(st0, None, None)
+    L.mwx_perf_enable(st0, args.perf_class.encode())
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    import ctypes
+    tot_ms = ctypes.c_double()
+    nl = ctypes.c_int()
+    L.mwx_perf_read(st0, ctypes.byref(tot_ms), ctypes.byref(nl))
+    L.mwx_perf_enable(st0, None)
+    if dist is not None:
+        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    audio_s = world * args.clips * 30.0 * args.steps
+    value = audio_s / elapsed
+    if rank == 0:
+        launches = max(1, nl.value)
+        avg_s = tot_ms.value / 1e3 / launches
+        bound, work, desc = kernel_model(args.arch, args.perf_class, args.clips, args.clips,
+                                         launches // max(1, args.steps), prompt_len,
+                                         args.decode_steps)
+        traffic = None
+        tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(tf):
+            try:
+                traffic = json.load(open(tf)).get(f"{args.arch}:{args.perf_class}:{args.clips}")
+            except Exception:
+                traffic = None
+        if bound == "hbm":
+            achieved = work / avg_s / 1e9
+            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": traffic}
+        else:
+            achieved = work / avg_s / 1e12
+            roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": MFMA_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(achieved / MFMA_PEAK_TFLOPS, 4),
+                    "traffic": traffic}
+        roof.update({"kernel": args.perf_class, "avg_launch_us": round(avg_s * 1e6, 2),
+                     "launches": nl.value, "work_per_launch": work, "work_desc": desc})
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
+            try:
+                cpu = cpu_baseline(path, args.arch, threads, prompt_len, args.decode_steps)
+            except Exception as ex:  # reported, never fatal to the GPU number
+                cpu = {"error": str(ex)}
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "audio-sec/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.wtype,
+            "data": "synthetic (seeded 30-s 16 kHz PCM16 clips; seeded weights in the ggml .bin layout)",
+            "config": {
+                "workload": (f"whisper-{args.arch} {args.wtype}: {args.clips} x 30 s clips per GPU, "
+                             f"mel + encoder + cross-KV + {args.decode_steps} greedy KV-cached "
+                             f"decode steps per clip, RCCL token gather to rank 0"),
+                "global_batch": world * args.clips,
+                "seq_len": 1500,
+                "parallelism": f"dp{world}",
+            },
+            "audio_sec_per_s_per_gpu": round(value / world, 2),
+            "rtf": round(elapsed / audio_s * world, 6),
+            "x_realtime_per_gpu": round(value / world, 1),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -221,6 +221,16 @@ int mwx_tokenize(struct mwx_context* ctx, const char* text, mwx_token* tokens,
 
 void mwx_log_set(mwx_log_callback log_callback, void* user_data);
 
+/* --- measurement ------------------------------------------------------------
+ * Times every launch of one kernel class with a pair of HIP events recorded on
+ * the state's stream (the stream the kernels run on). Classes: "mel",
+ * "enc_gemm", "enc_attn", "cross_gemm", "dec_gemm", "dec_attn_self",
+ * "dec_attn_cross", "logits_gemm", "logits_proc". NULL disables.
+ * mwx_perf_read synchronizes, returns the summed milliseconds and the launch
+ * count since the last read, and resets them. */
+void mwx_perf_enable(struct mwx_state* state, const char* kernel_class);
+int mwx_perf_read(struct mwx_state* state, double* total_ms, int* launches);
+
 /* --- model tooling --------------------------------------------------------
  * Writes a model in the ggml .bin layout read by whisper.cpp and by
  * mwx_init_from_file_with_params: magic, 11 hparams, mel filterbank, vocab,

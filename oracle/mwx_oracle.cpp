@@ -549,6 +549,10 @@ static void attention(const Model& m, const float* Q, const float* K, const floa
   }
 }
 
+// Encoder layer cap used only by the bounded CPU-baseline sample (bench.py):
+// < 0 runs all layers.
+static int g_enc_layer_limit = -1;
+
 // Encodes the 2*n_ctx mel frames starting at `seek`; out = embd_enc [n_ctx][D].
 static void encode(const Model& m, const Mel& mel, int seek, std::vector<float>& out) {
   const int n_ctx = m.n_audio_ctx, D = m.n_audio_state, H = m.n_audio_head;
@@ -573,7 +577,9 @@ static void encode(const Model& m, const Mel& mel, int seek, std::vector<float>&
   std::vector<float> cur((size_t)M * D), q((size_t)M * D), k((size_t)M * D),
       v((size_t)M * D), o((size_t)M * D), ff((size_t)M * 4 * D);
   const float KQscale = 1.0f / sqrtf((float)(D / H));
-  for (int il = 0; il < m.n_audio_layer; ++il) {
+  const int n_layers = g_enc_layer_limit >= 0 ? std::min(g_enc_layer_limit, m.n_audio_layer)
+                                             : m.n_audio_layer;
+  for (int il = 0; il < n_layers; ++il) {
     const std::string p = "encoder.blocks." + std::to_string(il);
     layer_norm(inp.data(), m.w(p + ".attn_ln.weight"), m.w(p + ".attn_ln.bias"), M, D, cur.data());
     matmul(m, m.w(p + ".attn.query.weight"), cur.data(), M, D, D, q.data());
@@ -1047,7 +1053,9 @@ static void token_level_timestamps(const Model& m, TsState& st, Segment& seg, fl
         if (st.energy[k] > thold) {
           while (k < n_samples - 1 && st.energy[k] > thold) k++;
           tokens[j].t1 = sample_to_ts(k);
-          if (j < ns - 1 && tokens[j].t1 > tokens[j + 1].t0) {
+          // upstream tests `j < ns - 1` (ns = samples, not tokens) and so reads
+          // tokens[j + 1] past the end for a trailing text token (UB); guarded
+          if (j < ns - 1 && j + 1 < n && tokens[j].t1 > tokens[j + 1].t0) {
             tokens[j].t1 = tokens[j + 1].t0;
           } else {
             s1 = k;
@@ -1380,6 +1388,7 @@ void orc_set_threads(int n) {
   (void)n;
 #endif
 }
+void orc_set_enc_layer_limit(int n) { g_enc_layer_limit = n; }
 void orc_hparams(void* h, int* out) {
   auto* m = (Model*)h;
   for (int i = 0; i < 11; ++i) out[i] = m->hp[i];

@@ -40,6 +40,7 @@ def lib() -> C.CDLL:
     L.orc_load.argtypes = [C.c_char_p, C.c_int]
     L.orc_free.argtypes = [P]
     L.orc_set_threads.argtypes = [C.c_int]
+    L.orc_set_enc_layer_limit.argtypes = [C.c_int]
     L.orc_hparams.argtypes = [P, C.POINTER(C.c_int)]
     L.orc_wtype.restype = C.c_int
     L.orc_wtype.argtypes = [P]

@@ -122,6 +122,70 @@ struct State {
   int lang_id = 0;
   std::mt19937 rng0 = std::mt19937(0);  // decoders[0].rng persists per state
   std::vector<float> probs_h, logprobs_h;
+  // perf: event pairs around launches of one kernel class. Eager launches
+  // use perf_ev; launches captured into a decode-step graph use perf_gev (the
+  // graph re-records them on every replay; harvested after each replay).
+  std::string perf_class;
+  std::vector<hipEvent_t> perf_ev, perf_gev;
+  size_t perf_used = 0, perf_gused = 0;
+  bool capturing = false;
+  double perf_acc_ms = 0.0;
+  long perf_acc_n = 0;
+};
+
+static void harvest_events(std::vector<hipEvent_t>& ev, size_t used, State& S) {
+  for (size_t i = 0; i + 1 < used; i += 2) {
+    float ms = 0.0f;
+    HIPC(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
+    S.perf_acc_ms += ms;
+    S.perf_acc_n += 1;
+  }
+}
+
+// Records a start/stop HIP event pair around a launch when `cls` is the
+// state's enabled perf class.
+struct PerfScope {
+  State& S;
+  bool on;
+  hipEvent_t stop = nullptr;
+  PerfScope(State& s, const char* cls) : S(s), on(!s.perf_class.empty() && s.perf_class == cls) {
+    if (!on) return;
+    std::vector<hipEvent_t>& ev = S.capturing ? S.perf_gev : S.perf_ev;
+    size_t& used = S.capturing ? S.perf_gused : S.perf_used;
+    while (ev.size() < used + 2) {
+      hipEvent_t e;
+      HIPC(hipEventCreate(&e));
+      ev.push_back(e);
+    }
+    record(ev[used]);
+    stop = ev[used + 1];
+    used += 2;
+  }
+  // Eager: hipEventRecord. While the stream is being captured, an explicit
+  // event-record node is appended to the capturing graph instead (HIP 7.2
+  // cannot time events recorded *through* capture; explicit nodes time fine).
+  void record(hipEvent_t e) {
+    if (!S.capturing) {
+      HIPC(hipEventRecord(e, S.stream));
+      return;
+    }
+    hipStreamCaptureStatus cs;
+    unsigned long long cid = 0;
+    hipGraph_t g = nullptr;
+    const hipGraphNode_t* deps = nullptr;
+    size_t ndeps = 0;
+    HIPC(hipStreamGetCaptureInfo_v2(S.stream, &cs, &cid, &g, &deps, &ndeps));
+    hipGraphNode_t node;
+    HIPC(hipGraphAddEventRecordNode(&node, g, deps, ndeps, e));
+    HIPC(hipStreamUpdateCaptureDependencies(S.stream, &node, 1, hipStreamSetCaptureDependencies));
+  }
+  ~PerfScope() {
+    if (!on) return;
+    try {
+      record(stop);
+    } catch (...) {
+    }
+  }
 };
 
 // ---------------------------------------------------------------------------
@@ -487,16 +551,18 @@ struct Driver {
     T* o = (T*)S.o.get((size_t)M * d * sizeof(T));
     T* ff = (T*)S.ff.get((size_t)M * 4 * d * sizeof(T));
     T* enc = (T*)S.enc.get((size_t)M * d * sizeof(T));
+    { PerfScope ps(S, "mel");
     launch_mel_window((const float*)S.mel.p, mel_clip_stride, ib, ib + 4096, ib + 2 * 4096,
-                      hp.n_mels, T2, cp, melT, nb, st);
+                      hp.n_mels, T2, cp, melT, nb, st); }
     EpiParams e;
     // conv1 (k3 s1 p1) as a GEMM over overlapping rows of the padded window
     e.bias = C.conv1_b;
     e.c16 = h1p + d;
     e.ldc = d;
     e.c_bstride = (long)(T2 + 2) * d;
+    { PerfScope ps(S, "enc_gemm");
     gemm<_Float16>(EPI_GELU, true, melT, cp, (long)(T2 + 2) * cp, C.conv1_w, 3 * cp, T2, d,
-                   3 * cp, nb, e, st);
+                   3 * cp, nb, e, st); }
     // conv2 (k3 s2 p1) + GELU + positional embedding -> residual stream x
     e = EpiParams();
     e.bias = C.conv2_b;
@@ -504,8 +570,9 @@ struct Driver {
     e.ldc = d;
     e.c_bstride = (long)Lc * d;
     e.pe = C.enc_pe;
+    { PerfScope ps(S, "enc_gemm");
     gemm<_Float16>(EPI_CONV2, false, h1p, 2 * d, (long)(T2 + 2) * d, C.conv2_w, 3 * d, Lc, d,
-                   3 * d, nb, e, st);
+                   3 * d, nb, e, st); }
     const float kq_scale = 1.0f / sqrtf(64.0f);
     for (int l = 0; l < L_enc; ++l) {
       const EncLayerW& W = C.enc[l];
@@ -519,26 +586,31 @@ struct Driver {
       e.H = H;
       e.d = d;
       e.ldv = Lp;  // V^T rows are padded to Lp (16-B aligned tile loads)
-      gemm<T>(EPI_ENC_QKV, false, h, d, 0, Wt(W.qkv_w), d, M, 3 * d, d, 1, e, st);
-      enc_attention<T>(q, k, vt, o, nb, H, Lc, kq_scale, st);
+      { PerfScope ps(S, "enc_gemm");
+      gemm<T>(EPI_ENC_QKV, false, h, d, 0, Wt(W.qkv_w), d, M, 3 * d, d, 1, e, st); }
+      { PerfScope ps(S, "enc_attn");
+      enc_attention<T>(q, k, vt, o, nb, H, Lc, kq_scale, st); }
       e = EpiParams();
       e.bias = W.o_b;
       e.c32 = x;
       e.r32 = x;
       e.ldc = d;
-      gemm<T>(EPI_RES, false, o, d, 0, Wt(W.o_w), d, M, d, d, 1, e, st);
+      { PerfScope ps(S, "enc_gemm");
+      gemm<T>(EPI_RES, false, o, d, 0, Wt(W.o_w), d, M, d, d, 1, e, st); }
       layer_norm<T>(x, W.ln2_w, W.ln2_b, h, M, d, nullptr, st);
       e = EpiParams();
       e.bias = W.fc1_b;
       e.c16 = ff;
       e.ldc = 4 * d;
-      gemm<T>(EPI_GELU, false, h, d, 0, Wt(W.fc1_w), d, M, 4 * d, d, 1, e, st);
+      { PerfScope ps(S, "enc_gemm");
+      gemm<T>(EPI_GELU, false, h, d, 0, Wt(W.fc1_w), d, M, 4 * d, d, 1, e, st); }
       e = EpiParams();
       e.bias = W.fc2_b;
       e.c32 = x;
       e.r32 = x;
       e.ldc = d;
-      gemm<T>(EPI_RES, false, ff, 4 * d, 0, Wt(W.fc2_w), 4 * d, M, d, 4 * d, 1, e, st);
+      { PerfScope ps(S, "enc_gemm");
+      gemm<T>(EPI_RES, false, ff, 4 * d, 0, Wt(W.fc2_w), 4 * d, M, d, 4 * d, 1, e, st); }
     }
     layer_norm<T>(x, C.enc_ln_w, C.enc_ln_b, enc, M, d, nullptr, st);
     // cross K/V of every decoder layer in one GEMM
@@ -552,6 +624,7 @@ struct Driver {
     e.ncap = S.cross_cap;
     e.slot = ib + 3 * 4096;
     e.kscale = powf(64.0f, -0.25f);
+    PerfScope ps(S, "cross_gemm");
     gemm<T>(EPI_CROSS_KV, false, enc, d, 0, Wt(C.cross_w), d, M, L_dec * 2 * d, d, 1, e, st);
   }
 
@@ -619,53 +692,63 @@ struct Driver {
       e.active = act;
       e.qscale = kqs;
       e.kscale = kqs;
-      gemm<T>(EPI_DEC_QKV, false, hd, d, 0, Wt(W.qkv_w), d, R, 3 * d, d, 1, e, st);
-      dec_attention<T>(qd, ks, vs, nullptr, pos, act, 0, Tctx, od, R, H, 1.0f, st);
+      { PerfScope ps(S, "dec_gemm");
+      gemm<T>(EPI_DEC_QKV, false, hd, d, 0, Wt(W.qkv_w), d, R, 3 * d, d, 1, e, st); }
+      { PerfScope ps(S, "dec_attn_self");
+      dec_attention<T>(qd, ks, vs, nullptr, pos, act, 0, Tctx, od, R, H, 1.0f, st); }
       e = EpiParams();
       e.bias = W.o_b;
       e.c32 = xd;
       e.r32 = xd;
       e.ldc = d;
-      gemm<T>(EPI_RES, false, od, d, 0, Wt(W.o_w), d, R, d, d, 1, e, st);
+      { PerfScope ps(S, "dec_gemm");
+      gemm<T>(EPI_RES, false, od, d, 0, Wt(W.o_w), d, R, d, d, 1, e, st); }
       layer_norm<T>(xd, W.lnc_w, W.lnc_b, hd, R, d, act, st);
       e = EpiParams();
       e.bias = W.cq_b;
       e.c16 = qd;
       e.ldc = d;
-      gemm<T>(EPI_STORE16, false, hd, d, 0, Wt(W.cq_w), d, R, d, d, 1, e, st);
+      { PerfScope ps(S, "dec_gemm");
+      gemm<T>(EPI_STORE16, false, hd, d, 0, Wt(W.cq_w), d, R, d, d, 1, e, st); }
+      { PerfScope ps(S, "dec_attn_cross");
       dec_attention<T>(qd, (_Float16*)S.cross_k.p + l * layer_cross,
                        (_Float16*)S.cross_v.p + l * layer_cross, xidx, pos, act,
-                       hp.n_audio_ctx, hp.n_audio_ctx, od, R, H, kqs, st);
+                       hp.n_audio_ctx, hp.n_audio_ctx, od, R, H, kqs, st); }
       e = EpiParams();
       e.bias = W.co_b;
       e.c32 = xd;
       e.r32 = xd;
       e.ldc = d;
-      gemm<T>(EPI_RES, false, od, d, 0, Wt(W.co_w), d, R, d, d, 1, e, st);
+      { PerfScope ps(S, "dec_gemm");
+      gemm<T>(EPI_RES, false, od, d, 0, Wt(W.co_w), d, R, d, d, 1, e, st); }
       layer_norm<T>(xd, W.ln2_w, W.ln2_b, hd, R, d, act, st);
       e = EpiParams();
       e.bias = W.fc1_b;
       e.c16 = ffd;
       e.ldc = 4 * d;
-      gemm<T>(EPI_GELU, false, hd, d, 0, Wt(W.fc1_w), d, R, 4 * d, d, 1, e, st);
+      { PerfScope ps(S, "dec_gemm");
+      gemm<T>(EPI_GELU, false, hd, d, 0, Wt(W.fc1_w), d, R, 4 * d, d, 1, e, st); }
       e = EpiParams();
       e.bias = W.fc2_b;
       e.c32 = xd;
       e.r32 = xd;
       e.ldc = d;
-      gemm<T>(EPI_RES, false, ffd, 4 * d, 0, Wt(W.fc2_w), 4 * d, R, d, 4 * d, 1, e, st);
+      { PerfScope ps(S, "dec_gemm");
+      gemm<T>(EPI_RES, false, ffd, 4 * d, 0, Wt(W.fc2_w), 4 * d, R, d, 4 * d, 1, e, st); }
     }
     layer_norm<T>(xd, C.dec_ln_w, C.dec_ln_b, hd, R, d, act, st);
     EpiParams e;
     e.c32 = (float*)S.logits.p;
     e.ldc = V;
-    gemm<T>(EPI_F32, false, hd, d, 0, Wt(C.tok_emb), d, R, V, d, 1, e, st);
+    { PerfScope ps(S, "logits_gemm");
+    gemm<T>(EPI_F32, false, hd, d, 0, Wt(C.tok_emb), d, R, V, d, 1, e, st); }
     float* pr = nullptr;
     float* lp = nullptr;
     if (want_probs) {
       pr = (float*)S.probs.get((size_t)R * V * 4);
       lp = (float*)S.logprobs.get((size_t)R * V * 4);
     }
+    PerfScope ps(S, "logits_proc");
     logits_process((float*)S.logits.p, (const float*)S.smask.p, (const RowCtl*)S.ctl.p,
                    (TokOut*)S.tokout.p, pr, lp, LC, R, st);
   }

@@ -54,44 +54,40 @@ __global__ __launch_bounds__(256) void enc_attn_kernel(const _Float16* __restric
     for (int u = 0; u < 2; ++u) oacc[te][u] = f32x4{0, 0, 0, 0};
   float mrow[2] = {-INFINITY, -INFINITY}, lrow[2] = {0.0f, 0.0f};
 
-  uint4 rk[2], rv[2];
-  int kso[2], vso[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int c = tid + 256 * i;
-    const int row = c >> 3, ch = c & 7;
-    kso[i] = row * 64 + ((ch ^ (row & 7)) << 3);
-    vso[i] = row * VSTR + ch * 8;
-  }
-  auto gload = [&](int kb) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = tid + 256 * i;
-      const int row = c >> 3, ch = c & 7;
-      const int key = min(kb * 64 + row, L - 1);
-      rk[i] = *reinterpret_cast<const uint4*>(Kh + (long)key * 64 + ch * 8);
-      const int key0 = kb * 64 + ch * 8;
-      if (key0 < Lp)
-        rv[i] = *reinterpret_cast<const uint4*>(VT + (long)row * Lp + key0);
-      else
-        rv[i] = uint4{0, 0, 0, 0};
-    }
-  };
-  auto sstore = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      *reinterpret_cast<uint4*>(&ks[buf][kso[i]]) = rk[i];
-      *reinterpret_cast<uint4*>(&vs[buf][vso[i]]) = rv[i];
-    }
-  };
+  // staging: thread t moves 16-B chunk (row = t/8 + 32 i, ch = t%8) of the K
+  // tile (64 keys x 64 dims) and of the V^T tile (64 dims x 64 keys)
+  const int srow = tid >> 3, sch = tid & 7;
+  const int kso0 = srow * 64 + ((sch ^ (srow & 7)) << 3);  // (row+32)&7 == row&7
+  const int vso0 = srow * VSTR + sch * 8;
+  uint4 rk0, rk1, rv0, rv1;
+#define GLOAD(kb)                                                                    \
+  do {                                                                               \
+    const int kr0 = min((kb) * 64 + srow, L - 1), kr1 = min((kb) * 64 + srow + 32, L - 1); \
+    rk0 = *reinterpret_cast<const uint4*>(Kh + (long)kr0 * 64 + sch * 8);            \
+    rk1 = *reinterpret_cast<const uint4*>(Kh + (long)kr1 * 64 + sch * 8);            \
+    const int key0 = (kb) * 64 + sch * 8;                                            \
+    if (key0 < Lp) {                                                                 \
+      rv0 = *reinterpret_cast<const uint4*>(VT + (long)srow * Lp + key0);            \
+      rv1 = *reinterpret_cast<const uint4*>(VT + (long)(srow + 32) * Lp + key0);     \
+    } else {                                                                         \
+      rv0 = rv1 = uint4{0, 0, 0, 0};                                                 \
+    }                                                                                \
+  } while (0)
+#define SSTORE(buf)                                                          \
+  do {                                                                       \
+    *reinterpret_cast<uint4*>(&ks[buf][kso0]) = rk0;                         \
+    *reinterpret_cast<uint4*>(&ks[buf][kso0 + 32 * 64]) = rk1;               \
+    *reinterpret_cast<uint4*>(&vs[buf][vso0]) = rv0;                         \
+    *reinterpret_cast<uint4*>(&vs[buf][vso0 + 32 * VSTR]) = rv1;             \
+  } while (0)
 
   const int nkb = (L + 63) / 64;
-  gload(0);
-  sstore(0);
+  GLOAD(0);
+  SSTORE(0);
   __syncthreads();
   for (int kb = 0; kb < nkb; ++kb) {
     const int cur = kb & 1;
-    if (kb + 1 < nkb) gload(kb + 1);
+    if (kb + 1 < nkb) GLOAD(kb + 1);
     // S^T = K Q^T : sacc[t][u] rows = keys 16t + 4g + r, col = query c16
     f32x4 sacc[4][2];
 #pragma unroll
@@ -179,9 +175,11 @@ __global__ __launch_bounds__(256) void enc_attn_kernel(const _Float16* __restric
           oacc[te][u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pf[u][s2], oacc[te][u], 0, 0, 0);
       }
     }
-    if (kb + 1 < nkb) sstore(cur ^ 1);
+    if (kb + 1 < nkb) SSTORE(cur ^ 1);
     __syncthreads();
   }
+#undef GLOAD
+#undef SSTORE
   const int D = H * 64;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
@@ -251,19 +249,25 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
 #pragma unroll
     for (int j = 0; j < 8; ++j) qv[j] = (float)qq[j];
   }
-  // scores: 8 lanes per key row
-  for (int j0 = wid * 8; j0 < n; j0 += 32) {
-    const int j = j0 + kg;
-    float d = 0.0f;
-    if (j < n) {
-      const f16x8 kk = *reinterpret_cast<const f16x8*>(K + (long)j * 64 + c * 8);
+  // scores: 8 lanes per 128-B key row, 4 rows in flight per lane group
+  for (int j0 = wid * 32; j0 < n; j0 += 128) {
+    f16x8 kk[4];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) d += qv[e] * (float)kk[e];
+    for (int u = 0; u < 4; ++u) {
+      const int j = min(j0 + u * 8 + kg, n - 1);
+      kk[u] = *reinterpret_cast<const f16x8*>(K + (long)j * 64 + c * 8);
     }
-    d += __shfl_xor(d, 1, 64);
-    d += __shfl_xor(d, 2, 64);
-    d += __shfl_xor(d, 4, 64);
-    if (c == 0 && j < n) sc[j] = d * scale;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = j0 + u * 8 + kg;
+      float d = 0.0f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d += qv[e] * (float)kk[u][e];
+      d += __shfl_xor(d, 1, 64);
+      d += __shfl_xor(d, 2, 64);
+      d += __shfl_xor(d, 4, 64);
+      if (c == 0 && j < n) sc[j] = d * scale;
+    }
   }
   __syncthreads();
   float mx = -INFINITY;
@@ -282,11 +286,20 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
   float acc[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) acc[e] = 0.0f;
-  for (int j = wid * 8 + kg; j < n; j += 32) {
-    const f16x8 vv = *reinterpret_cast<const f16x8*>(V + (long)j * 64 + c * 8);
-    const float p = sc[j];
+  for (int j0 = wid * 32; j0 < n; j0 += 128) {
+    f16x8 vv[4];
+    float p[4];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] += p * (float)vv[e];
+    for (int u = 0; u < 4; ++u) {
+      const int j = j0 + u * 8 + kg;
+      const int jc = min(j, n - 1);
+      vv[u] = *reinterpret_cast<const f16x8*>(V + (long)jc * 64 + c * 8);
+      p[u] = j < n ? sc[jc] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += p[u] * (float)vv[u][e];
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) {

@@ -108,34 +108,44 @@ __global__ __launch_bounds__(256, 2) void gemm_big(const T* __restrict__ A, long
   const int bz = blockIdx.z;
   A += (long)bz * a_bstride;
 
-  uint4 ra[4], rw[4];
-  const T* ap[4];
-  const T* wp[4];
-  int soff[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int c = tid + 256 * i;
-    const int row = c >> 3, kc = c & 7;
-    const int gm = min(m0 + row, M - 1);
-    const int gn = min(n0 + row, N - 1);
-    ap[i] = A + (long)gm * lda + kc * 8;
-    wp[i] = W + (long)gn * ldw + kc * 8;
-    soff[i] = row * BK + ((kc ^ (row & 7)) << 3);
-  }
-  auto gload = [&](int kt) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      ra[i] = *reinterpret_cast<const uint4*>(ap[i] + kt * BK);
-      rw[i] = *reinterpret_cast<const uint4*>(wp[i] + kt * BK);
-    }
-  };
-  auto sstore = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      *reinterpret_cast<uint4*>(&lds[buf][0][soff[i]]) = ra[i];
-      *reinterpret_cast<uint4*>(&lds[buf][1][soff[i]]) = rw[i];
-    }
-  };
+  // staging: thread t moves 16-B chunk (row = t/8 + 32 i, kc = t%8) of both
+  // 128x64 tiles; rows past M / N are clamped (their outputs are discarded)
+  const int srow = tid >> 3, kc0 = tid & 7;
+  const T* a0 = A + (long)min(m0 + srow, M - 1) * lda + kc0 * 8;
+  const T* a1 = A + (long)min(m0 + srow + 32, M - 1) * lda + kc0 * 8;
+  const T* a2 = A + (long)min(m0 + srow + 64, M - 1) * lda + kc0 * 8;
+  const T* a3 = A + (long)min(m0 + srow + 96, M - 1) * lda + kc0 * 8;
+  const T* w0 = W + (long)min(n0 + srow, N - 1) * ldw + kc0 * 8;
+  const T* w1 = W + (long)min(n0 + srow + 32, N - 1) * ldw + kc0 * 8;
+  const T* w2 = W + (long)min(n0 + srow + 64, N - 1) * ldw + kc0 * 8;
+  const T* w3 = W + (long)min(n0 + srow + 96, N - 1) * ldw + kc0 * 8;
+  // swizzled LDS offsets: (row & 7) is the same for rows srow + 32 i
+  const int soff0 = srow * BK + ((kc0 ^ (srow & 7)) << 3);
+  constexpr int SROW32 = 32 * BK;
+  uint4 ra0, ra1, ra2, ra3, rw0, rw1, rw2, rw3;
+#define GLOAD(kt)                                                   \
+  do {                                                              \
+    const int ko = (kt) * BK;                                       \
+    ra0 = *reinterpret_cast<const uint4*>(a0 + ko);                 \
+    ra1 = *reinterpret_cast<const uint4*>(a1 + ko);                 \
+    ra2 = *reinterpret_cast<const uint4*>(a2 + ko);                 \
+    ra3 = *reinterpret_cast<const uint4*>(a3 + ko);                 \
+    rw0 = *reinterpret_cast<const uint4*>(w0 + ko);                 \
+    rw1 = *reinterpret_cast<const uint4*>(w1 + ko);                 \
+    rw2 = *reinterpret_cast<const uint4*>(w2 + ko);                 \
+    rw3 = *reinterpret_cast<const uint4*>(w3 + ko);                 \
+  } while (0)
+#define SSTORE(buf)                                                                 \
+  do {                                                                              \
+    *reinterpret_cast<uint4*>(&lds[buf][0][soff0]) = ra0;                           \
+    *reinterpret_cast<uint4*>(&lds[buf][0][soff0 + SROW32]) = ra1;                  \
+    *reinterpret_cast<uint4*>(&lds[buf][0][soff0 + 2 * SROW32]) = ra2;              \
+    *reinterpret_cast<uint4*>(&lds[buf][0][soff0 + 3 * SROW32]) = ra3;              \
+    *reinterpret_cast<uint4*>(&lds[buf][1][soff0]) = rw0;                           \
+    *reinterpret_cast<uint4*>(&lds[buf][1][soff0 + SROW32]) = rw1;                  \
+    *reinterpret_cast<uint4*>(&lds[buf][1][soff0 + 2 * SROW32]) = rw2;              \
+    *reinterpret_cast<uint4*>(&lds[buf][1][soff0 + 3 * SROW32]) = rw3;              \
+  } while (0)
 
   f32x4 acc[4][4];
 #pragma unroll
@@ -143,13 +153,13 @@ __global__ __launch_bounds__(256, 2) void gemm_big(const T* __restrict__ A, long
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
 
-  gload(0);
-  sstore(0);
+  GLOAD(0);
+  SSTORE(0);
   __syncthreads();
   const int nk = K / BK;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) gload(kt + 1);
+    if (kt + 1 < nk) GLOAD(kt + 1);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       V8 af[4], bf[4];
@@ -169,9 +179,11 @@ __global__ __launch_bounds__(256, 2) void gemm_big(const T* __restrict__ A, long
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = Elt<T>::mfma(af[i], bf[j], acc[i][j]);
     }
-    if (kt + 1 < nk) sstore(cur ^ 1);
+    if (kt + 1 < nk) SSTORE(cur ^ 1);
     __syncthreads();
   }
+#undef GLOAD
+#undef SSTORE
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -186,46 +198,52 @@ __global__ __launch_bounds__(256, 2) void gemm_big(const T* __restrict__ A, long
 }
 
 // ---------------------------------------------------------------------------
-// skinny (decode) GEMM: M <= 16*MT rows
+// skinny (decode) GEMM: M <= 16*MT rows. One workgroup = one 16-column strip;
+// its NW waves split K, each wave owns KCH consecutive 32-deep k-steps and
+// issues all of its W and A fragment loads before the first MFMA (one memory
+// round trip per launch), then the NW partial tiles are summed through LDS.
 // ---------------------------------------------------------------------------
-template <typename T, int EPI, bool OUT16, int MT, int WN>
-__global__ __launch_bounds__(256) void gemm_skinny(const T* __restrict__ A, long lda,
-                                                   const T* __restrict__ W, long ldw, int M,
-                                                   int N, int K, EpiParams P) {
+template <int EPI, typename T, bool OUT16>
+__device__ __forceinline__ void skinny_store(const EpiParams& P, int m, int n, float v) {
+  epi_store<EPI, T, OUT16>(P, 0, m, n, v);
+}
+
+template <typename T, int MT, int KCH>
+__global__ __launch_bounds__(1024) void gemm_skinny(int epi, const T* __restrict__ A, long lda,
+                                                    const T* __restrict__ W, long ldw, int M,
+                                                    int N, EpiParams P) {
   using V8 = typename Elt<T>::v8;
-  constexpr int WK = 4 / WN;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wn = wid % WN, wk = wid / WN;
-  const int n0 = (blockIdx.x * WN + wn) * 16;
+  __shared__ f32x4 red[16][MT][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, NW = blockDim.x >> 6;
+  const int n0 = blockIdx.x * 16;
   const int ncol = min(n0 + (lane & 15), N - 1);
-  const T* wrow = W + (long)ncol * ldw + (lane >> 4) * 8;
-  const T* arow[MT];
+  const int kb = wid * KCH * 32 + (lane >> 4) * 8;
+  const T* wrow = W + (long)ncol * ldw + kb;
+  V8 bfr[KCH];
+  V8 afr[MT][KCH];
+#pragma unroll
+  for (int c = 0; c < KCH; ++c) bfr[c] = ld8(wrow + c * 32);
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int row = min(mt * 16 + (lane & 15), M - 1);
-    arow[mt] = A + (long)row * lda + (lane >> 4) * 8;
+    const T* ar = A + (long)row * lda + kb;
+#pragma unroll
+    for (int c = 0; c < KCH; ++c) afr[mt][c] = ld8(ar + c * 32);
   }
-  const int kper = K / WK;
-  const int kb = wk * kper;
   f32x4 acc[MT];
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0, 0, 0, 0};
-  for (int k = kb; k < kb + kper; k += 32) {
-    const V8 b = ld8(wrow + k);
+  for (int mt = 0; mt < MT; ++mt) {
+    acc[mt] = f32x4{0, 0, 0, 0};
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) acc[mt] = Elt<T>::mfma(ld8(arow[mt] + k), b, acc[mt]);
+    for (int c = 0; c < KCH; ++c) acc[mt] = Elt<T>::mfma(afr[mt][c], bfr[c], acc[mt]);
   }
-  if constexpr (WK > 1) {
-    __shared__ f32x4 red[4][MT][64];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) red[wid][mt][lane] = acc[mt];
-    __syncthreads();
-    if (wk != 0) return;
+  for (int mt = 0; mt < MT; ++mt) red[wid][mt][lane] = acc[mt];
+  __syncthreads();
+  if (wid != 0) return;
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int w = 1; w < WK; ++w) acc[mt] += red[w * WN + wn][mt][lane];
-  }
+  for (int mt = 0; mt < MT; ++mt)
+    for (int w = 1; w < NW; ++w) acc[mt] += red[w][mt][lane];
   const int n = n0 + (lane & 15);
   if (n >= N) return;
 #pragma unroll
@@ -233,8 +251,49 @@ __global__ __launch_bounds__(256) void gemm_skinny(const T* __restrict__ A, long
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int m = mt * 16 + (lane >> 4) * 4 + r;
-      if (m < M) epi_store<EPI, T, OUT16>(P, 0, m, n, acc[mt][r]);
+      if (m >= M) continue;
+      const float v = acc[mt][r];
+      switch (epi) {
+        case EPI_GELU: skinny_store<EPI_GELU, T, false>(P, m, n, v); break;
+        case EPI_RES: skinny_store<EPI_RES, T, false>(P, m, n, v); break;
+        case EPI_F32: skinny_store<EPI_F32, T, false>(P, m, n, v); break;
+        case EPI_DEC_QKV: skinny_store<EPI_DEC_QKV, T, false>(P, m, n, v); break;
+        case EPI_STORE16: skinny_store<EPI_STORE16, T, false>(P, m, n, v); break;
+        default: break;
+      }
     }
+}
+
+// (waves, k-steps per wave) for a K: all 32-deep k-steps split evenly over at
+// most 16 waves with at most 10 k-steps each.
+static bool skinny_split(int K, int& nw, int& kch) {
+  if (K % 32) return false;
+  const int S = K / 32;
+  for (int w = 16; w >= 1; --w) {
+    if (S % w) continue;
+    const int c = S / w;
+    if (c == 1 || c == 2 || c == 3 || c == 4 || c == 6 || c == 8 || c == 10) {
+      nw = w;
+      kch = c;
+      return true;
+    }
+  }
+  return false;
+}
+
+template <typename T, int MT>
+static bool skinny_launch(int epi, const T* A, long lda, const T* W, long ldw, int M, int N, int K,
+                          const EpiParams& P, hipStream_t st) {
+  int nw = 0, kch = 0;
+  if (!skinny_split(K, nw, kch)) return false;
+  const dim3 g((N + 15) / 16), b(64 * nw);
+  switch (kch) {
+#define SK(C) \
+  case C: gemm_skinny<T, MT, C><<<g, b, 0, st>>>(epi, A, lda, W, ldw, M, N, P); return true;
+    SK(1) SK(2) SK(3) SK(4) SK(6) SK(8) SK(10)
+#undef SK
+    default: return false;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -243,24 +302,15 @@ __global__ __launch_bounds__(256) void gemm_skinny(const T* __restrict__ A, long
 template <typename T, int EPI, bool OUT16>
 static void gemm_dispatch(const T* A, long lda, long a_bstride, const T* W, long ldw, int M,
                           int N, int K, int batch, const EpiParams& P, hipStream_t st) {
-  if (batch == 1 && M <= 64 && (K % 128) == 0) {
+  if (batch == 1 && M <= 64 && !OUT16 && EPI != EPI_ENC_QKV && EPI != EPI_CONV2 &&
+      EPI != EPI_CROSS_KV) {
     const int MT = (M + 15) / 16;
-    const bool wide = N >= 4096;
-#define SKINNY(MTV)                                                                         \
-  if (MT == MTV) {                                                                          \
-    if (wide)                                                                               \
-      gemm_skinny<T, EPI, OUT16, MTV, 4><<<(N + 63) / 64, 256, 0, st>>>(A, lda, W, ldw, M, \
-                                                                         N, K, P);          \
-    else                                                                                    \
-      gemm_skinny<T, EPI, OUT16, MTV, 1><<<(N + 15) / 16, 256, 0, st>>>(A, lda, W, ldw, M, \
-                                                                         N, K, P);          \
-    return;                                                                                 \
-  }
-    SKINNY(1)
-    SKINNY(2)
-    SKINNY(3)
-    SKINNY(4)
-#undef SKINNY
+    bool ok = false;
+    if (MT == 1) ok = skinny_launch<T, 1>(EPI, A, lda, W, ldw, M, N, K, P, st);
+    else if (MT == 2) ok = skinny_launch<T, 2>(EPI, A, lda, W, ldw, M, N, K, P, st);
+    else if (MT == 3) ok = skinny_launch<T, 3>(EPI, A, lda, W, ldw, M, N, K, P, st);
+    else ok = skinny_launch<T, 4>(EPI, A, lda, W, ldw, M, N, K, P, st);
+    if (ok) return;
   }
   dim3 g((N + BN - 1) / BN, (M + BM - 1) / BM, batch);
   gemm_big<T, EPI, OUT16><<<g, 256, 0, st>>>(A, lda, a_bstride, W, ldw, M, N, K, P);

@@ -11,40 +11,67 @@
 
 namespace mwx {
 
-// ggml_norm (eps 1e-5, double accumulation) followed by *w + b; one wave/row.
-template <typename T>
+// ggml_norm (eps 1e-5, double accumulation) followed by *w + b. One 256-thread
+// workgroup per row; every element of the row is loaded once, all loads of a
+// thread are issued back to back (NPT = ceil(N / 256) registers per thread).
+template <typename T, int NPT>
 __global__ __launch_bounds__(256) void ln_kernel(const float* __restrict__ x,
                                                  const float* __restrict__ w,
                                                  const float* __restrict__ b, T* __restrict__ y,
-                                                 int M, int N, const int* __restrict__ active) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= M) return;
+                                                 int N, const int* __restrict__ active) {
+  __shared__ double red[2][4];
+  const int row = blockIdx.x;
   if (active && !active[row]) return;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const float* xr = x + (long)row * N;
+  float v[NPT], wv[NPT], bv[NPT];
+#pragma unroll
+  for (int j = 0; j < NPT; ++j) {
+    const int i = tid + 256 * j;
+    v[j] = i < N ? xr[i] : 0.0f;
+    wv[j] = i < N ? w[i] : 0.0f;
+    bv[j] = i < N ? b[i] : 0.0f;
+  }
   double s = 0.0;
-  for (int i = lane; i < N; i += 64) s += (double)xr[i];
+#pragma unroll
+  for (int j = 0; j < NPT; ++j) s += (double)v[j];
   s = wave_sum_d(s);
+  if (lane == 0) red[0][wid] = s;
+  __syncthreads();
+  s = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
   const float mean = (float)(s / N);
   double s2 = 0.0;
-  for (int i = lane; i < N; i += 64) {
-    const float v = xr[i] - mean;
-    s2 += (double)(v * v);
+#pragma unroll
+  for (int j = 0; j < NPT; ++j) {
+    const int i = tid + 256 * j;
+    const float d = v[j] - mean;
+    if (i < N) s2 += (double)(d * d);
   }
   s2 = wave_sum_d(s2);
+  if (lane == 0) red[1][wid] = s2;
+  __syncthreads();
+  s2 = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
   const float variance = (float)(s2 / N);
   const float scale = 1.0f / sqrtf(variance + 1e-5f);
   T* yr = y + (long)row * N;
-  for (int i = lane; i < N; i += 64) {
-    const float v = (xr[i] - mean) * scale;
-    yr[i] = to_t<T>(v * w[i] + b[i]);
+#pragma unroll
+  for (int j = 0; j < NPT; ++j) {
+    const int i = tid + 256 * j;
+    if (i < N) yr[i] = to_t<T>(((v[j] - mean) * scale) * wv[j] + bv[j]);
   }
 }
 
 template <typename T>
 void layer_norm(const float* x, const float* w, const float* b, T* y, int M, int N,
                 const int* active, hipStream_t st) {
-  ln_kernel<T><<<(M + 3) / 4, 256, 0, st>>>(x, w, b, y, M, N, active);
+  const int npt = (N + 255) / 256;
+  switch (npt) {
+#define LNC(K) \
+  case K: ln_kernel<T, K><<<M, 256, 0, st>>>(x, w, b, y, N, active); break;
+    LNC(1) LNC(2) LNC(3) LNC(4) LNC(5) LNC(6) LNC(7) LNC(8)
+#undef LNC
+    default: break;
+  }
 }
 
 // x[r] = te[tok[r]] + pe[pos[r]]   (ggml_get_rows(d_te) + ggml_get_rows(d_pe))

@@ -130,6 +130,10 @@ def lib() -> C.CDLL:
         f.argtypes = [P]
     L.mwx_write_synthetic_model.restype = C.c_int
     L.mwx_write_synthetic_model.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_uint64]
+    L.mwx_perf_enable.restype = None
+    L.mwx_perf_enable.argtypes = [P, C.c_char_p]
+    L.mwx_perf_read.restype = C.c_int
+    L.mwx_perf_read.argtypes = [P, C.POINTER(C.c_double), C.POINTER(C.c_int)]
     L.mwx_tokenize.restype = C.c_int
     L.mwx_tokenize.argtypes = [P, C.c_char_p, C.POINTER(C.c_int32), C.c_int]
     L.mwx_test_mel.restype = C.c_int

@@ -86,16 +86,23 @@ def service_params(ctx, beam=1, temperature_inc=0.2, language=b"auto"):
     return p
 
 
-def assert_same(segs, osegs):
-    assert [t.id for s in segs for t in s.tokens] == [t.id for s in osegs for t in s.tokens]
+def assert_same(segs, osegs, p_tol=5e-3):
+    """Token ids, segment text/times and token timestamps must match exactly;
+    token probabilities within p_tol (logits agree to ~1e-2 abs for f16: the
+    activations are rounded to 16 bits at the same points, only the f32
+    summation order differs; bf16 rounding is 8x coarser)."""
+    ids = [t.id for s in segs for t in s.tokens]
+    oids = [t.id for s in osegs for t in s.tokens]
+    assert ids == oids, next(((i, a, b) for i, (a, b) in enumerate(zip(ids, oids)) if a != b), None)
     assert [(s.t0, s.t1, s.text) for s in segs] == [(s.t0, s.t1, s.text) for s in osegs]
-    assert [(t.t0, t.t1) for s in segs for t in s.tokens] == [(t.t0, t.t1) for s in osegs for t in s.tokens]
-    for s, so in zip(segs, osegs):
-        for t, to in zip(s.tokens, so.tokens):
-            assert t.tid == to.tid
-            # logits agree to ~1e-2 abs (f16-rounded activations, different f32
-            # summation order), so token probabilities agree to a few 1e-3
-            assert abs(t.p - to.p) < 5e-3 and abs(t.plog - to.plog) < 1e-2
+    toks = [t for s in segs for t in s.tokens]
+    otoks = [t for s in osegs for t in s.tokens]
+    for i, (t, to) in enumerate(zip(toks, otoks)):
+        assert (t.t0, t.t1) == (to.t0, to.t1), (
+            f"token {i}: dev t0/t1 {t.t0}/{t.t1} pt {t.pt:.6f} ptsum {t.ptsum:.6f} tid {t.tid} | "
+            f"oracle {to.t0}/{to.t1} pt {to.pt:.6f} ptsum {to.ptsum:.6f} tid {to.tid}")
+        assert t.tid == to.tid
+        assert abs(t.p - to.p) < p_tol and abs(t.plog - to.plog) < 2 * p_tol, (i, t, to)
 
 
 def test_greedy_tokens_match_oracle(micro):
@@ -159,7 +166,7 @@ def test_bf16_model(make_model):
         opt = orc.FullOptions.service_defaults()
         opt.temperature_inc = 0.0
         segs, osegs, _ = run_both(ctx, o, pcm_clip(5), opt, service_params(ctx, temperature_inc=0.0))
-        assert_same(segs, osegs)
+        assert_same(segs, osegs, p_tol=2e-2)
 
 
 def test_tiny_en_greedy(make_model):
