@@ -151,7 +151,8 @@ def main():
         os.replace(tmp, path)
     barrier()
     ctx = mwx.Context.open(path, device=local)
-    pcms = [mwx.pcm16_to_f32(mwx.synth_pcm16(rank * args.clips + k)) for k in range(args.clips)]
+    import shard
+    pcms = [mwx.pcm16_to_f32(mwx.synth_pcm16(k)) for k in shard.clip_ids(rank, args.clips)]
     p = ctx.default_params(mwx.SAMPLING_GREEDY)
     p.language = b"en"
     p.temperature = 0.0
@@ -167,18 +168,12 @@ def main():
         rc = ctx.full_batch(pcms, p)
         if rc != 0:
             raise RuntimeError(f"mwx_full_batch rc={rc}")
-        toks = np.zeros((args.clips, max_tok), np.int32)
-        for c in range(args.clips):
-            ids = mwx.token_ids(ctx.segments(c))[:max_tok]
-            toks[c, :len(ids)] = ids
-        t = torch.from_numpy(toks).cuda()
-        if dist is not None:
-            out = torch.empty((world * args.clips, max_tok), dtype=torch.int32, device=t.device)
-            dist.all_gather_into_tensor(out, t)  # RCCL over xGMI: token streams to rank 0
-            if rank == 0:
-                gathered["tokens"] = out.cpu().numpy()
-        else:
-            gathered["tokens"] = t.cpu().numpy()
+        block = shard.pack_tokens([mwx.token_ids(ctx.segments(c)) for c in range(args.clips)],
+                                  max_tok)
+        # RCCL over xGMI: every rank's token streams to rank 0
+        g = shard.gather_to_rank0(dist, block, device="cuda")
+        if g is not None:
+            gathered["tokens"] = g
 
     for _ in range(args.warmup):
         step()

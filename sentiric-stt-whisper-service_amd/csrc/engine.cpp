@@ -89,7 +89,8 @@ struct Context {
   const float* enc_pe = nullptr;
   std::vector<EncLayerW> enc;
   const float *enc_ln_w = nullptr, *enc_ln_b = nullptr;
-  const void* tok_emb = nullptr;
+  const void* tok_emb = nullptr;    // [n_vocab][d] rows (embedding gather)
+  const void* tok_emb_p = nullptr;  // fragment-tiled copy (logits GEMM)
   const float* dec_pe = nullptr;
   std::vector<DecLayerW> dec;
   const void* cross_w = nullptr;
@@ -116,6 +117,7 @@ struct State {
   DBuf ibuf;  // small int arrays (slot maps)
   // decoder workspace (row-batched)
   DBuf xd, hd, qd, od, ffd, logits, kself, vself, stepin, ctl, tokout, probs, logprobs, smask;
+  DBuf pqkv, pres, pq;  // split-K partial slabs of the decode GEMMs
   int cross_cap = 0;  // cross cache slots
   int row_cap = 0;    // self cache rows
   std::vector<Segment> result_all;
@@ -268,24 +270,25 @@ static bool upload_model(Context& C, const ModelFile& mf) {
     for (int64_t i = 0; i < expect; ++i) v[i] = elem_f32(*t, i);
     A.add(v.data(), v.size() * 4, (const void**)slot);
   };
-  // 16-bit weight in the model type, rows concatenated from several tensors
-  auto w16 = [&](const std::vector<std::string>& names, int64_t K, const void** slot) {
+  // 16-bit weight rows in the model type, concatenated from several tensors
+  auto rows16 = [&](const std::vector<std::string>& names, int64_t K, std::vector<uint16_t>& out,
+                    int64_t& rows) -> bool {
     std::vector<const FileTensor*> ts;
-    int64_t rows = 0;
+    rows = 0;
     for (const auto& n : names) {
       const FileTensor* t = need(n);
-      if (!t) return;
+      if (!t) return false;
       if (t->ne[0] != K) {
         MWX_LOG_ERROR("mwx: tensor '%s' inner dim %lld != %lld\n", n.c_str(), (long long)t->ne[0],
                       (long long)K);
         ok = false;
-        return;
+        return false;
       }
       ts.push_back(t);
       rows += t->nelements() / K;
     }
-    const size_t off = A.add(nullptr, (size_t)rows * K * 2, slot);
-    uint16_t* dst = (uint16_t*)A.at(off);
+    out.resize((size_t)rows * K);
+    uint16_t* dst = out.data();
     for (const FileTensor* t : ts) {
       const int64_t n = t->nelements();
       const int want = bf ? GGML_BF16 : GGML_F16;
@@ -299,6 +302,29 @@ static bool upload_model(Context& C, const ModelFile& mf) {
       }
       dst += n;
     }
+    return true;
+  };
+  // row layout [N][K] (encoder GEMMs, embedding gather)
+  auto w16 = [&](const std::vector<std::string>& names, int64_t K, const void** slot) {
+    std::vector<uint16_t> w;
+    int64_t rows = 0;
+    if (rows16(names, K, w, rows)) A.add(w.data(), w.size() * 2, slot);
+  };
+  // decode-GEMM fragment tiles (see kernels.h: pack_index)
+  auto w16p = [&](const std::vector<std::string>& names, int64_t K, const void** slot) {
+    std::vector<uint16_t> w;
+    int64_t rows = 0;
+    if (!rows16(names, K, w, rows)) return;
+    if (K % 32) {
+      MWX_LOG_ERROR("mwx: decoder weight inner dim %lld is not a multiple of 32\n", (long long)K);
+      ok = false;
+      return;
+    }
+    const int64_t np = (rows + 15) / 16 * 16;
+    std::vector<uint16_t> p((size_t)np * K, 0);
+    for (int64_t n = 0; n < rows; ++n)
+      for (int64_t k = 0; k < K; ++k) p[pack_index(n, k, K)] = w[(size_t)n * K + k];
+    A.add(p.data(), p.size() * 2, slot);
   };
   // filters + mel tables
   A.add(mf.filters.data(), mf.filters.size() * 4, (const void**)&C.d_filters);
@@ -363,6 +389,7 @@ static bool upload_model(Context& C, const ModelFile& mf) {
   f32v("encoder.ln_post.weight", &C.enc_ln_w, d);
   f32v("encoder.ln_post.bias", &C.enc_ln_b, d);
   w16({"decoder.token_embedding.weight"}, dt, &C.tok_emb);
+  w16p({"decoder.token_embedding.weight"}, dt, &C.tok_emb_p);
   f32v("decoder.positional_embedding", &C.dec_pe, (int64_t)hp.n_text_ctx * dt);
   C.dec.resize(hp.n_text_layer);
   std::vector<std::string> cross_names;
@@ -376,7 +403,7 @@ static bool upload_model(Context& C, const ModelFile& mf) {
     f32v(p + ".cross_attn_ln.bias", &L.lnc_b, dt);
     f32v(p + ".mlp_ln.weight", &L.ln2_w, dt);
     f32v(p + ".mlp_ln.bias", &L.ln2_b, dt);
-    w16({p + ".attn.query.weight", p + ".attn.key.weight", p + ".attn.value.weight"}, dt, &L.qkv_w);
+    w16p({p + ".attn.query.weight", p + ".attn.key.weight", p + ".attn.value.weight"}, dt, &L.qkv_w);
     {
       const FileTensor* qb = need(p + ".attn.query.bias");
       const FileTensor* vb = need(p + ".attn.value.bias");
@@ -388,15 +415,15 @@ static bool upload_model(Context& C, const ModelFile& mf) {
       }
       A.add(b.data(), b.size() * 4, (const void**)&L.qkv_b);
     }
-    w16({p + ".attn.out.weight"}, dt, &L.o_w);
+    w16p({p + ".attn.out.weight"}, dt, &L.o_w);
     f32v(p + ".attn.out.bias", &L.o_b, dt);
-    w16({p + ".cross_attn.query.weight"}, dt, &L.cq_w);
+    w16p({p + ".cross_attn.query.weight"}, dt, &L.cq_w);
     f32v(p + ".cross_attn.query.bias", &L.cq_b, dt);
-    w16({p + ".cross_attn.out.weight"}, dt, &L.co_w);
+    w16p({p + ".cross_attn.out.weight"}, dt, &L.co_w);
     f32v(p + ".cross_attn.out.bias", &L.co_b, dt);
-    w16({p + ".mlp.0.weight"}, dt, &L.fc1_w);
+    w16p({p + ".mlp.0.weight"}, dt, &L.fc1_w);
     f32v(p + ".mlp.0.bias", &L.fc1_b, 4 * dt);
-    w16({p + ".mlp.2.weight"}, 4 * dt, &L.fc2_w);
+    w16p({p + ".mlp.2.weight"}, 4 * dt, &L.fc2_w);
     f32v(p + ".mlp.2.bias", &L.fc2_b, dt);
     cross_names.push_back(p + ".cross_attn.key.weight");
     cross_names.push_back(p + ".cross_attn.value.weight");
@@ -648,6 +675,9 @@ struct Driver {
       S.vself.get(per * R);
       S.row_cap = R;
     }
+    S.pqkv.get((size_t)8 * R * 3 * d * 4);
+    S.pres.get((size_t)8 * R * d * 4);
+    S.pq.get((size_t)8 * R * d * 4);
     S.xd.get((size_t)R * d * 4, true);
     S.hd.get((size_t)R * d * sizeof(T), true);
     S.qd.get((size_t)R * d * 2, true);
@@ -675,73 +705,61 @@ struct Driver {
     embed<T>(Wt(C.tok_emb), C.dec_pe, tok, pos, act, xd, R, d, st);
     const size_t layer_self = (size_t)S.row_cap * H * Tctx * 64;
     const size_t layer_cross = (size_t)S.cross_cap * H * hp.n_audio_ctx * 64;
+    float* Pqkv = (float*)S.pqkv.p;
+    float* Pres = (float*)S.pres.p;
+    float* Pq = (float*)S.pq.p;
+    // The d- and 3d-wide projections run as split-K GEMMs writing f32 partial
+    // slabs; each consumer (LN: bias + residual, attention: bias/scale/f16 and
+    // the KV-cache append) folds the slabs in, so no launch is added.
+    int ks_prev = 0;
+    const float* bias_prev = nullptr;
     for (int l = 0; l < L_dec; ++l) {
       const DecLayerW& W = C.dec[l];
       _Float16* ks = (_Float16*)S.kself.p + l * layer_self;
       _Float16* vs = (_Float16*)S.vself.p + l * layer_self;
-      layer_norm<T>(xd, W.ln1_w, W.ln1_b, hd, R, d, act, st);
-      EpiParams e;
-      e.bias = W.qkv_b;
-      e.q = qd;
-      e.k = ks;
-      e.v = vs;
-      e.L = Tctx;
-      e.H = H;
-      e.d = d;
-      e.pos = pos;
-      e.active = act;
-      e.qscale = kqs;
-      e.kscale = kqs;
+      layer_norm<T>(xd, W.ln1_w, W.ln1_b, hd, R, d, act, st, ks_prev ? Pres : nullptr, ks_prev,
+                    bias_prev);
+      int k1;
       { PerfScope ps(S, "dec_gemm");
-      gemm<T>(EPI_DEC_QKV, false, hd, d, 0, Wt(W.qkv_w), d, R, 3 * d, d, 1, e, st); }
+        k1 = gemm_splitk_partials<T>(hd, d, Wt(W.qkv_w), R, 3 * d, d, Pqkv, st); }
       { PerfScope ps(S, "dec_attn_self");
-      dec_attention<T>(qd, ks, vs, nullptr, pos, act, 0, Tctx, od, R, H, 1.0f, st); }
-      e = EpiParams();
-      e.bias = W.o_b;
-      e.c32 = xd;
-      e.r32 = xd;
-      e.ldc = d;
+        dec_attention<T>(Pqkv, k1, 3 * d, W.qkv_b, kqs, kqs, ks, vs, nullptr, pos, act, 0, Tctx,
+                         od, R, H, 1.0f, st); }
+      int k2;
       { PerfScope ps(S, "dec_gemm");
-      gemm<T>(EPI_RES, false, od, d, 0, Wt(W.o_w), d, R, d, d, 1, e, st); }
-      layer_norm<T>(xd, W.lnc_w, W.lnc_b, hd, R, d, act, st);
-      e = EpiParams();
-      e.bias = W.cq_b;
-      e.c16 = qd;
-      e.ldc = d;
+        k2 = gemm_splitk_partials<T>(od, d, Wt(W.o_w), R, d, d, Pres, st); }
+      layer_norm<T>(xd, W.lnc_w, W.lnc_b, hd, R, d, act, st, Pres, k2, W.o_b);
+      int k3;
       { PerfScope ps(S, "dec_gemm");
-      gemm<T>(EPI_STORE16, false, hd, d, 0, Wt(W.cq_w), d, R, d, d, 1, e, st); }
+        k3 = gemm_splitk_partials<T>(hd, d, Wt(W.cq_w), R, d, d, Pq, st); }
       { PerfScope ps(S, "dec_attn_cross");
-      dec_attention<T>(qd, (_Float16*)S.cross_k.p + l * layer_cross,
-                       (_Float16*)S.cross_v.p + l * layer_cross, xidx, pos, act,
-                       hp.n_audio_ctx, hp.n_audio_ctx, od, R, H, kqs, st); }
-      e = EpiParams();
-      e.bias = W.co_b;
-      e.c32 = xd;
-      e.r32 = xd;
-      e.ldc = d;
+        dec_attention<T>(Pq, k3, d, W.cq_b, 1.0f, 1.0f,
+                         (_Float16*)S.cross_k.p + l * layer_cross,
+                         (_Float16*)S.cross_v.p + l * layer_cross, xidx, pos, act,
+                         hp.n_audio_ctx, hp.n_audio_ctx, od, R, H, kqs, st); }
+      int k4;
       { PerfScope ps(S, "dec_gemm");
-      gemm<T>(EPI_RES, false, od, d, 0, Wt(W.co_w), d, R, d, d, 1, e, st); }
-      layer_norm<T>(xd, W.ln2_w, W.ln2_b, hd, R, d, act, st);
-      e = EpiParams();
+        k4 = gemm_splitk_partials<T>(od, d, Wt(W.co_w), R, d, d, Pres, st); }
+      layer_norm<T>(xd, W.ln2_w, W.ln2_b, hd, R, d, act, st, Pres, k4, W.co_b);
+      EpiParams e;
       e.bias = W.fc1_b;
       e.c16 = ffd;
       e.ldc = 4 * d;
+      bool k5;
       { PerfScope ps(S, "dec_gemm");
-      gemm<T>(EPI_GELU, false, hd, d, 0, Wt(W.fc1_w), d, R, 4 * d, d, 1, e, st); }
-      e = EpiParams();
-      e.bias = W.fc2_b;
-      e.c32 = xd;
-      e.r32 = xd;
-      e.ldc = d;
+        k5 = gemm_decode<T>(EPI_GELU, hd, d, Wt(W.fc1_w), R, 4 * d, d, e, st); }
       { PerfScope ps(S, "dec_gemm");
-      gemm<T>(EPI_RES, false, ffd, 4 * d, 0, Wt(W.fc2_w), 4 * d, R, d, 4 * d, 1, e, st); }
+        ks_prev = gemm_splitk_partials<T>(ffd, 4 * d, Wt(W.fc2_w), R, d, 4 * d, Pres, st); }
+      bias_prev = W.fc2_b;
+      if (!k1 || !k2 || !k3 || !k4 || !k5 || !ks_prev) throw std::runtime_error("mwx: unsupported split-K shape");
     }
-    layer_norm<T>(xd, C.dec_ln_w, C.dec_ln_b, hd, R, d, act, st);
+    layer_norm<T>(xd, C.dec_ln_w, C.dec_ln_b, hd, R, d, act, st, Pres, ks_prev, bias_prev);
     EpiParams e;
     e.c32 = (float*)S.logits.p;
     e.ldc = V;
     { PerfScope ps(S, "logits_gemm");
-    gemm<T>(EPI_F32, false, hd, d, 0, Wt(C.tok_emb), d, R, V, d, 1, e, st); }
+    if (!gemm_decode<T>(EPI_F32, hd, d, Wt(C.tok_emb_p), R, V, d, e, st))
+      throw std::runtime_error("mwx: unsupported logits GEMM shape"); }
     float* pr = nullptr;
     float* lp = nullptr;
     if (want_probs) {

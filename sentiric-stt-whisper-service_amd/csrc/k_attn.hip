@@ -226,48 +226,94 @@ __device__ __forceinline__ double block_sum_256d(double v, double* red) {
 
 template <typename T>
 __global__ __launch_bounds__(256) void dec_attn_kernel(
-    const _Float16* __restrict__ q, const _Float16* __restrict__ kbase,
-    const _Float16* __restrict__ vbase, const int* __restrict__ kv_index,
-    const int* __restrict__ pos, const int* __restrict__ active, int fixed_len, int cap,
-    T* __restrict__ o, int H, float scale) {
+    const float* __restrict__ P, int KS, int pcols, const float* __restrict__ bias, float qscale,
+    float kscale, _Float16* __restrict__ kbase, _Float16* __restrict__ vbase,
+    const int* __restrict__ kv_index, const int* __restrict__ pos, const int* __restrict__ active,
+    int fixed_len, int cap, T* __restrict__ o, int H, float scale) {
   __shared__ float sc[DEC_MAX_KEYS];
   __shared__ float redf[4];
   __shared__ double redd[4];
   __shared__ float pv[4][64][9];
+  __shared__ float sq[64], snk[64], snv[64];
   const int row = blockIdx.y, h = blockIdx.x;
   if (!active[row]) return;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int kg = lane >> 3, c = lane & 7;
-  const int n = fixed_len > 0 ? fixed_len : pos[row] + 1;
+  const bool self = fixed_len == 0;
+  const int p_row = self ? pos[row] : 0;
+  const int n = self ? p_row + 1 : fixed_len;
   const int slot = kv_index ? kv_index[row] : row;
-  const _Float16* K = kbase + (((long)slot * H + h) * cap) * 64;
-  const _Float16* V = vbase + (((long)slot * H + h) * cap) * 64;
   const int D = H * 64;
-  float qv[8];
-  {
-    const f16x8 qq = *reinterpret_cast<const f16x8*>(q + (long)row * D + h * 64 + c * 8);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) qv[j] = (float)qq[j];
+  _Float16* K = kbase + (((long)slot * H + h) * cap) * 64;
+  _Float16* V = vbase + (((long)slot * H + h) * cap) * 64;
+  // Key/value rows are streamed in batches of 8 rows per 8-lane group (each
+  // lane 16 B of a 128-B row), double-buffered: batch i+1 is in flight while
+  // batch i is consumed. A wave covers 64 rows per batch, the workgroup 256.
+  // The first key batch is issued before the projection reduction.
+  const int jnew = self ? p_row : -1;
+  constexpr int UB = 8;
+  f16x8 ka[UB], kb2[UB];
+#define LOADROWS(buf, base, j0v)                                                   \
+  _Pragma("unroll") for (int u = 0; u < UB; ++u) {                               \
+    const int j = min((j0v) + u * 8 + kg, n - 1);                                 \
+    if (j != jnew) buf[u] = *reinterpret_cast<const f16x8*>(base + (long)j * 64 + c * 8); \
   }
-  // scores: 8 lanes per 128-B key row, 4 rows in flight per lane group
-  for (int j0 = wid * 32; j0 < n; j0 += 128) {
-    f16x8 kk[4];
+  LOADROWS(ka, K, wid * 64)
+  // reduce the projections of this head from the split-K slabs (KS <= 8)
+  const long pstride = (long)gridDim.y * pcols;
+  if (tid < (self ? 192 : 64)) {
+    const int part = tid >> 6, e = tid & 63;
+    const int col = part * D + h * 64 + e;
+    const float* pp = P + (long)row * pcols + col;
+    float pk[8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int j = min(j0 + u * 8 + kg, n - 1);
-      kk[u] = *reinterpret_cast<const f16x8*>(K + (long)j * 64 + c * 8);
+    for (int k = 0; k < 8; ++k) pk[k] = k < KS ? pp[k * pstride] : 0.0f;
+    float acc = pk[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k)
+      if (k < KS) acc += pk[k];
+    if (part == 0) {
+      sq[e] = (float)(_Float16)((acc + bias[col]) * qscale);
+    } else if (part == 1) {
+      const _Float16 kv = (_Float16)(acc * kscale);
+      snk[e] = (float)kv;
+      K[(long)p_row * 64 + e] = kv;
+    } else {
+      const _Float16 vv = (_Float16)(acc + bias[col]);
+      snv[e] = (float)vv;
+      V[(long)p_row * 64 + e] = vv;
     }
+  }
+  __syncthreads();
+  float qv[8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+  for (int j = 0; j < 8; ++j) qv[j] = sq[c * 8 + j];
+  // scores (q.k in f32 over the f16 rows; the row appended by this launch is
+  // taken from LDS)
+  auto score_batch = [&](const f16x8* kk, int j0) {
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
       const int j = j0 + u * 8 + kg;
       float d = 0.0f;
+      if (min(j, n - 1) == jnew) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) d += qv[e] * (float)kk[u][e];
+        for (int e = 0; e < 8; ++e) d += qv[e] * snk[c * 8 + e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d += qv[e] * (float)kk[u][e];
+      }
       d += __shfl_xor(d, 1, 64);
       d += __shfl_xor(d, 2, 64);
       d += __shfl_xor(d, 4, 64);
       if (c == 0 && j < n) sc[j] = d * scale;
     }
+  };
+  for (int j0 = wid * 64; j0 < n; j0 += 512) {
+    if (j0 + 256 < n) LOADROWS(kb2, K, j0 + 256)
+    score_batch(ka, j0);
+    if (j0 + 256 >= n) break;
+    if (j0 + 512 < n) LOADROWS(ka, K, j0 + 512)
+    score_batch(kb2, j0 + 256);
   }
   __syncthreads();
   float mx = -INFINITY;
@@ -286,21 +332,30 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
   float acc[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) acc[e] = 0.0f;
-  for (int j0 = wid * 32; j0 < n; j0 += 128) {
-    f16x8 vv[4];
-    float p[4];
+  auto pv_batch = [&](const f16x8* vv, int j0) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < UB; ++u) {
       const int j = j0 + u * 8 + kg;
       const int jc = min(j, n - 1);
-      vv[u] = *reinterpret_cast<const f16x8*>(V + (long)jc * 64 + c * 8);
-      p[u] = j < n ? sc[jc] : 0.0f;
+      const float p = j < n ? sc[jc] : 0.0f;
+      if (jc == jnew) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += p * snv[c * 8 + e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += p * (float)vv[u][e];
+      }
     }
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] += p[u] * (float)vv[u][e];
+  };
+  LOADROWS(ka, V, wid * 64)
+  for (int j0 = wid * 64; j0 < n; j0 += 512) {
+    if (j0 + 256 < n) LOADROWS(kb2, V, j0 + 256)
+    pv_batch(ka, j0);
+    if (j0 + 256 >= n) break;
+    if (j0 + 512 < n) LOADROWS(ka, V, j0 + 512)
+    pv_batch(kb2, j0 + 256);
   }
+#undef LOADROWS
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     acc[e] += __shfl_xor(acc[e], 8, 64);
@@ -320,23 +375,24 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
 }
 
 template <typename T>
-void dec_attention(const _Float16* q, const _Float16* kbase, const _Float16* vbase,
-                   const int* kv_index, const int* pos, const int* active, int fixed_len,
-                   int kv_len_cap, T* o, int R, int H, float scale, hipStream_t st) {
+void dec_attention(const float* P, int KS, int pcols, const float* bias, float qscale,
+                   float kscale, _Float16* kbase, _Float16* vbase, const int* kv_index,
+                   const int* pos, const int* active, int fixed_len, int kv_len_cap, T* o, int R,
+                   int H, float scale, hipStream_t st) {
   dim3 g(H, R);
-  dec_attn_kernel<T><<<g, 256, 0, st>>>(q, kbase, vbase, kv_index, pos, active, fixed_len,
-                                        kv_len_cap, o, H, scale);
+  dec_attn_kernel<T><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale, kbase, vbase,
+                                        kv_index, pos, active, fixed_len, kv_len_cap, o, H, scale);
 }
 
 template void enc_attention<_Float16>(const _Float16*, const _Float16*, const _Float16*, _Float16*,
                                       int, int, int, float, hipStream_t);
 template void enc_attention<__bf16>(const _Float16*, const _Float16*, const _Float16*, __bf16*, int,
                                     int, int, float, hipStream_t);
-template void dec_attention<_Float16>(const _Float16*, const _Float16*, const _Float16*, const int*,
-                                      const int*, const int*, int, int, _Float16*, int, int, float,
-                                      hipStream_t);
-template void dec_attention<__bf16>(const _Float16*, const _Float16*, const _Float16*, const int*,
-                                    const int*, const int*, int, int, __bf16*, int, int, float,
-                                    hipStream_t);
+template void dec_attention<_Float16>(const float*, int, int, const float*, float, float,
+                                      _Float16*, _Float16*, const int*, const int*, const int*, int,
+                                      int, _Float16*, int, int, float, hipStream_t);
+template void dec_attention<__bf16>(const float*, int, int, const float*, float, float, _Float16*,
+                                    _Float16*, const int*, const int*, const int*, int, int,
+                                    __bf16*, int, int, float, hipStream_t);
 
 }  // namespace mwx

@@ -17,6 +17,8 @@
 //                 loaded straight to VGPRs (no LDS round trip), 4 waves split
 //                 K (or N for wide outputs), LDS reduction, one 16-column
 //                 strip per wave.
+#include <algorithm>
+
 #include "kcommon.h"
 #include "kernels.h"
 
@@ -210,22 +212,26 @@ __device__ __forceinline__ void skinny_store(const EpiParams& P, int m, int n, f
 
 template <typename T, int MT, int KCH>
 __global__ __launch_bounds__(1024) void gemm_skinny(int epi, const T* __restrict__ A, long lda,
-                                                    const T* __restrict__ W, long ldw, int M,
+                                                    const T* __restrict__ Wp, int KT, int M,
                                                     int N, EpiParams P) {
   using V8 = typename Elt<T>::v8;
   __shared__ f32x4 red[16][MT][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, NW = blockDim.x >> 6;
   const int n0 = blockIdx.x * 16;
-  const int ncol = min(n0 + (lane & 15), N - 1);
-  const int kb = wid * KCH * 32 + (lane >> 4) * 8;
-  const T* wrow = W + (long)ncol * ldw + kb;
+  // row block of 64 (grid.y): per-row arithmetic does not depend on M
+  const int m_base = blockIdx.y * 64;
+  const int Mb = min(64, M - m_base);
+  A += (long)m_base * lda;
+  const int kt0 = wid * KCH;
+  const int kb = kt0 * 32 + (lane >> 4) * 8;
+  const T* wt = Wp + ((long)blockIdx.x * KT + kt0) * 512 + lane * 8;
   V8 bfr[KCH];
   V8 afr[MT][KCH];
 #pragma unroll
-  for (int c = 0; c < KCH; ++c) bfr[c] = ld8(wrow + c * 32);
+  for (int c = 0; c < KCH; ++c) bfr[c] = ld8(wt + c * 512);
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
-    const int row = min(mt * 16 + (lane & 15), M - 1);
+    const int row = min(mt * 16 + (lane & 15), Mb - 1);
     const T* ar = A + (long)row * lda + kb;
 #pragma unroll
     for (int c = 0; c < KCH; ++c) afr[mt][c] = ld8(ar + c * 32);
@@ -250,8 +256,9 @@ __global__ __launch_bounds__(1024) void gemm_skinny(int epi, const T* __restrict
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int m = mt * 16 + (lane >> 4) * 4 + r;
-      if (m >= M) continue;
+      const int ml = mt * 16 + (lane >> 4) * 4 + r;
+      if (ml >= Mb) continue;
+      const int m = m_base + ml;
       const float v = acc[mt][r];
       switch (epi) {
         case EPI_GELU: skinny_store<EPI_GELU, T, false>(P, m, n, v); break;
@@ -282,14 +289,14 @@ static bool skinny_split(int K, int& nw, int& kch) {
 }
 
 template <typename T, int MT>
-static bool skinny_launch(int epi, const T* A, long lda, const T* W, long ldw, int M, int N, int K,
+static bool skinny_launch(int epi, const T* A, long lda, const T* Wp, int M, int N, int K,
                           const EpiParams& P, hipStream_t st) {
   int nw = 0, kch = 0;
   if (!skinny_split(K, nw, kch)) return false;
-  const dim3 g((N + 15) / 16), b(64 * nw);
+  const dim3 g((N + 15) / 16, (M + 63) / 64), b(64 * nw);
   switch (kch) {
 #define SK(C) \
-  case C: gemm_skinny<T, MT, C><<<g, b, 0, st>>>(epi, A, lda, W, ldw, M, N, P); return true;
+  case C: gemm_skinny<T, MT, C><<<g, b, 0, st>>>(epi, A, lda, Wp, K / 32, M, N, P); return true;
     SK(1) SK(2) SK(3) SK(4) SK(6) SK(8) SK(10)
 #undef SK
     default: return false;
@@ -297,21 +304,117 @@ static bool skinny_launch(int epi, const T* A, long lda, const T* W, long ldw, i
 }
 
 // ---------------------------------------------------------------------------
+// split-K decode GEMM: P[ks][m][n] = sum_{k in slice ks} A[m][k] * W[n][k]
+// (raw f32 partials, no epilogue). Grid (N/16, KS): far more workgroups than
+// 16-column strips alone, each reading only its K slice of A and W, so every
+// CU streams a small share of the weights. The KS partials are summed (in ks
+// order) by the consumer kernel together with the epilogue ggml applies
+// (bias, residual, scale, f16 rounding), so the reduction costs no launch.
+// ---------------------------------------------------------------------------
+template <typename T, int MT, int KCH>
+__global__ __launch_bounds__(256) void gemm_splitk(const T* __restrict__ A, long lda,
+                                                   const T* __restrict__ Wp, int KT, int M,
+                                                   int N, int kslice, float* __restrict__ P) {
+  using V8 = typename Elt<T>::v8;
+  __shared__ f32x4 red[4][MT][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int n0 = blockIdx.x * 16, ks = blockIdx.y;
+  const int m_base = blockIdx.z * 64;  // row block (64 rows per grid.z slice)
+  const int Mb = min(64, M - m_base);
+  A += (long)m_base * lda;
+  const int kt0 = (ks * kslice >> 5) + wid * KCH;
+  const int kb = kt0 * 32 + (lane >> 4) * 8;
+  const T* wt = Wp + ((long)blockIdx.x * KT + kt0) * 512 + lane * 8;
+  V8 bfr[KCH];
+  V8 afr[MT][KCH];
+#pragma unroll
+  for (int c = 0; c < KCH; ++c) bfr[c] = ld8(wt + c * 512);
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int row = min(mt * 16 + (lane & 15), Mb - 1);
+    const T* ar = A + (long)row * lda + kb;
+#pragma unroll
+    for (int c = 0; c < KCH; ++c) afr[mt][c] = ld8(ar + c * 32);
+  }
+  f32x4 acc[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    acc[mt] = f32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int c = 0; c < KCH; ++c) acc[mt] = Elt<T>::mfma(afr[mt][c], bfr[c], acc[mt]);
+  }
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) red[wid][mt][lane] = acc[mt];
+  __syncthreads();
+  if (wid != 0) return;
+  const int n = n0 + (lane & 15);
+  if (n >= N) return;
+  float* Pk = P + (long)ks * M * N;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const f32x4 v = (red[0][mt][lane] + red[1][mt][lane]) + (red[2][mt][lane] + red[3][mt][lane]);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = mt * 16 + (lane >> 4) * 4 + r;
+      if (m < Mb) Pk[(long)(m_base + m) * N + n] = v[r];
+    }
+  }
+}
+
+int splitk_factor(int K) {
+  if (K % 128) return 0;
+  const int S = K / 32;  // 32-deep k-steps
+  for (int ks = 8; ks >= 1; --ks)
+    if (S % ks == 0 && (S / ks) % 4 == 0 && (S / ks) / 4 <= 5) return ks;
+  return 0;
+}
+
+template <typename T>
+int gemm_splitk_partials(const T* A, long lda, const T* Wp, int M, int N, int K, float* P,
+                         hipStream_t st) {
+  const int ks = splitk_factor(K);
+  if (ks == 0) return 0;
+  const int kslice = K / ks;
+  const int kch = kslice / 128;
+  const int MT = (std::min(M, 64) + 15) / 16;
+  const dim3 g((N + 15) / 16, ks, (M + 63) / 64);
+#define SKL(MTV, C)                                                                       \
+  if (MT == MTV && kch == C) {                                                            \
+    gemm_splitk<T, MTV, C><<<g, 256, 0, st>>>(A, lda, Wp, K / 32, M, N, kslice, P);        \
+    return ks;                                                                            \
+  }
+#define SKM(MTV) SKL(MTV, 1) SKL(MTV, 2) SKL(MTV, 3) SKL(MTV, 4) SKL(MTV, 5)
+  SKM(1) SKM(2) SKM(3) SKM(4)
+#undef SKM
+#undef SKL
+  return 0;
+}
+
+template int gemm_splitk_partials<_Float16>(const _Float16*, long, const _Float16*, int, int, int,
+                                            float*, hipStream_t);
+template int gemm_splitk_partials<__bf16>(const __bf16*, long, const __bf16*, int, int, int,
+                                          float*, hipStream_t);
+
+template <typename T>
+bool gemm_decode(int epi, const T* A, long lda, const T* Wp, int M, int N, int K,
+                 const EpiParams& P, hipStream_t st) {
+  const int MT = (std::min(M, 64) + 15) / 16;
+  if (MT == 1) return skinny_launch<T, 1>(epi, A, lda, Wp, M, N, K, P, st);
+  if (MT == 2) return skinny_launch<T, 2>(epi, A, lda, Wp, M, N, K, P, st);
+  if (MT == 3) return skinny_launch<T, 3>(epi, A, lda, Wp, M, N, K, P, st);
+  return skinny_launch<T, 4>(epi, A, lda, Wp, M, N, K, P, st);
+}
+template bool gemm_decode<_Float16>(int, const _Float16*, long, const _Float16*, int, int, int,
+                                    const EpiParams&, hipStream_t);
+template bool gemm_decode<__bf16>(int, const __bf16*, long, const __bf16*, int, int, int,
+                                  const EpiParams&, hipStream_t);
+
+// ---------------------------------------------------------------------------
 // dispatch
 // ---------------------------------------------------------------------------
 template <typename T, int EPI, bool OUT16>
 static void gemm_dispatch(const T* A, long lda, long a_bstride, const T* W, long ldw, int M,
                           int N, int K, int batch, const EpiParams& P, hipStream_t st) {
-  if (batch == 1 && M <= 64 && !OUT16 && EPI != EPI_ENC_QKV && EPI != EPI_CONV2 &&
-      EPI != EPI_CROSS_KV) {
-    const int MT = (M + 15) / 16;
-    bool ok = false;
-    if (MT == 1) ok = skinny_launch<T, 1>(EPI, A, lda, W, ldw, M, N, K, P, st);
-    else if (MT == 2) ok = skinny_launch<T, 2>(EPI, A, lda, W, ldw, M, N, K, P, st);
-    else if (MT == 3) ok = skinny_launch<T, 3>(EPI, A, lda, W, ldw, M, N, K, P, st);
-    else ok = skinny_launch<T, 4>(EPI, A, lda, W, ldw, M, N, K, P, st);
-    if (ok) return;
-  }
   dim3 g((N + BN - 1) / BN, (M + BM - 1) / BM, batch);
   gemm_big<T, EPI, OUT16><<<g, 256, 0, st>>>(A, lda, a_bstride, W, ldw, M, N, K, P);
 }

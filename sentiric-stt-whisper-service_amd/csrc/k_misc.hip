@@ -14,16 +14,22 @@ namespace mwx {
 // ggml_norm (eps 1e-5, double accumulation) followed by *w + b. One 256-thread
 // workgroup per row; every element of the row is loaded once, all loads of a
 // thread are issued back to back (NPT = ceil(N / 256) registers per thread).
+//
+// With P != nullptr the row is first completed from the KS split-K partial
+// slabs of the producing GEMM: x = (sum_ks P[ks] + pbias) + x (ggml: the
+// matmul + bias, then the residual add), written back to x.
 template <typename T, int NPT>
-__global__ __launch_bounds__(256) void ln_kernel(const float* __restrict__ x,
+__global__ __launch_bounds__(256) void ln_kernel(float* __restrict__ x,
                                                  const float* __restrict__ w,
                                                  const float* __restrict__ b, T* __restrict__ y,
-                                                 int N, const int* __restrict__ active) {
+                                                 int N, const int* __restrict__ active,
+                                                 const float* __restrict__ P, int KS,
+                                                 long pstride, const float* __restrict__ pbias) {
   __shared__ double red[2][4];
   const int row = blockIdx.x;
   if (active && !active[row]) return;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const float* xr = x + (long)row * N;
+  float* xr = x + (long)row * N;
   float v[NPT], wv[NPT], bv[NPT];
 #pragma unroll
   for (int j = 0; j < NPT; ++j) {
@@ -31,6 +37,29 @@ __global__ __launch_bounds__(256) void ln_kernel(const float* __restrict__ x,
     v[j] = i < N ? xr[i] : 0.0f;
     wv[j] = i < N ? w[i] : 0.0f;
     bv[j] = i < N ? b[i] : 0.0f;
+  }
+  if (P) {
+    // all KS (<= 8) partials of all NPT elements are loaded before summing
+    float pk[NPT][8];
+#pragma unroll
+    for (int j = 0; j < NPT; ++j) {
+      const int i = min(tid + 256 * j, N - 1);
+      const float* pp = P + (long)row * N + i;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) pk[j][k] = k < KS ? pp[k * pstride] : 0.0f;
+    }
+#pragma unroll
+    for (int j = 0; j < NPT; ++j) {
+      const int i = tid + 256 * j;
+      float acc = pk[j][0];
+#pragma unroll
+      for (int k = 1; k < 8; ++k)
+        if (k < KS) acc += pk[j][k];
+      if (i < N) {
+        v[j] = (acc + pbias[i]) + v[j];
+        xr[i] = v[j];
+      }
+    }
   }
   double s = 0.0;
 #pragma unroll
@@ -63,11 +92,14 @@ __global__ __launch_bounds__(256) void ln_kernel(const float* __restrict__ x,
 
 template <typename T>
 void layer_norm(const float* x, const float* w, const float* b, T* y, int M, int N,
-                const int* active, hipStream_t st) {
+                const int* active, hipStream_t st, const float* P, int KS, const float* pbias) {
   const int npt = (N + 255) / 256;
+  const long pstride = (long)M * N;
   switch (npt) {
-#define LNC(K) \
-  case K: ln_kernel<T, K><<<M, 256, 0, st>>>(x, w, b, y, N, active); break;
+#define LNC(K)                                                                               \
+  case K:                                                                                    \
+    ln_kernel<T, K><<<M, 256, 0, st>>>((float*)x, w, b, y, N, active, P, KS, pstride, pbias); \
+    break;
     LNC(1) LNC(2) LNC(3) LNC(4) LNC(5) LNC(6) LNC(7) LNC(8)
 #undef LNC
     default: break;
@@ -96,9 +128,9 @@ void embed(const T* te, const float* pe, const int* tok, const int* pos, const i
 }
 
 template void layer_norm<_Float16>(const float*, const float*, const float*, _Float16*, int, int,
-                                   const int*, hipStream_t);
+                                   const int*, hipStream_t, const float*, int, const float*);
 template void layer_norm<__bf16>(const float*, const float*, const float*, __bf16*, int, int,
-                                 const int*, hipStream_t);
+                                 const int*, hipStream_t, const float*, int, const float*);
 template void embed<_Float16>(const _Float16*, const float*, const int*, const int*, const int*,
                               float*, int, int, hipStream_t);
 template void embed<__bf16>(const __bf16*, const float*, const int*, const int*, const int*, float*,

@@ -43,11 +43,36 @@ struct EpiParams {
   float qscale = 1.0f;
 };
 
+// Decode weights live in HBM as MFMA fragment tiles: for each 16-column strip
+// nt and 32-deep k-step kt, the 16x32 block is 1 KB contiguous in the order the
+// 64 lanes of a wave consume it (lane = (k%32/8)*16 + n%16, 8 elements per
+// lane), so one wave-wide 16-B-per-lane load is one fully used 1-KB burst.
+// Rows are zero-padded to a multiple of 16.
+__host__ __device__ inline long pack_index(long n, long k, long K) {
+  const long nt = n >> 4, c = n & 15, kt = k >> 5, kk = k & 31;
+  return ((nt * (K >> 5) + kt) * 64 + (kk >> 3) * 16 + c) * 8 + (kk & 7);
+}
+
 // T = _Float16 or __bf16 (model weight type). `OutT16` selects the 16-bit
 // output type of EPI_GELU (f16 for conv1, T for FFN1).
 template <typename T>
 void gemm(int epi, bool out_f16, const T* A, long lda, long a_bstride, const T* W, long ldw,
           int M, int N, int K, int batch, const EpiParams& P, hipStream_t st);
+
+// Decode split-K GEMM over fragment-tiled weights Wp (pack_index): writes KS
+// f32 partial slabs P[KS][M][N] (no epilogue) and returns KS (0 if the shape is
+// unsupported). The consumer kernel sums the slabs and applies the epilogue.
+int splitk_factor(int K);
+template <typename T>
+int gemm_splitk_partials(const T* A, long lda, const T* Wp, int M, int N, int K, float* P,
+                         hipStream_t st);
+// Decode full-K GEMM over fragment-tiled weights with a fused epilogue
+// (EPI_GELU / EPI_RES / EPI_F32 / EPI_STORE16 / EPI_DEC_QKV), rows in blocks of
+// 64 so a row's arithmetic does not depend on the batch. Returns false if K is
+// unsupported.
+template <typename T>
+bool gemm_decode(int epi, const T* A, long lda, const T* Wp, int M, int N, int K,
+                 const EpiParams& P, hipStream_t st);
 
 void launch_mel(const float* pcm, int n, int n_len, int n_fft_frames, const float* filters,
                 int n_mels, const float* tables, float* out, hipStream_t st);
@@ -58,9 +83,12 @@ void launch_mel_window(const float* mel, long mel_clip_stride, const int* clip_o
                        int cpad, _Float16* melT, int n_slots, hipStream_t st);
 void launch_signal_energy(const float* x, int n, float* out, hipStream_t st);
 
+// LayerNorm of x rows into y. With P != nullptr, x is first completed from
+// the KS split-K partial slabs P[KS][M][N]: x = (sum P + pbias) + x.
 template <typename T>
 void layer_norm(const float* x, const float* w, const float* b, T* y, int M, int N,
-                const int* active, hipStream_t st);
+                const int* active, hipStream_t st, const float* P = nullptr, int KS = 0,
+                const float* pbias = nullptr);
 template <typename T>
 void embed(const T* te, const float* pe, const int* tok, const int* pos, const int* active,
            float* x, int R, int d, hipStream_t st);
@@ -73,10 +101,16 @@ void enc_attention(const _Float16* q, const _Float16* k, const _Float16* vt, T* 
 // decode attention for R rows: q [R][H*64] f16; K/V rows [n_keys][64] per
 // (row, head). self: K = kbase + ((row*H + h)*kstride_rows)*64, n_keys =
 // pos[row] + 1. cross: K = kbase + ((clip[row]*H + h)*L)*64, n_keys = L.
+// The query of (row, head) is reduced from the producing split-K GEMM's
+// slabs P[KS][R][pcols] (q = f16((sum P + bias) * qscale), columns h*64..).
+// self (fixed_len == 0): the slabs hold Q|K|V (pcols = 3d); the kernel also
+// forms k = f16(sum * kscale), v = f16(sum + bias) for the row's position and
+// appends them to the KV cache before attending over positions 0..pos.
 template <typename T>
-void dec_attention(const _Float16* q, const _Float16* kbase, const _Float16* vbase,
-                   const int* kv_index, const int* pos, const int* active, int fixed_len,
-                   int kv_len_cap, T* o, int R, int H, float scale, hipStream_t st);
+void dec_attention(const float* P, int KS, int pcols, const float* bias, float qscale,
+                   float kscale, _Float16* kbase, _Float16* vbase, const int* kv_index,
+                   const int* pos, const int* active, int fixed_len, int kv_len_cap, T* o, int R,
+                   int H, float scale, hipStream_t st);
 
 struct RowCtl {
   int active;        // row participates in this step

@@ -250,9 +250,13 @@ class Context:
                                          len(pcm))
 
     def full_batch(self, pcms: Sequence[np.ndarray], params: FullParams) -> int:
+        return self.full_batch_states(pcms, params, range(len(pcms)))
+
+    def full_batch_states(self, pcms: Sequence[np.ndarray], params: FullParams,
+                          state_indices: Sequence[int]) -> int:
         n = len(pcms)
         arrs = [np.ascontiguousarray(p, dtype=np.float32) for p in pcms]
-        states = (C.c_void_p * n)(*[self.state(i) for i in range(n)])
+        states = (C.c_void_p * n)(*[self.state(i) for i in state_indices])
         ptrs = (C.POINTER(C.c_float) * n)(*[fptr(a) for a in arrs])
         lens = (C.c_int * n)(*[len(a) for a in arrs])
         self._keep = arrs

@@ -185,3 +185,22 @@ def test_bench_fixed_steps_workload(micro):
     p.bench_fixed_steps = 40
     assert ctx.full(pcm_clip(0), p) == 0
     assert sum(len(s.tokens) for s in ctx.segments()) == 40
+
+
+def test_fallback_batch_over_64_rows_equals_single(micro):
+    """Temperature fallback on 14 clips at once runs 14 x best_of(5) = 70
+    decoder rows (row blocks > 64 in every split-K GEMM); each clip must decode
+    exactly as when it runs alone (5 rows)."""
+    ctx, o, _ = micro
+    # decoder 0's std::mt19937 lives in the state (whisper_init_state) and
+    # advances with every sampled token, so batch and singles use fresh states
+    p = service_params(ctx, language=b"en")
+    pcms = [pcm_clip(20 + k, 8.0 + k) for k in range(14)]
+    base = len(ctx.states)
+    assert ctx.full_batch_states(pcms, p, range(base, base + 14)) == 0
+    batched = [mwx.token_ids(ctx.segments(base + i)) for i in range(14)]
+    singles = []
+    for i, pcm in enumerate(pcms):
+        assert ctx.full(pcm, p, state_index=base + 14 + i) == 0
+        singles.append(mwx.token_ids(ctx.segments(base + 14 + i)))
+    assert batched == singles
