@@ -118,6 +118,7 @@ struct State {
   // decoder workspace (row-batched)
   DBuf xd, hd, qd, od, ffd, logits, kself, vself, stepin, ctl, tokout, probs, logprobs, smask;
   DBuf pqkv, pres, pq;  // split-K partial slabs of the decode GEMMs
+  DBuf lpflt, lpparts, lpres;  // logits-processing scratch
   int cross_cap = 0;  // cross cache slots
   int row_cap = 0;    // self cache rows
   std::vector<Segment> result_all;
@@ -679,11 +680,15 @@ struct Driver {
     S.pres.get((size_t)8 * R * d * 4);
     S.pq.get((size_t)8 * R * d * 4);
     S.xd.get((size_t)R * d * 4, true);
-    S.hd.get((size_t)R * d * sizeof(T), true);
-    S.qd.get((size_t)R * d * 2, true);
-    S.od.get((size_t)R * d * sizeof(T), true);
-    S.ffd.get((size_t)R * 4 * d * sizeof(T), true);
+    // decode-GEMM A operands (fragment tiles), rows padded to the 64-row block
+    const size_t R64 = (size_t)(R + 63) / 64 * 64;
+    S.hd.get(R64 * d * sizeof(T), true);
+    S.od.get(R64 * d * sizeof(T), true);
+    S.ffd.get(R64 * 4 * d * sizeof(T), true);
     S.logits.get((size_t)R * V * 4);
+    S.lpflt.get((size_t)R * V * 4);
+    S.lpparts.get((size_t)R * LP_G * sizeof(LPPart));
+    S.lpres.get((size_t)R * LP_G * sizeof(LPRes));
     S.stepin.get((size_t)R * 4 * 4);
     S.ctl.get((size_t)R * sizeof(RowCtl));
     S.tokout.get((size_t)R * sizeof(TokOut));
@@ -698,7 +703,6 @@ struct Driver {
     const int* xidx = si + 3 * R;
     float* xd = (float*)S.xd.p;
     T* hd = (T*)S.hd.p;
-    _Float16* qd = (_Float16*)S.qd.p;
     T* od = (T*)S.od.p;
     T* ffd = (T*)S.ffd.p;
     const float kqs = powf(64.0f, -0.25f);
@@ -717,21 +721,21 @@ struct Driver {
       const DecLayerW& W = C.dec[l];
       _Float16* ks = (_Float16*)S.kself.p + l * layer_self;
       _Float16* vs = (_Float16*)S.vself.p + l * layer_self;
-      layer_norm<T>(xd, W.ln1_w, W.ln1_b, hd, R, d, act, st, ks_prev ? Pres : nullptr, ks_prev,
-                    bias_prev);
+      layer_norm_dec<T>(xd, W.ln1_w, W.ln1_b, hd, R, d, act, st, ks_prev ? Pres : nullptr,
+                        ks_prev, bias_prev);
       int k1;
       { PerfScope ps(S, "dec_gemm");
-        k1 = gemm_splitk_partials<T>(hd, d, Wt(W.qkv_w), R, 3 * d, d, Pqkv, st); }
+        k1 = gemm_splitk_partials<T>(hd, Wt(W.qkv_w), R, 3 * d, d, Pqkv, st); }
       { PerfScope ps(S, "dec_attn_self");
         dec_attention<T>(Pqkv, k1, 3 * d, W.qkv_b, kqs, kqs, ks, vs, nullptr, pos, act, 0, Tctx,
                          od, R, H, 1.0f, st); }
       int k2;
       { PerfScope ps(S, "dec_gemm");
-        k2 = gemm_splitk_partials<T>(od, d, Wt(W.o_w), R, d, d, Pres, st); }
-      layer_norm<T>(xd, W.lnc_w, W.lnc_b, hd, R, d, act, st, Pres, k2, W.o_b);
+        k2 = gemm_splitk_partials<T>(od, Wt(W.o_w), R, d, d, Pres, st); }
+      layer_norm_dec<T>(xd, W.lnc_w, W.lnc_b, hd, R, d, act, st, Pres, k2, W.o_b);
       int k3;
       { PerfScope ps(S, "dec_gemm");
-        k3 = gemm_splitk_partials<T>(hd, d, Wt(W.cq_w), R, d, d, Pq, st); }
+        k3 = gemm_splitk_partials<T>(hd, Wt(W.cq_w), R, d, d, Pq, st); }
       { PerfScope ps(S, "dec_attn_cross");
         dec_attention<T>(Pq, k3, d, W.cq_b, 1.0f, 1.0f,
                          (_Float16*)S.cross_k.p + l * layer_cross,
@@ -739,26 +743,27 @@ struct Driver {
                          hp.n_audio_ctx, hp.n_audio_ctx, od, R, H, kqs, st); }
       int k4;
       { PerfScope ps(S, "dec_gemm");
-        k4 = gemm_splitk_partials<T>(od, d, Wt(W.co_w), R, d, d, Pres, st); }
-      layer_norm<T>(xd, W.ln2_w, W.ln2_b, hd, R, d, act, st, Pres, k4, W.co_b);
+        k4 = gemm_splitk_partials<T>(od, Wt(W.co_w), R, d, d, Pres, st); }
+      layer_norm_dec<T>(xd, W.ln2_w, W.ln2_b, hd, R, d, act, st, Pres, k4, W.co_b);
       EpiParams e;
       e.bias = W.fc1_b;
       e.c16 = ffd;
       e.ldc = 4 * d;
+      e.pack_out = true;
       bool k5;
       { PerfScope ps(S, "dec_gemm");
-        k5 = gemm_decode<T>(EPI_GELU, hd, d, Wt(W.fc1_w), R, 4 * d, d, e, st); }
+        k5 = gemm_decode<T>(EPI_GELU, hd, Wt(W.fc1_w), R, 4 * d, d, e, st); }
       { PerfScope ps(S, "dec_gemm");
-        ks_prev = gemm_splitk_partials<T>(ffd, 4 * d, Wt(W.fc2_w), R, d, 4 * d, Pres, st); }
+        ks_prev = gemm_splitk_partials<T>(ffd, Wt(W.fc2_w), R, d, 4 * d, Pres, st); }
       bias_prev = W.fc2_b;
       if (!k1 || !k2 || !k3 || !k4 || !k5 || !ks_prev) throw std::runtime_error("mwx: unsupported split-K shape");
     }
-    layer_norm<T>(xd, C.dec_ln_w, C.dec_ln_b, hd, R, d, act, st, Pres, ks_prev, bias_prev);
+    layer_norm_dec<T>(xd, C.dec_ln_w, C.dec_ln_b, hd, R, d, act, st, Pres, ks_prev, bias_prev);
     EpiParams e;
     e.c32 = (float*)S.logits.p;
     e.ldc = V;
     { PerfScope ps(S, "logits_gemm");
-    if (!gemm_decode<T>(EPI_F32, hd, d, Wt(C.tok_emb_p), R, V, d, e, st))
+    if (!gemm_decode<T>(EPI_F32, hd, Wt(C.tok_emb_p), R, V, d, e, st))
       throw std::runtime_error("mwx: unsupported logits GEMM shape"); }
     float* pr = nullptr;
     float* lp = nullptr;
@@ -768,7 +773,8 @@ struct Driver {
     }
     PerfScope ps(S, "logits_proc");
     logits_process((float*)S.logits.p, (const float*)S.smask.p, (const RowCtl*)S.ctl.p,
-                   (TokOut*)S.tokout.p, pr, lp, LC, R, st);
+                   (TokOut*)S.tokout.p, pr, lp, LC, R,
+                   LPScratch{(float*)S.lpflt.p, (LPPart*)S.lpparts.p, (LPRes*)S.lpres.p}, st);
   }
 };
 

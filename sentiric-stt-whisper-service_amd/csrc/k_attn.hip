@@ -370,7 +370,7 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
   if (tid < 64) {
     const int cc = tid >> 3, e = tid & 7;
     const float r = (pv[0][cc][e] + pv[1][cc][e]) + (pv[2][cc][e] + pv[3][cc][e]);
-    o[(long)row * D + h * 64 + cc * 8 + e] = to_t<T>(r);
+    o[pack_index(row, h * 64 + cc * 8 + e, D)] = to_t<T>(r);
   }
 }
 

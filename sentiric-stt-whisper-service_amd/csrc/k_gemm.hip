@@ -41,7 +41,8 @@ __device__ __forceinline__ void epi_store(const EpiParams& P, int bz, int m, int
       P.v[(((long)b * P.H + h) * 64 + e) * P.ldv + t] = hv;
   } else if constexpr (EPI == EPI_GELU) {
     const float g = gelu_ggml(acc + P.bias[n]);
-    const long idx = (long)bz * P.c_bstride + (long)m * P.ldc + n;
+    const long idx = P.pack_out ? pack_index(m, n, P.ldc)
+                                : (long)bz * P.c_bstride + (long)m * P.ldc + n;
     if constexpr (OUT16)
       ((_Float16*)P.c16)[idx] = (_Float16)g;
     else
@@ -211,7 +212,7 @@ __device__ __forceinline__ void skinny_store(const EpiParams& P, int m, int n, f
 }
 
 template <typename T, int MT, int KCH>
-__global__ __launch_bounds__(1024) void gemm_skinny(int epi, const T* __restrict__ A, long lda,
+__global__ __launch_bounds__(1024) void gemm_skinny(int epi, const T* __restrict__ Ap,
                                                     const T* __restrict__ Wp, int KT, int M,
                                                     int N, EpiParams P) {
   using V8 = typename Elt<T>::v8;
@@ -221,21 +222,17 @@ __global__ __launch_bounds__(1024) void gemm_skinny(int epi, const T* __restrict
   // row block of 64 (grid.y): per-row arithmetic does not depend on M
   const int m_base = blockIdx.y * 64;
   const int Mb = min(64, M - m_base);
-  A += (long)m_base * lda;
   const int kt0 = wid * KCH;
-  const int kb = kt0 * 32 + (lane >> 4) * 8;
   const T* wt = Wp + ((long)blockIdx.x * KT + kt0) * 512 + lane * 8;
+  const T* at = Ap + ((long)(blockIdx.y * 4) * KT + kt0) * 512 + lane * 8;
   V8 bfr[KCH];
   V8 afr[MT][KCH];
 #pragma unroll
   for (int c = 0; c < KCH; ++c) bfr[c] = ld8(wt + c * 512);
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    const int row = min(mt * 16 + (lane & 15), Mb - 1);
-    const T* ar = A + (long)row * lda + kb;
+  for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-    for (int c = 0; c < KCH; ++c) afr[mt][c] = ld8(ar + c * 32);
-  }
+    for (int c = 0; c < KCH; ++c) afr[mt][c] = ld8(at + ((long)mt * KT + c) * 512);
   f32x4 acc[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
@@ -289,14 +286,14 @@ static bool skinny_split(int K, int& nw, int& kch) {
 }
 
 template <typename T, int MT>
-static bool skinny_launch(int epi, const T* A, long lda, const T* Wp, int M, int N, int K,
+static bool skinny_launch(int epi, const T* Ap, const T* Wp, int M, int N, int K,
                           const EpiParams& P, hipStream_t st) {
   int nw = 0, kch = 0;
   if (!skinny_split(K, nw, kch)) return false;
   const dim3 g((N + 15) / 16, (M + 63) / 64), b(64 * nw);
   switch (kch) {
 #define SK(C) \
-  case C: gemm_skinny<T, MT, C><<<g, b, 0, st>>>(epi, A, lda, Wp, K / 32, M, N, P); return true;
+  case C: gemm_skinny<T, MT, C><<<g, b, 0, st>>>(epi, Ap, Wp, K / 32, M, N, P); return true;
     SK(1) SK(2) SK(3) SK(4) SK(6) SK(8) SK(10)
 #undef SK
     default: return false;
@@ -312,7 +309,7 @@ static bool skinny_launch(int epi, const T* A, long lda, const T* Wp, int M, int
 // (bias, residual, scale, f16 rounding), so the reduction costs no launch.
 // ---------------------------------------------------------------------------
 template <typename T, int MT, int KCH>
-__global__ __launch_bounds__(256) void gemm_splitk(const T* __restrict__ A, long lda,
+__global__ __launch_bounds__(256) void gemm_splitk(const T* __restrict__ Ap,
                                                    const T* __restrict__ Wp, int KT, int M,
                                                    int N, int kslice, float* __restrict__ P) {
   using V8 = typename Elt<T>::v8;
@@ -321,21 +318,17 @@ __global__ __launch_bounds__(256) void gemm_splitk(const T* __restrict__ A, long
   const int n0 = blockIdx.x * 16, ks = blockIdx.y;
   const int m_base = blockIdx.z * 64;  // row block (64 rows per grid.z slice)
   const int Mb = min(64, M - m_base);
-  A += (long)m_base * lda;
   const int kt0 = (ks * kslice >> 5) + wid * KCH;
-  const int kb = kt0 * 32 + (lane >> 4) * 8;
   const T* wt = Wp + ((long)blockIdx.x * KT + kt0) * 512 + lane * 8;
+  const T* at = Ap + ((long)(blockIdx.z * 4) * KT + kt0) * 512 + lane * 8;
   V8 bfr[KCH];
   V8 afr[MT][KCH];
 #pragma unroll
   for (int c = 0; c < KCH; ++c) bfr[c] = ld8(wt + c * 512);
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    const int row = min(mt * 16 + (lane & 15), Mb - 1);
-    const T* ar = A + (long)row * lda + kb;
+  for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-    for (int c = 0; c < KCH; ++c) afr[mt][c] = ld8(ar + c * 32);
-  }
+    for (int c = 0; c < KCH; ++c) afr[mt][c] = ld8(at + ((long)mt * KT + c) * 512);
   f32x4 acc[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
@@ -370,7 +363,7 @@ int splitk_factor(int K) {
 }
 
 template <typename T>
-int gemm_splitk_partials(const T* A, long lda, const T* Wp, int M, int N, int K, float* P,
+int gemm_splitk_partials(const T* Ap, const T* Wp, int M, int N, int K, float* P,
                          hipStream_t st) {
   const int ks = splitk_factor(K);
   if (ks == 0) return 0;
@@ -380,7 +373,7 @@ int gemm_splitk_partials(const T* A, long lda, const T* Wp, int M, int N, int K,
   const dim3 g((N + 15) / 16, ks, (M + 63) / 64);
 #define SKL(MTV, C)                                                                       \
   if (MT == MTV && kch == C) {                                                            \
-    gemm_splitk<T, MTV, C><<<g, 256, 0, st>>>(A, lda, Wp, K / 32, M, N, kslice, P);        \
+    gemm_splitk<T, MTV, C><<<g, 256, 0, st>>>(Ap, Wp, K / 32, M, N, kslice, P);        \
     return ks;                                                                            \
   }
 #define SKM(MTV) SKL(MTV, 1) SKL(MTV, 2) SKL(MTV, 3) SKL(MTV, 4) SKL(MTV, 5)
@@ -390,23 +383,23 @@ int gemm_splitk_partials(const T* A, long lda, const T* Wp, int M, int N, int K,
   return 0;
 }
 
-template int gemm_splitk_partials<_Float16>(const _Float16*, long, const _Float16*, int, int, int,
-                                            float*, hipStream_t);
-template int gemm_splitk_partials<__bf16>(const __bf16*, long, const __bf16*, int, int, int,
-                                          float*, hipStream_t);
+template int gemm_splitk_partials<_Float16>(const _Float16*, const _Float16*, int, int, int, float*,
+                                            hipStream_t);
+template int gemm_splitk_partials<__bf16>(const __bf16*, const __bf16*, int, int, int, float*,
+                                          hipStream_t);
 
 template <typename T>
-bool gemm_decode(int epi, const T* A, long lda, const T* Wp, int M, int N, int K,
-                 const EpiParams& P, hipStream_t st) {
+bool gemm_decode(int epi, const T* Ap, const T* Wp, int M, int N, int K, const EpiParams& P,
+                 hipStream_t st) {
   const int MT = (std::min(M, 64) + 15) / 16;
-  if (MT == 1) return skinny_launch<T, 1>(epi, A, lda, Wp, M, N, K, P, st);
-  if (MT == 2) return skinny_launch<T, 2>(epi, A, lda, Wp, M, N, K, P, st);
-  if (MT == 3) return skinny_launch<T, 3>(epi, A, lda, Wp, M, N, K, P, st);
-  return skinny_launch<T, 4>(epi, A, lda, Wp, M, N, K, P, st);
+  if (MT == 1) return skinny_launch<T, 1>(epi, Ap, Wp, M, N, K, P, st);
+  if (MT == 2) return skinny_launch<T, 2>(epi, Ap, Wp, M, N, K, P, st);
+  if (MT == 3) return skinny_launch<T, 3>(epi, Ap, Wp, M, N, K, P, st);
+  return skinny_launch<T, 4>(epi, Ap, Wp, M, N, K, P, st);
 }
-template bool gemm_decode<_Float16>(int, const _Float16*, long, const _Float16*, int, int, int,
+template bool gemm_decode<_Float16>(int, const _Float16*, const _Float16*, int, int, int,
                                     const EpiParams&, hipStream_t);
-template bool gemm_decode<__bf16>(int, const __bf16*, long, const __bf16*, int, int, int,
+template bool gemm_decode<__bf16>(int, const __bf16*, const __bf16*, int, int, int,
                                   const EpiParams&, hipStream_t);
 
 // ---------------------------------------------------------------------------

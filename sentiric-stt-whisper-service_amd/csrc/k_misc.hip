@@ -6,6 +6,8 @@
 // 32-byte token record per row crosses PCIe per step. One 1024-thread
 // workgroup per row keeps the row in registers (51 values per thread) and
 // does every pass with wave-shuffle + LDS reductions.
+#include <type_traits>
+
 #include "kcommon.h"
 #include "kernels.h"
 
@@ -106,6 +108,98 @@ void layer_norm(const float* x, const float* w, const float* b, T* y, int M, int
   }
 }
 
+// Decode LayerNorm (same arithmetic as ln_kernel) for the few rows of a
+// decode step: each thread owns 8 consecutive elements, so all loads are
+// 16-B vectors, and the normalised row is stored as 16-B pieces of the
+// decode-GEMM A tiles (pack_index).
+template <typename T>
+__global__ __launch_bounds__(256) void ln_dec_kernel(float* __restrict__ x,
+                                                     const float* __restrict__ w,
+                                                     const float* __restrict__ b,
+                                                     T* __restrict__ y, int N,
+                                                     const int* __restrict__ active,
+                                                     const float* __restrict__ P, int KS,
+                                                     long pstride,
+                                                     const float* __restrict__ pbias) {
+  __shared__ double red[2][4];
+  const int row = blockIdx.x;
+  if (active && !active[row]) return;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const bool own = tid * 8 < N;
+  const int i0 = own ? tid * 8 : 0;
+  float* xr = x + (long)row * N + i0;
+  float v[8];
+  {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(xr);
+    const f32x4 c = *reinterpret_cast<const f32x4*>(xr + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] = a[e];
+      v[4 + e] = c[e];
+    }
+  }
+  if (P) {
+    f32x4 pk[8][2];
+    const float* pp = P + (long)row * N + i0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (k < KS) {
+        pk[k][0] = *reinterpret_cast<const f32x4*>(pp + k * pstride);
+        pk[k][1] = *reinterpret_cast<const f32x4*>(pp + k * pstride + 4);
+      }
+    const f32x4 pb0 = *reinterpret_cast<const f32x4*>(pbias + i0);
+    const f32x4 pb1 = *reinterpret_cast<const f32x4*>(pbias + i0 + 4);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float acc = pk[0][e >> 2][e & 3];
+#pragma unroll
+      for (int k = 1; k < 8; ++k)
+        if (k < KS) acc += pk[k][e >> 2][e & 3];
+      v[e] = (acc + (e < 4 ? pb0[e] : pb1[e - 4])) + v[e];
+    }
+    if (own) {
+      *reinterpret_cast<f32x4*>(xr) = f32x4{v[0], v[1], v[2], v[3]};
+      *reinterpret_cast<f32x4*>(xr + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    }
+  }
+  double s = 0.0;
+  if (own) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += (double)v[e];
+  }
+  s = wave_sum_d(s);
+  if (lane == 0) red[0][wid] = s;
+  __syncthreads();
+  s = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+  const float mean = (float)(s / N);
+  double s2 = 0.0;
+  if (own) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float d = v[e] - mean;
+      s2 += (double)(d * d);
+    }
+  }
+  s2 = wave_sum_d(s2);
+  if (lane == 0) red[1][wid] = s2;
+  __syncthreads();
+  if (!own) return;
+  s2 = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+  const float variance = (float)(s2 / N);
+  const float scale = 1.0f / sqrtf(variance + 1e-5f);
+  typename Elt<T>::v8 o;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = to_t<T>(((v[e] - mean) * scale) * w[i0 + e] + b[i0 + e]);
+  *reinterpret_cast<typename Elt<T>::v8*>(y + pack_index(row, i0, N)) = o;
+}
+
+template <typename T>
+void layer_norm_dec(float* x, const float* w, const float* b, T* y, int M, int N,
+                    const int* active, hipStream_t st, const float* P, int KS,
+                    const float* pbias) {
+  ln_dec_kernel<T><<<M, 256, 0, st>>>(x, w, b, y, N, active, P, KS, (long)M * N, pbias);
+}
+
 // x[r] = te[tok[r]] + pe[pos[r]]   (ggml_get_rows(d_te) + ggml_get_rows(d_pe))
 template <typename T>
 __global__ __launch_bounds__(256) void embed_kernel(const T* __restrict__ te,
@@ -131,6 +225,10 @@ template void layer_norm<_Float16>(const float*, const float*, const float*, _Fl
                                    const int*, hipStream_t, const float*, int, const float*);
 template void layer_norm<__bf16>(const float*, const float*, const float*, __bf16*, int, int,
                                  const int*, hipStream_t, const float*, int, const float*);
+template void layer_norm_dec<_Float16>(float*, const float*, const float*, _Float16*, int, int,
+                                       const int*, hipStream_t, const float*, int, const float*);
+template void layer_norm_dec<__bf16>(float*, const float*, const float*, __bf16*, int, int,
+                                     const int*, hipStream_t, const float*, int, const float*);
 template void embed<_Float16>(const _Float16*, const float*, const int*, const int*, const int*,
                               float*, int, int, hipStream_t);
 template void embed<__bf16>(const __bf16*, const float*, const int*, const int*, const int*, float*,
@@ -138,121 +236,101 @@ template void embed<__bf16>(const __bf16*, const float*, const int*, const int*,
 
 // ---------------------------------------------------------------------------
 // logits processing + greedy sampling
+//
+// Each row is split over LP_G chunk workgroups so the exp/compare passes run
+// on LP_G x rows CUs instead of one CU per row:
+//   phase 1: filter (temperature, suppression, timestamp rules) -> flt, and
+//            per-chunk max / sum-exp statistics;
+//   phase 2: combine the chunk statistics (lse, timestamp log-prob, text max
+//            -> the "force timestamp" rule), probs = expf(logprob), per-chunk
+//            argmax / timestamp argmax / timestamp prob sum;
+//   phase 3: combine the chunks in index order (lowest-index tie break).
 // ---------------------------------------------------------------------------
-constexpr int LP_T = 1024;
-constexpr int LP_NPT = 51;  // 51 * 1024 = 52224 >= 51866
+constexpr int LP_T = 256;
+constexpr int LP_NPT = (LP_CHUNK + LP_T - 1) / LP_T;
 
-struct BlockRed {
-  float f[16];
-  double d[16];
-  int i[16];
-};
+template <int I, int N, typename F>
+__device__ __forceinline__ void sfor(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    sfor<I + 1, N>(f);
+  }
+}
 
-__device__ __forceinline__ float bmax(float v, BlockRed& R) {
+__device__ __forceinline__ float bmax256(float v, float* red) {
   v = wave_max(v);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   __syncthreads();
-  if (lane == 0) R.f[wid] = v;
+  if (lane == 0) red[wid] = v;
   __syncthreads();
-  float r = R.f[0];
-#pragma unroll
-  for (int k = 1; k < 16; ++k) r = fmaxf(r, R.f[k]);
-  return r;
+  return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 }
-__device__ __forceinline__ float bsum(float v, BlockRed& R) {
+__device__ __forceinline__ float bsum256(float v, float* red) {
   v = wave_sum(v);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   __syncthreads();
-  if (lane == 0) R.f[wid] = v;
+  if (lane == 0) red[wid] = v;
   __syncthreads();
-  float r = 0.0f;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) r += R.f[k];
-  return r;
+  return (red[0] + red[1]) + (red[2] + red[3]);
 }
-__device__ __forceinline__ double bsumd(double v, BlockRed& R) {
+__device__ __forceinline__ double bsum256d(double v, double* red) {
   v = wave_sum_d(v);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   __syncthreads();
-  if (lane == 0) R.d[wid] = v;
+  if (lane == 0) red[wid] = v;
   __syncthreads();
-  double r = 0.0;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) r += R.d[k];
-  return r;
+  return (red[0] + red[1]) + (red[2] + red[3]);
 }
-// argmax with lowest-index tie break; entries with v <= floor never win
-__device__ __forceinline__ void bargmax(float& v, int& idx, BlockRed& R) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float ov = __shfl_xor(v, o, 64);
-    const int oi = __shfl_xor(idx, o, 64);
-    if (ov > v || (ov == v && oi < idx)) {
-      v = ov;
-      idx = oi;
-    }
+// argmax with lowest-index tie break
+__device__ __forceinline__ void better(float& v, int& idx, float ov, int oi) {
+  if (ov > v || (ov == v && oi < idx)) {
+    v = ov;
+    idx = oi;
   }
+}
+__device__ __forceinline__ void bargmax256(float& v, int& idx, float* redf, int* redi) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) better(v, idx, __shfl_xor(v, o, 64), __shfl_xor(idx, o, 64));
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   __syncthreads();
   if (lane == 0) {
-    R.f[wid] = v;
-    R.i[wid] = idx;
+    redf[wid] = v;
+    redi[wid] = idx;
   }
   __syncthreads();
-  v = R.f[0];
-  idx = R.i[0];
+  v = redf[0];
+  idx = redi[0];
 #pragma unroll
-  for (int k = 1; k < 16; ++k) {
-    if (R.f[k] > v || (R.f[k] == v && R.i[k] < idx)) {
-      v = R.f[k];
-      idx = R.i[k];
-    }
-  }
+  for (int k = 1; k < 4; ++k) better(v, idx, redf[k], redi[k]);
 }
 
-__global__ __launch_bounds__(LP_T) void logits_process_kernel(
-    const float* __restrict__ logits, const float* __restrict__ smask,
-    const RowCtl* __restrict__ ctl, TokOut* __restrict__ out, float* __restrict__ probs_out,
-    float* __restrict__ logprobs_out, LogitsConst C, int nosp_id) {
-  __shared__ BlockRed R;
-  const int row = blockIdx.x;
+__global__ __launch_bounds__(LP_T) void lp_filter_kernel(const float* __restrict__ logits,
+                                                         const float* __restrict__ smask,
+                                                         const RowCtl* __restrict__ ctl,
+                                                         float* __restrict__ flt,
+                                                         LPPart* __restrict__ parts,
+                                                         LogitsConst C) {
+  __shared__ float red[4];
+  const int row = blockIdx.y, ch = blockIdx.x;
   const RowCtl c = ctl[row];
   if (!c.active || !c.sample) return;
-  const int V = C.n_vocab;
-  const int tid = threadIdx.x;
+  const int V = C.n_vocab, tid = threadIdx.x;
+  const int base = ch * LP_CHUNK;
   const float* L = logits + (long)row * V;
-  float x[LP_NPT];
-  float rmax = -INFINITY;
-#pragma unroll
-  for (int k = 0; k < LP_NPT; ++k) {
-    const int i = tid + k * LP_T;
-    x[k] = i < V ? L[i] : -INFINITY;
-    rmax = fmaxf(rmax, x[k]);
-  }
-  float nosp = 0.0f;
-  if (c.want_nosp) {
-    // no_speech_prob from the raw logits (before any filtering)
-    rmax = bmax(rmax, R);
-    float s = 0.0f;
-#pragma unroll
-    for (int k = 0; k < LP_NPT; ++k) {
-      const int i = tid + k * LP_T;
-      if (i < V && x[k] > -INFINITY) s += expf(x[k] - rmax);
-    }
-    s = bsum(s, R);
-    const float lse = logf(s) + rmax;
-    nosp = expf(L[nosp_id] - lse);
-  }
+  float* F = flt + (long)row * V;
   const int tid0_init = C.max_initial_tid;
   const int ts_lo = C.beg + c.seek_delta / 2;
-  float vmax = -INFINITY;
-#pragma unroll
-  for (int k = 0; k < LP_NPT; ++k) {
-    const int i = tid + k * LP_T;
-    if (i >= V) continue;
-    float v = x[k];
-    if (c.temperature > 0.0f) v = v / c.temperature;
-    bool kill = smask[i] < 0.0f;
+  float x[LP_NPT], v[LP_NPT];
+  float rmax = -INFINITY, m = -INFINITY, mtext = -INFINITY, mts = -INFINITY;
+  sfor<0, LP_NPT>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    const int off = tid + k * LP_T;
+    const int i = min(base + off, V - 1);
+    const bool in = off < LP_CHUNK && base + off < V;
+    x[k] = in ? L[i] : -INFINITY;
+    float y = x[k];
+    if (c.temperature > 0.0f) y = y / c.temperature;
+    bool kill = !in || smask[i] < 0.0f;
     if (c.is_initial && C.suppress_blank && (i == C.eot || i == C.space_id)) kill = true;
     if (c.last_ts) {
       if (c.penult_ts) {
@@ -263,100 +341,182 @@ __global__ __launch_bounds__(LP_T) void logits_process_kernel(
     }
     if (c.is_initial && tid0_init >= 0 && i > tid0_init) kill = true;
     if (c.has_ts && i >= C.beg && i < ts_lo) kill = true;
-    if (kill) v = -INFINITY;
-    x[k] = v;
-    vmax = fmaxf(vmax, v);
-  }
-  vmax = bmax(vmax, R);
-  float s = 0.0f;
-#pragma unroll
-  for (int k = 0; k < LP_NPT; ++k) {
-    const int i = tid + k * LP_T;
-    if (i < V && x[k] > -INFINITY) s += expf(x[k] - vmax);
-  }
-  s = bsum(s, R);
-  const float lse = logf(s) + vmax;
-  // x -> logprobs
-  float tsmax = -INFINITY, txmax = -INFINITY;
-#pragma unroll
-  for (int k = 0; k < LP_NPT; ++k) {
-    const int i = tid + k * LP_T;
-    if (i >= V) continue;
-    x[k] = x[k] > -INFINITY ? x[k] - lse : -INFINITY;
+    v[k] = kill ? -INFINITY : y;
+    if (in) F[i] = v[k];
+    rmax = fmaxf(rmax, x[k]);
+    m = fmaxf(m, v[k]);
     if (i >= C.beg)
-      tsmax = fmaxf(tsmax, x[k]);
+      mts = fmaxf(mts, v[k]);
     else
-      txmax = fmaxf(txmax, x[k]);
+      mtext = fmaxf(mtext, v[k]);
+  });
+  m = bmax256(m, red);
+  mts = bmax256(mts, red);
+  mtext = bmax256(mtext, red);
+  float s = 0.0f, sts = 0.0f, rs = 0.0f;
+  sfor<0, LP_NPT>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    const int i = base + tid + k * LP_T;
+    if (v[k] > -INFINITY) {
+      s += expf(v[k] - m);
+      if (i >= C.beg) sts += expf(v[k] - mts);
+    }
+  });
+  s = bsum256(s, red);
+  sts = bsum256(sts, red);
+  if (c.want_nosp) {
+    rmax = bmax256(rmax, red);
+    sfor<0, LP_NPT>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      if (x[k] > -INFINITY) rs += expf(x[k] - rmax);
+    });
+    rs = bsum256(rs, red);
   }
-  tsmax = bmax(tsmax, R);
-  txmax = bmax(txmax, R);
-  float ss = 0.0f;
-  if (tsmax > -INFINITY) {
-#pragma unroll
-    for (int k = 0; k < LP_NPT; ++k) {
-      const int i = tid + k * LP_T;
-      if (i < V && i >= C.beg && x[k] > -INFINITY) ss += expf(x[k] - tsmax);
-    }
-  }
-  ss = bsum(ss, R);
-  const float ts_logprob = ss > 0.0f ? logf(ss) + tsmax : -INFINITY;
-  const bool kill_text = ts_logprob > txmax;
-  // probs, greedy argmax, timestamp stats
-  float best = 0.0f;
-  int best_i = 0x7fffffff;
-  float tbest = 0.0f;
-  int tbest_i = 0x7fffffff;
-  double sum_ts = 0.0;
-#pragma unroll
-  for (int k = 0; k < LP_NPT; ++k) {
-    const int i = tid + k * LP_T;
-    if (i >= V) continue;
-    if (kill_text && i < C.beg) x[k] = -INFINITY;
-    const float p = x[k] == -INFINITY ? 0.0f : expf(x[k]);
-    if (c.want_probs) {
-      probs_out[(long)row * V + i] = p;
-      logprobs_out[(long)row * V + i] = x[k];
-    }
-    if (p > best) {
-      best = p;
-      best_i = i;
-    }
-    if (i >= C.beg) {
-      sum_ts += (double)p;
-      if (p > tbest) {
-        tbest = p;
-        tbest_i = i;
-      }
-    }
-  }
-  bargmax(best, best_i, R);
-  bargmax(tbest, tbest_i, R);
-  sum_ts = bsumd(sum_ts, R);
-  // plog = logprobs[id]: the owning thread publishes it through LDS
-  const int id = best > 0.0f ? best_i : 0;
-  __shared__ float plog_sh;
-#pragma unroll
-  for (int k = 0; k < LP_NPT; ++k)
-    if (tid + k * LP_T == id) plog_sh = x[k];
-  __syncthreads();
   if (tid == 0) {
-    TokOut t;
-    t.tid = tbest > 0.0f ? tbest_i : 0;
-    t.pt = (float)((double)tbest / (sum_ts + 1e-10));
-    t.ptsum = (float)sum_ts;
-    t.id = id;
-    t.p = best;
-    t.plog = plog_sh;  // (host applies the id >= beg -> tid/pt override)
-    t.nosp = nosp;
-    t.pad = 0;
-    out[row] = t;
+    LPPart P;
+    P.m = m;
+    P.s = s;
+    P.mtext = mtext;
+    P.mts = mts;
+    P.sts = sts;
+    P.rm = rmax;
+    P.rs = rs;
+    P.pad = 0.0f;
+    parts[row * LP_G + ch] = P;
   }
 }
 
+struct LPStats {
+  float lse, rlse;
+  bool kill_text;
+};
+__device__ __forceinline__ LPStats lp_combine(const LPPart* P, bool want_nosp) {
+  float M = -INFINITY, Mts = -INFINITY, Mtext = -INFINITY, RM = -INFINITY;
+  for (int g = 0; g < LP_G; ++g) {
+    M = fmaxf(M, P[g].m);
+    Mts = fmaxf(Mts, P[g].mts);
+    Mtext = fmaxf(Mtext, P[g].mtext);
+    RM = fmaxf(RM, P[g].rm);
+  }
+  float S = 0.0f, Sts = 0.0f, RS = 0.0f;
+  for (int g = 0; g < LP_G; ++g) {
+    if (P[g].m > -INFINITY) S += P[g].s * expf(P[g].m - M);
+    if (P[g].mts > -INFINITY) Sts += P[g].sts * expf(P[g].mts - Mts);
+    if (want_nosp && P[g].rm > -INFINITY) RS += P[g].rs * expf(P[g].rm - RM);
+  }
+  LPStats st;
+  st.lse = logf(S) + M;
+  st.rlse = want_nosp ? logf(RS) + RM : 0.0f;
+  // whisper_process_logits: timestamp log-prob = logsumexp of the timestamp
+  // log-probs; max text log-prob = max(text logits) - lse
+  const float ts_logprob = Sts > 0.0f ? (logf(Sts) + Mts) - st.lse : -INFINITY;
+  const float txmax = Mtext > -INFINITY ? Mtext - st.lse : -INFINITY;
+  st.kill_text = ts_logprob > txmax;
+  return st;
+}
+
+__global__ __launch_bounds__(LP_T) void lp_probs_kernel(float* __restrict__ flt,
+                                                        const LPPart* __restrict__ parts,
+                                                        const RowCtl* __restrict__ ctl,
+                                                        LPRes* __restrict__ res,
+                                                        float* __restrict__ probs_out,
+                                                        float* __restrict__ logprobs_out,
+                                                        LogitsConst C) {
+  __shared__ float redf[4];
+  __shared__ int redi[4];
+  __shared__ double redd[4];
+  const int row = blockIdx.y, ch = blockIdx.x;
+  const RowCtl c = ctl[row];
+  if (!c.active || !c.sample) return;
+  const int V = C.n_vocab, tid = threadIdx.x;
+  const int base = ch * LP_CHUNK;
+  const LPStats st = lp_combine(parts + row * LP_G, c.want_nosp);
+  const float* F = flt + (long)row * V;
+  float best = 0.0f, tbest = 0.0f;
+  int best_i = 0x7fffffff, tbest_i = 0x7fffffff;
+  double sum_ts = 0.0;
+  sfor<0, LP_NPT>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    const int off = tid + k * LP_T;
+    const int i = base + off;
+    if (off < LP_CHUNK && i < V) {
+      const float v = F[i];
+      const float lp = (v == -INFINITY || (st.kill_text && i < C.beg)) ? -INFINITY : v - st.lse;
+      const float p = lp == -INFINITY ? 0.0f : expf(lp);
+      if (c.want_probs) {
+        probs_out[(long)row * V + i] = p;
+        logprobs_out[(long)row * V + i] = lp;
+      }
+      if (p > best) {
+        best = p;
+        best_i = i;
+      }
+      if (i >= C.beg) {
+        sum_ts += (double)p;
+        if (p > tbest) {
+          tbest = p;
+          tbest_i = i;
+        }
+      }
+    }
+  });
+  bargmax256(best, best_i, redf, redi);
+  bargmax256(tbest, tbest_i, redf, redi);
+  sum_ts = bsum256d(sum_ts, redd);
+  if (tid == 0) {
+    LPRes r;
+    r.best = best;
+    r.best_i = best_i;
+    r.tbest = tbest;
+    r.tbest_i = tbest_i;
+    r.sum_ts = sum_ts;
+    res[row * LP_G + ch] = r;
+  }
+}
+
+__global__ __launch_bounds__(64) void lp_pick_kernel(const float* __restrict__ logits,
+                                                     const float* __restrict__ flt,
+                                                     const LPPart* __restrict__ parts,
+                                                     const LPRes* __restrict__ res,
+                                                     const RowCtl* __restrict__ ctl,
+                                                     TokOut* __restrict__ out, LogitsConst C) {
+  const int row = blockIdx.x;
+  const RowCtl c = ctl[row];
+  if (!c.active || !c.sample || threadIdx.x != 0) return;
+  const int V = C.n_vocab;
+  const LPStats st = lp_combine(parts + row * LP_G, c.want_nosp);
+  const LPRes* R = res + row * LP_G;
+  float best = 0.0f, tbest = 0.0f;
+  int best_i = 0x7fffffff, tbest_i = 0x7fffffff;
+  double sum_ts = 0.0;
+  for (int g = 0; g < LP_G; ++g) {
+    better(best, best_i, R[g].best, R[g].best_i);
+    better(tbest, tbest_i, R[g].tbest, R[g].tbest_i);
+    sum_ts += R[g].sum_ts;
+  }
+  const int id = best > 0.0f ? best_i : 0;
+  const float v = flt[(long)row * V + id];
+  const float plog =
+      (v == -INFINITY || (st.kill_text && id < C.beg)) ? -INFINITY : v - st.lse;
+  TokOut t;
+  t.tid = tbest > 0.0f ? tbest_i : 0;
+  t.pt = (float)((double)tbest / (sum_ts + 1e-10));
+  t.ptsum = (float)sum_ts;
+  t.id = id;
+  t.p = best;
+  t.plog = plog;  // (host applies the id >= beg -> tid/pt override)
+  t.nosp = c.want_nosp ? expf(logits[(long)row * V + C.nosp_id] - st.rlse) : 0.0f;
+  t.pad = 0;
+  out[row] = t;
+}
+
 void logits_process(float* logits, const float* static_mask, const RowCtl* ctl, TokOut* out,
-                    float* probs, float* logprobs, const LogitsConst& C, int R, hipStream_t st) {
-  logits_process_kernel<<<R, LP_T, 0, st>>>(logits, static_mask, ctl, out, probs, logprobs, C,
-                                            C.nosp_id);
+                    float* probs, float* logprobs, const LogitsConst& C, int R, LPScratch ws,
+                    hipStream_t st) {
+  const dim3 g(LP_G, R);
+  lp_filter_kernel<<<g, LP_T, 0, st>>>(logits, static_mask, ctl, ws.flt, ws.parts, C);
+  lp_probs_kernel<<<g, LP_T, 0, st>>>(ws.flt, ws.parts, ctl, ws.res, probs, logprobs, C);
+  lp_pick_kernel<<<R, 64, 0, st>>>(logits, ws.flt, ws.parts, ws.res, ctl, out, C);
 }
 
 }  // namespace mwx

@@ -41,6 +41,7 @@ struct EpiParams {
   const int* slot = nullptr;    // cross: cache slot per encoder batch index
   float kscale = 1.0f;
   float qscale = 1.0f;
+  bool pack_out = false;  // EPI_GELU: write the output as decode-GEMM A tiles (pack_index, K = ldc)
 };
 
 // Decode weights live in HBM as MFMA fragment tiles: for each 16-column strip
@@ -59,20 +60,23 @@ template <typename T>
 void gemm(int epi, bool out_f16, const T* A, long lda, long a_bstride, const T* W, long ldw,
           int M, int N, int K, int batch, const EpiParams& P, hipStream_t st);
 
+// Decode GEMMs take both operands as fragment tiles: Ap = activations
+// [ceil64(M) rows] packed with pack_index(m, k, K) by their producer kernel
+// (decode LayerNorm, decode attention, FFN1 epilogue), Wp = weights.
+//
 // Decode split-K GEMM over fragment-tiled weights Wp (pack_index): writes KS
 // f32 partial slabs P[KS][M][N] (no epilogue) and returns KS (0 if the shape is
 // unsupported). The consumer kernel sums the slabs and applies the epilogue.
 int splitk_factor(int K);
 template <typename T>
-int gemm_splitk_partials(const T* A, long lda, const T* Wp, int M, int N, int K, float* P,
-                         hipStream_t st);
+int gemm_splitk_partials(const T* Ap, const T* Wp, int M, int N, int K, float* P, hipStream_t st);
 // Decode full-K GEMM over fragment-tiled weights with a fused epilogue
 // (EPI_GELU / EPI_RES / EPI_F32 / EPI_STORE16 / EPI_DEC_QKV), rows in blocks of
 // 64 so a row's arithmetic does not depend on the batch. Returns false if K is
 // unsupported.
 template <typename T>
-bool gemm_decode(int epi, const T* A, long lda, const T* Wp, int M, int N, int K,
-                 const EpiParams& P, hipStream_t st);
+bool gemm_decode(int epi, const T* Ap, const T* Wp, int M, int N, int K, const EpiParams& P,
+                 hipStream_t st);
 
 void launch_mel(const float* pcm, int n, int n_len, int n_fft_frames, const float* filters,
                 int n_mels, const float* tables, float* out, hipStream_t st);
@@ -89,6 +93,13 @@ template <typename T>
 void layer_norm(const float* x, const float* w, const float* b, T* y, int M, int N,
                 const int* active, hipStream_t st, const float* P = nullptr, int KS = 0,
                 const float* pbias = nullptr);
+// Decode LayerNorm: as above, but y is written as decode-GEMM A tiles
+// (pack_index) and each thread owns 8 consecutive elements (N % 8 == 0,
+// N <= 2048).
+template <typename T>
+void layer_norm_dec(float* x, const float* w, const float* b, T* y, int M, int N,
+                    const int* active, hipStream_t st, const float* P, int KS,
+                    const float* pbias);
 template <typename T>
 void embed(const T* te, const float* pe, const int* tok, const int* pos, const int* active,
            float* x, int R, int d, hipStream_t st);
@@ -101,6 +112,7 @@ void enc_attention(const _Float16* q, const _Float16* k, const _Float16* vt, T* 
 // decode attention for R rows: q [R][H*64] f16; K/V rows [n_keys][64] per
 // (row, head). self: K = kbase + ((row*H + h)*kstride_rows)*64, n_keys =
 // pos[row] + 1. cross: K = kbase + ((clip[row]*H + h)*L)*64, n_keys = L.
+// o is written as decode-GEMM A tiles (pack_index, K = H*64).
 // The query of (row, head) is reduced from the producing split-K GEMM's
 // slabs P[KS][R][pcols] (q = f16((sum P + bias) * qscale), columns h*64..).
 // self (fixed_len == 0): the slabs hold Q|K|V (pcols = 3d); the kernel also
@@ -144,7 +156,27 @@ struct LogitsConst {
   int max_initial_tid;  // timestamps > beg + tid0 suppressed at the first step (-1: off)
   int nosp_id;
 };
+// Logits processing is split over LP_G chunks of LP_CHUNK vocabulary entries
+// per row (LP_G * LP_CHUNK >= n_vocab for every Whisper vocabulary).
+constexpr int LP_G = 16;
+constexpr int LP_CHUNK = 3328;  // 13 x 256
+struct LPPart {  // per-chunk statistics of the filtered (and raw) logits
+  float m, s, mtext, mts, sts, rm, rs, pad;
+};
+struct LPRes {  // per-chunk argmax / timestamp argmax / timestamp prob sum
+  float best;
+  int best_i;
+  float tbest;
+  int tbest_i;
+  double sum_ts;
+};
+struct LPScratch {
+  float* flt;     // [R][n_vocab] filtered logits
+  LPPart* parts;  // [R][LP_G]
+  LPRes* res;     // [R][LP_G]
+};
 void logits_process(float* logits, const float* static_mask, const RowCtl* ctl, TokOut* out,
-                    float* probs, float* logprobs, const LogitsConst& C, int R, hipStream_t st);
+                    float* probs, float* logprobs, const LogitsConst& C, int R, LPScratch ws,
+                    hipStream_t st);
 
 }  // namespace mwx
