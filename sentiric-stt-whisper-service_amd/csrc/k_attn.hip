@@ -224,7 +224,25 @@ __device__ __forceinline__ double block_sum_256d(double v, double* red) {
   return (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-template <typename T>
+// sum over the 8 lanes of an aligned lane group (DPP: xor 1, xor 2 within a
+// quad, then the mirrored quad); every lane of the group gets the same value
+__device__ __forceinline__ float dpp_sum8(float d) {
+  d += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(d), 0xB1, 0xF, 0xF, false));
+  d += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(d), 0x4E, 0xF, 0xF, false));
+  d += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(d), 0x141, 0xF, 0xF, false));
+  return d;
+}
+
+// One workgroup per (row, head). Key/value rows are streamed in batches: 8
+// rows per 8-lane group (each lane 16 B of a 128-B row), 64 rows per wave,
+// 256 per workgroup, double-buffered so batch b+1 is in flight while batch b
+// is consumed. All loads are unconditional (indices clamped to the last key)
+// so the compiler can keep exactly one batch outstanding across the loop.
+// SELF: the row appended by this launch is formed here from the QKV slabs,
+// written to the cache and taken from LDS (its cache line may be stale in L1).
+// The loop body is straight-line (two batches per trip, no early exit), so the
+// compiler keeps exactly one batch in flight with counted vmcnt waits.
+template <typename T, bool SELF>
 __global__ __launch_bounds__(256) void dec_attn_kernel(
     const float* __restrict__ P, int KS, int pcols, const float* __restrict__ bias, float qscale,
     float kscale, _Float16* __restrict__ kbase, _Float16* __restrict__ vbase,
@@ -239,39 +257,43 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
   if (!active[row]) return;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int kg = lane >> 3, c = lane & 7;
-  const bool self = fixed_len == 0;
-  const int p_row = self ? pos[row] : 0;
-  const int n = self ? p_row + 1 : fixed_len;
+  const int p_row = SELF ? pos[row] : 0;
+  const int n = SELF ? p_row + 1 : fixed_len;
+  const int jnew = SELF ? p_row : -1;
   const int slot = kv_index ? kv_index[row] : row;
   const int D = H * 64;
   _Float16* K = kbase + (((long)slot * H + h) * cap) * 64;
   _Float16* V = vbase + (((long)slot * H + h) * cap) * 64;
-  // Key/value rows are streamed in batches of 8 rows per 8-lane group (each
-  // lane 16 B of a 128-B row), double-buffered: batch i+1 is in flight while
-  // batch i is consumed. A wave covers 64 rows per batch, the workgroup 256.
-  // The first key batch is issued before the projection reduction.
-  const int jnew = self ? p_row : -1;
   constexpr int UB = 8;
+  const int nb = (n + 255) >> 8;
+  // rows past the end are clamped to the last OLD row (self: the new row is
+  // being written by this workgroup and is taken from LDS instead)
+  const int jmax = SELF ? max(n - 2, 0) : n - 1;
+  const bool wave_busy = wid * 64 < n;  // self: waves past the last row idle (n <= 256)
   f16x8 ka[UB], kb2[UB];
-#define LOADROWS(buf, base, j0v)                                                   \
+#define LOADROWS(buf, base, bidx)                                                  \
   _Pragma("unroll") for (int u = 0; u < UB; ++u) {                               \
-    const int j = min((j0v) + u * 8 + kg, n - 1);                                 \
-    if (j != jnew) buf[u] = *reinterpret_cast<const f16x8*>(base + (long)j * 64 + c * 8); \
+    const int j = min((bidx) * 256 + wid * 64 + u * 8 + kg, jmax);                \
+    buf[u] = *reinterpret_cast<const f16x8*>(base + (long)j * 64 + c * 8);        \
   }
-  LOADROWS(ka, K, wid * 64)
-  // reduce the projections of this head from the split-K slabs (KS <= 8)
+  // reduce the projections of this head from the split-K slabs (KS <= 8):
+  // the slab loads are issued first, then the first key batch, so the
+  // reduction waits only for its own loads
   const long pstride = (long)gridDim.y * pcols;
-  if (tid < (self ? 192 : 64)) {
-    const int part = tid >> 6, e = tid & 63;
-    const int col = part * D + h * 64 + e;
+  const bool red = tid < (SELF ? 192 : 64);
+  const int part = tid >> 6, e = tid & 63;
+  const int col = part * D + h * 64 + e;
+  float pk[8];
+  if (red) {
     const float* pp = P + (long)row * pcols + col;
-    float pk[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) pk[k] = k < KS ? pp[k * pstride] : 0.0f;
+    for (int k = 0; k < 8; ++k) pk[k] = pp[min(k, KS - 1) * pstride];
+  }
+  LOADROWS(ka, K, 0)
+  if (red) {
     float acc = pk[0];
 #pragma unroll
-    for (int k = 1; k < 8; ++k)
-      if (k < KS) acc += pk[k];
+    for (int k = 1; k < 8; ++k) acc += k < KS ? pk[k] : 0.0f;
     if (part == 0) {
       sq[e] = (float)(_Float16)((acc + bias[col]) * qscale);
     } else if (part == 1) {
@@ -285,36 +307,43 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
     }
   }
   __syncthreads();
-  float qv[8];
+  float qv[8], nk[8], nv[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) qv[j] = sq[c * 8 + j];
-  // scores (q.k in f32 over the f16 rows; the row appended by this launch is
-  // taken from LDS)
-  auto score_batch = [&](const f16x8* kk, int j0) {
+  for (int e = 0; e < 8; ++e) {
+    qv[e] = sq[c * 8 + e];
+    nk[e] = SELF ? snk[c * 8 + e] : 0.0f;
+    nv[e] = SELF ? snv[c * 8 + e] : 0.0f;
+  }
+  // scores (q.k in f32 over the f16 rows)
+  auto score_batch = [&](const f16x8* kk, int bidx) {
+    __builtin_amdgcn_sched_barrier(0);  // keep exactly one batch of loads ahead
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
-      const int j = j0 + u * 8 + kg;
+      const int j = bidx * 256 + wid * 64 + u * 8 + kg;
+      // (j >= n lanes also take the LDS row: finite, and their score is dropped)
+      const bool isnew = SELF && min(j, n - 1) == jnew;
       float d = 0.0f;
-      if (min(j, n - 1) == jnew) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) d += qv[e] * snk[c * 8 + e];
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) d += qv[e] * (float)kk[u][e];
-      }
-      d += __shfl_xor(d, 1, 64);
-      d += __shfl_xor(d, 2, 64);
-      d += __shfl_xor(d, 4, 64);
+      for (int e = 0; e < 8; ++e) d += qv[e] * (isnew ? nk[e] : (float)kk[u][e]);
+      d = dpp_sum8(d);
       if (c == 0 && j < n) sc[j] = d * scale;
     }
   };
-  for (int j0 = wid * 64; j0 < n; j0 += 512) {
-    if (j0 + 256 < n) LOADROWS(kb2, K, j0 + 256)
-    score_batch(ka, j0);
-    if (j0 + 256 >= n) break;
-    if (j0 + 512 < n) LOADROWS(ka, K, j0 + 512)
-    score_batch(kb2, j0 + 256);
+  if constexpr (SELF) {
+    // <= 2 batches (n <= 448): latency-bound, one batch per trip
+    for (int b = 0; wave_busy && b < nb; ++b) {
+      if (b > 0) LOADROWS(ka, K, b)
+      score_batch(ka, b);
+    }
+  } else {
+    for (int b = 0; b < nb; b += 2) {  // (odd nb: one clamped batch extra)
+      LOADROWS(kb2, K, b + 1)
+      score_batch(ka, b);
+      LOADROWS(ka, K, b + 2)
+      score_batch(kb2, b + 1);
+    }
   }
+  LOADROWS(ka, V, 0)
   __syncthreads();
   float mx = -INFINITY;
   for (int j = tid; j < n; j += 256) mx = fmaxf(mx, sc[j]);
@@ -332,28 +361,29 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
   float acc[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) acc[e] = 0.0f;
-  auto pv_batch = [&](const f16x8* vv, int j0) {
+  auto pv_batch = [&](const f16x8* vv, int bidx) {
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
-      const int j = j0 + u * 8 + kg;
-      const int jc = min(j, n - 1);
-      const float p = j < n ? sc[jc] : 0.0f;
-      if (jc == jnew) {
+      const int j = bidx * 256 + wid * 64 + u * 8 + kg;
+      const bool isnew = SELF && min(j, n - 1) == jnew;  // p = 0 past the end
+      const float p = j < n ? sc[min(j, n - 1)] : 0.0f;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e] += p * snv[c * 8 + e];
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e] += p * (float)vv[u][e];
-      }
+      for (int e = 0; e < 8; ++e) acc[e] += p * (isnew ? nv[e] : (float)vv[u][e]);
     }
   };
-  LOADROWS(ka, V, wid * 64)
-  for (int j0 = wid * 64; j0 < n; j0 += 512) {
-    if (j0 + 256 < n) LOADROWS(kb2, V, j0 + 256)
-    pv_batch(ka, j0);
-    if (j0 + 256 >= n) break;
-    if (j0 + 512 < n) LOADROWS(ka, V, j0 + 512)
-    pv_batch(kb2, j0 + 256);
+  if constexpr (SELF) {
+    for (int b = 0; wave_busy && b < nb; ++b) {
+      if (b > 0) LOADROWS(ka, V, b)
+      pv_batch(ka, b);
+    }
+  } else {
+    for (int b = 0; b < nb; b += 2) {
+      LOADROWS(kb2, V, b + 1)
+      pv_batch(ka, b);
+      LOADROWS(ka, V, b + 2)
+      pv_batch(kb2, b + 1);
+    }
   }
 #undef LOADROWS
 #pragma unroll
@@ -380,8 +410,14 @@ void dec_attention(const float* P, int KS, int pcols, const float* bias, float q
                    const int* pos, const int* active, int fixed_len, int kv_len_cap, T* o, int R,
                    int H, float scale, hipStream_t st) {
   dim3 g(H, R);
-  dec_attn_kernel<T><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale, kbase, vbase,
-                                        kv_index, pos, active, fixed_len, kv_len_cap, o, H, scale);
+if (fixed_len == 0)
+    dec_attn_kernel<T, true><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale, kbase, vbase,
+                                                kv_index, pos, active, fixed_len, kv_len_cap, o,
+                                                H, scale);
+  else
+    dec_attn_kernel<T, false><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale, kbase,
+                                                 vbase, kv_index, pos, active, fixed_len,
+                                                 kv_len_cap, o, H, scale);
 }
 
 template void enc_attention<_Float16>(const _Float16*, const _Float16*, const _Float16*, _Float16*,
