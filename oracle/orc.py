@@ -99,6 +99,7 @@ class OSegment:
     t1: int
     text: str
     tokens: List[OToken] = field(default_factory=list)
+    raw: bytes = b""  # segment text bytes as produced (may be partial UTF-8)
 
 
 @dataclass
@@ -185,6 +186,9 @@ class Oracle:
     def token_str(self, i: int) -> str:
         return lib().orc_token_str(self.h, i).decode("utf-8", "replace")
 
+    def token_bytes(self, i: int) -> bytes:
+        return lib().orc_token_str(self.h, i)
+
     def mel(self, pcm: np.ndarray):
         pcm = np.ascontiguousarray(pcm, dtype=np.float32)
         n_len = (len(pcm) + 480000) // 160
@@ -232,7 +236,8 @@ class Oracle:
         for i in range(L.orc_full_n_segments(r)):
             t = (C.c_int64 * 2)()
             L.orc_full_segment_times(r, i, t)
-            seg = OSegment(t[0], t[1], L.orc_full_segment_text(r, i).decode("utf-8", "replace"))
+            raw = L.orc_full_segment_text(r, i)
+            seg = OSegment(t[0], t[1], raw.decode("utf-8", "replace"), raw=raw)
             for j in range(L.orc_full_n_tokens(r, i)):
                 ids = (C.c_int * 2)()
                 f = (C.c_float * 4)()

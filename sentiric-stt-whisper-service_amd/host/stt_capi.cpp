@@ -1,0 +1,109 @@
+// Plain-C entry points over mwx_host::SttEngine for the Python tests (ctypes).
+// Results are returned as JSON with every string hex-encoded (token text may
+// be a partial UTF-8 sequence).
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "stt_engine.h"
+#include "text_filters.h"
+
+using namespace mwx_host;
+
+namespace {
+
+std::string hex(const std::string& s) {
+  static const char* d = "0123456789abcdef";
+  std::string o;
+  o.reserve(s.size() * 2);
+  for (unsigned char c : s) {
+    o.push_back(d[c >> 4]);
+    o.push_back(d[c & 15]);
+  }
+  return o;
+}
+
+std::string to_json(const std::vector<TranscriptionResult>& rs) {
+  std::string o = "[";
+  char buf[256];
+  for (size_t i = 0; i < rs.size(); ++i) {
+    const TranscriptionResult& r = rs[i];
+    std::snprintf(buf, sizeof buf, "%s{\"prob\":%.9g,\"t0\":%lld,\"t1\":%lld,\"turn\":%d,\"n\":%d,",
+                  i ? "," : "", r.prob, (long long)r.t0, (long long)r.t1, (int)r.speaker_turn_next,
+                  r.token_count);
+    o += buf;
+    o += "\"text\":\"" + hex(r.text) + "\",\"language\":\"" + hex(r.language) + "\",\"tokens\":[";
+    for (size_t j = 0; j < r.tokens.size(); ++j) {
+      const TokenData& t = r.tokens[j];
+      std::snprintf(buf, sizeof buf, "%s{\"p\":%.9g,\"t0\":%lld,\"t1\":%lld,\"text\":\"", j ? "," : "",
+                    t.p, (long long)t.t0, (long long)t.t1);
+      o += buf;
+      o += hex(t.text) + "\"}";
+    }
+    o += "]}";
+  }
+  return o + "]";
+}
+
+int emit(const std::string& s, char* out, int cap) {
+  if ((int)s.size() + 1 > cap) return -(int)(s.size() + 1);
+  std::memcpy(out, s.c_str(), s.size() + 1);
+  return (int)s.size();
+}
+
+}  // namespace
+
+extern "C" {
+
+int mwx_stt_is_hallucination(const char* text) { return is_hallucination(text ? text : "") ? 1 : 0; }
+
+void* mwx_stt_new(const char* model_dir, const char* model_filename, int parallel_requests,
+                  int queue_timeout_ms, int beam_size, const char* language, int vad_ms_min,
+                  int gpu_device) {
+  Settings s;
+  s.model_dir = model_dir;
+  s.model_filename = model_filename;
+  s.parallel_requests = parallel_requests;
+  s.request_queue_timeout_ms = queue_timeout_ms;
+  s.beam_size = beam_size;
+  s.language = language;
+  s.vad_ms_min_duration = vad_ms_min;
+  s.gpu_device = gpu_device;
+  try {
+    return new SttEngine(s);
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "SttEngine: %s\n", e.what());
+    return nullptr;
+  }
+}
+
+void mwx_stt_free(void* eng) { delete static_cast<SttEngine*>(eng); }
+
+// 0.. = JSON length written; -1 = error; -2 = EngineBusyException;
+// < -2 = -(needed capacity)
+int mwx_stt_transcribe_pcm16(void* eng, const int16_t* pcm, int n, int sample_rate,
+                             const char* language, int beam_size, float temperature, char* out,
+                             int cap, double* metrics3) {
+  RequestOptions o;
+  o.language = language ? language : "";
+  o.beam_size = beam_size;
+  o.temperature = temperature;
+  SttEngine::PerformanceMetrics m{0, 0, 0};
+  try {
+    const auto rs = static_cast<SttEngine*>(eng)->transcribe_pcm16(
+        std::vector<int16_t>(pcm, pcm + n), sample_rate, o, &m);
+    if (metrics3) {
+      metrics3[0] = m.queue_time_ms;
+      metrics3[1] = m.processing_time_ms;
+      metrics3[2] = m.token_count;
+    }
+    const int r = emit(to_json(rs), out, cap);
+    return r < -1 ? r - 2 : r;
+  } catch (const EngineBusyException&) {
+    return -2;
+  } catch (...) {
+    return -1;
+  }
+}
+
+}  // extern "C"

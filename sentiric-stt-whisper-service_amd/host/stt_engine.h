@@ -1,0 +1,145 @@
+// SttEngine on the mwx C ABI — the drop-in for the reference's
+// src/stt_engine.h:16-115 (same class, method names, argument meaning, result
+// types and error behaviour), with whisper.h replaced by include/mwx.h.
+//
+// Kept from the reference: the state pool with a queue timeout that throws
+// EngineBusyException (src/stt_engine.cpp:63-85), the request-option defaults
+// (:204-212), the whisper_full parameter mapping (:214-243), the too-short
+// audio gate (:153-167), and the result post-filters (:261-311: hallucination
+// phrases, tokens with id >= eot skipped, average token p < 0.40 drops the
+// segment). Out of scope: VAD, resampling (non-16 kHz input is
+// passed through, as the reference does when libsamplerate fails, :141),
+// prosody and speaker clustering (their result fields keep neutral values).
+#pragma once
+
+#include <condition_variable>
+#include <cstdint>
+#include <functional>
+#include <mutex>
+#include <queue>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "mwx.h"
+
+namespace mwx_host {
+
+// The Settings fields SttEngine reads (reference src/config.h:10-80 defaults).
+struct Settings {
+  std::string model_dir = "/models";
+  std::string model_filename = "ggml-medium.bin";
+  bool enable_vad = false;  // VAD is out of scope: must stay false
+  int vad_ms_min_duration = 500;
+  int n_threads = 4;
+  int parallel_requests = 2;
+  int request_queue_timeout_ms = 5000;
+  std::string language = "auto";
+  bool no_timestamps = false;
+  int beam_size = 5;
+  float temperature = 0.0f;
+  int best_of = 5;
+  float logprob_threshold = -0.7f;
+  float no_speech_threshold = 0.85f;
+  bool flash_attn = true;
+  bool suppress_nst = true;
+  int gpu_device = 0;
+  int stream_buffer_samples = 8000;
+};
+
+struct TokenData {
+  std::string text;
+  float p;
+  int64_t t0;
+  int64_t t1;
+};
+
+struct RequestOptions {
+  std::string language;
+  std::string prompt;
+  bool translate = false;
+  bool enable_diarization = false;
+  float temperature = -1.0f;
+  int beam_size = -1;
+  int best_of = -1;
+  std::function<bool()> should_abort = nullptr;
+};
+
+struct TranscriptionResult {
+  std::string text;
+  std::string language;
+  float prob;
+  int64_t t0;
+  int64_t t1;
+  bool speaker_turn_next;
+  std::vector<TokenData> tokens;
+  int token_count = 0;
+  std::string gender_proxy;
+  std::string emotion_proxy;
+  float arousal = 0.0f;
+  float valence = 0.0f;
+  std::string speaker_id;
+};
+
+class EngineBusyException : public std::runtime_error {
+ public:
+  explicit EngineBusyException(const std::string& msg) : std::runtime_error(msg) {}
+};
+
+class SttEngine {
+ public:
+  explicit SttEngine(const Settings& settings);  // throws std::runtime_error on load failure
+  ~SttEngine();
+  SttEngine(const SttEngine&) = delete;
+  SttEngine& operator=(const SttEngine&) = delete;
+
+  bool is_ready() const { return ctx_ != nullptr; }
+  const Settings& get_settings() const { return settings_; }
+
+  struct PerformanceMetrics {
+    double queue_time_ms;
+    double processing_time_ms;
+    int token_count;
+  };
+
+  std::vector<TranscriptionResult> transcribe(const std::vector<float>& pcmf32,
+                                              int input_sample_rate,
+                                              const RequestOptions& options,
+                                              PerformanceMetrics* out_metrics = nullptr);
+  std::vector<TranscriptionResult> transcribe_pcm16(const std::vector<int16_t>& pcm16,
+                                                    int input_sample_rate,
+                                                    const RequestOptions& options,
+                                                    PerformanceMetrics* out_metrics = nullptr);
+
+  // Batched entry (no reference counterpart): B independent clips in one GPU
+  // pass, each result list filtered exactly as transcribe() filters it.
+  std::vector<std::vector<TranscriptionResult>> transcribe_batch(
+      const std::vector<std::vector<float>>& clips, const RequestOptions& options);
+
+ private:
+  mwx_state* acquire_state();
+  void release_state(mwx_state* state);
+  mwx_full_params make_params(const RequestOptions& options, std::string& target_lang,
+                              std::function<bool()>& abort_fn) const;
+  std::vector<TranscriptionResult> collect(mwx_state* state, const std::string& lang,
+                                           size_t pcm_size, int* token_count) const;
+
+  Settings settings_;
+  mwx_context* ctx_ = nullptr;
+  std::queue<mwx_state*> state_pool_;
+  std::mutex pool_mutex_;
+  std::condition_variable pool_cv_;
+  std::vector<mwx_state*> all_states_;
+
+  struct StateGuard {
+    SttEngine& engine;
+    mwx_state* state;
+    explicit StateGuard(SttEngine& e) : engine(e) { state = engine.acquire_state(); }
+    ~StateGuard() {
+      if (state) engine.release_state(state);
+    }
+    mwx_state* get() { return state; }
+  };
+};
+
+}  // namespace mwx_host
