@@ -31,6 +31,11 @@ int mwx_test_encode(struct mwx_context* ctx, struct mwx_state* state, const floa
 int mwx_test_decode(struct mwx_context* ctx, struct mwx_state* state, const int* tokens, int n,
                     float* logits_out);
 
+/* As mwx_test_decode, but only the logits of the last token are copied out
+ * (logits_last [n_vocab]). */
+int mwx_test_decode_last(struct mwx_context* ctx, struct mwx_state* state, const int* tokens,
+                         int n, float* logits_last);
+
 #ifdef __cplusplus
 }
 #endif

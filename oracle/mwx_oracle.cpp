@@ -895,6 +895,64 @@ static TokenData sample_token(const Model& m, Decoder& dec, bool best) {
   return r;
 }
 
+// whisper_sample_token_topk (whisper.cpp v1.8.2): the timestamp statistics of
+// whisper_sample_token, then k draws with replacement from
+// std::discrete_distribution over the decoder's probs with the decoder's RNG
+// (upstream also partial-sorts the logits here, but the candidates come from
+// the draws).
+static std::vector<TokenData> sample_topk(const Model& m, Decoder& dec, int k) {
+  const int n = m.n_vocab;
+  const auto& probs = dec.probs;
+  const auto& lp = dec.logprobs;
+  int tid = m.beg;
+  float pt = 0.0f, ptsum = 0.0f;
+  {
+    double sum_ts = 0.0, max_ts = 0.0;
+    for (int i = m.beg; i < n; i++) {
+      if (probs[i] == -INFINITY) continue;
+      sum_ts += probs[i];
+      if (max_ts < probs[i]) {
+        max_ts = probs[i];
+        tid = i;
+      }
+    }
+    pt = (float)(max_ts / (sum_ts + 1e-10));
+    ptsum = (float)sum_ts;
+  }
+  std::discrete_distribution<> dist(probs.begin(), probs.end());
+  std::vector<TokenData> out;
+  for (int i = 0; i < k; ++i) {
+    TokenData r;
+    r.id = dist(dec.rng);
+    r.tid = tid;
+    r.p = probs[r.id];
+    r.plog = lp[r.id];
+    r.pt = pt;
+    r.ptsum = ptsum;
+    if (r.id >= m.beg) {
+      r.tid = r.id;
+      r.pt = r.p;
+    }
+    out.push_back(r);
+  }
+  return out;
+}
+
+// whisper_sequence_tokens_equal
+static bool tokens_equal(const Sequence& a, const Sequence& b) {
+  if (a.tokens.size() != b.tokens.size()) return false;
+  for (int i = (int)a.tokens.size() - 1; i >= 0; i--)
+    if (a.tokens[i].id != b.tokens[i].id) return false;
+  return true;
+}
+
+struct BeamCand {
+  int decoder_idx;
+  int seek_delta;
+  bool has_ts;
+  Sequence seq;
+};
+
 static void sequence_score(const Params& P, Sequence& s) {
   if (s.result_len == 0) return;
   double result = 0.0;
@@ -1119,17 +1177,35 @@ static int lang_auto_detect(const Model& m, const Cross& cr) {
   return lid[0].second;
 }
 
+// External decoder (test replay): when set, full() takes the logits of every
+// decode from these callbacks instead of its own encoder/decoder — used to run
+// the token-loop logic (logits rules, sampling, beam search) on logits
+// produced by the device, so that logic is compared exactly.
+typedef void (*ExtEncodeFn)(void* user, int seek);
+typedef void (*ExtLogitsFn)(void* user, const int* tokens, int n, float* logits_last);
+static ExtEncodeFn g_ext_encode = nullptr;
+static ExtLogitsFn g_ext_logits = nullptr;
+static void* g_ext_user = nullptr;
+
 static int full(const Model& m, Params P, const float* samples, int n_samples, Result& R) {
   R.segs.clear();
+  const bool ext = g_ext_logits != nullptr;
   Mel mel;
-  if (n_samples > 0) log_mel(m, samples, n_samples, mel);
+  if (n_samples > 0 && !ext) log_mel(m, samples, n_samples, mel);
+  if (ext && n_samples > 0) {  // only n_len_org is needed from the mel
+    mel.n_len_org = 1 + (n_samples + 200 - 400) / 160;
+  }
   std::vector<float> enc;
   Cross cr;
   int cached_seek = -1;
   auto encode_at = [&](int seek) {
     if (cached_seek == seek) return;
-    encode(m, mel, seek, enc);
-    cross(m, enc, cr);
+    if (ext) {
+      g_ext_encode(g_ext_user, seek);
+    } else {
+      encode(m, mel, seek, enc);
+      cross(m, enc, cr);
+    }
     cached_seek = seek;
   };
   std::string language = P.language;
@@ -1208,8 +1284,15 @@ static int full(const Model& m, Params P, const float* samples, int n_samples, R
       }
       prompt.insert(prompt.end(), prompt_init.begin(), prompt_init.end());
       decs[0].kv = KV();
-      decode(m, cr, decs[0].kv, prompt.data(), (int)prompt.size(), 0, logits);
-      const float* last = logits.data() + (size_t)(prompt.size() - 1) * m.n_vocab;
+      const float* last;
+      if (ext) {
+        logits.resize(m.n_vocab);
+        g_ext_logits(g_ext_user, prompt.data(), (int)prompt.size(), logits.data());
+        last = logits.data();
+      } else {
+        decode(m, cr, decs[0].kv, prompt.data(), (int)prompt.size(), 0, logits);
+        last = logits.data() + (size_t)(prompt.size() - 1) * m.n_vocab;
+      }
       {
         std::vector<float> l(last, last + m.n_vocab), lp(m.n_vocab), pr(m.n_vocab);
         compute_logprobs(l, m.n_vocab, lp);
@@ -1225,11 +1308,51 @@ static int full(const Model& m, Params P, const float* samples, int n_samples, R
       }
       const int n_max = P.bench_fixed_steps > 0 ? P.bench_fixed_steps : m.n_text_ctx / 2 - 4;
       for (int i = 0; i < n_max; ++i) {
-        for (int j = 0; j < n_cur; ++j) {
-          auto& d = decs[j];
-          if (d.completed || d.failed) continue;
-          d.seq.tokens.push_back(sample_token(m, d, t_cur < 1e-6f));
-          d.seq.sum_logprobs_all += d.seq.tokens.back().plog;
+        if (P.strategy == 1) {
+          // beam search: beam_size candidates per live decoder, sorted by
+          // sum_logprobs_all (desc, then decoder index), assigned in order,
+          // skipping candidates equal to the one just taken (from i > 0);
+          // each decoder takes over its candidate's KV cache
+          std::vector<BeamCand> cands;
+          for (int j = 0; j < n_cur; ++j) {
+            auto& d = decs[j];
+            if (d.completed || d.failed) continue;
+            for (const auto& tok : sample_topk(m, d, P.beam_size)) {
+              cands.push_back({j, d.seek_delta, d.has_ts, d.seq});
+              cands.back().seq.tokens.push_back(tok);
+              cands.back().seq.sum_logprobs_all += tok.plog;
+            }
+          }
+          std::sort(cands.begin(), cands.end(), [](const BeamCand& a, const BeamCand& b) {
+            if (a.seq.sum_logprobs_all != b.seq.sum_logprobs_all)
+              return a.seq.sum_logprobs_all > b.seq.sum_logprobs_all;
+            return a.decoder_idx < b.decoder_idx;
+          });
+          size_t cur_c = 0;
+          std::vector<int> src(n_cur, -1);
+          for (int j = 0; j < n_cur; ++j) {
+            auto& d = decs[j];
+            if (d.completed || d.failed) continue;
+            if (cur_c >= cands.size()) cur_c = 0;
+            const BeamCand& cur = cands[cur_c++];
+            while (cands.size() > cur_c && tokens_equal(cands[cur_c].seq, cur.seq) && i > 0) ++cur_c;
+            d.seek_delta = cur.seek_delta;
+            d.has_ts = cur.has_ts;
+            d.seq = cur.seq;
+            src[j] = cur.decoder_idx;
+          }
+          std::vector<KV> kv_new(n_cur);
+          for (int j = 0; j < n_cur; ++j)
+            if (src[j] >= 0 && src[j] != j) kv_new[j] = decs[src[j]].kv;
+          for (int j = 0; j < n_cur; ++j)
+            if (src[j] >= 0 && src[j] != j) decs[j].kv = std::move(kv_new[j]);
+        } else {
+          for (int j = 0; j < n_cur; ++j) {
+            auto& d = decs[j];
+            if (d.completed || d.failed) continue;
+            d.seq.tokens.push_back(sample_token(m, d, t_cur < 1e-6f));
+            d.seq.sum_logprobs_all += d.seq.tokens.back().plog;
+          }
         }
         for (int j = 0; j < n_cur; ++j) {
           auto& d = decs[j];
@@ -1276,7 +1399,14 @@ static int full(const Model& m, Params P, const float* samples, int n_samples, R
           auto& d = decs[j];
           if (d.failed || d.completed) continue;
           const int tok = d.seq.tokens.back().id;
-          decode(m, cr, d.kv, &tok, 1, n_past, logits);
+          if (ext) {
+            std::vector<int> ctxt(prompt);
+            for (const auto& t : d.seq.tokens) ctxt.push_back(t.id);
+            logits.resize(m.n_vocab);
+            g_ext_logits(g_ext_user, ctxt.data(), (int)ctxt.size(), logits.data());
+          } else {
+            decode(m, cr, d.kv, &tok, 1, n_past, logits);
+          }
           process_logits(m, P, d, logits.data(), t_cur);
         }
       }
@@ -1389,6 +1519,11 @@ void orc_set_threads(int n) {
 #endif
 }
 void orc_set_enc_layer_limit(int n) { g_enc_layer_limit = n; }
+void orc_set_external(ExtEncodeFn enc, ExtLogitsFn lg, void* user) {
+  g_ext_encode = enc;
+  g_ext_logits = lg;
+  g_ext_user = user;
+}
 void orc_hparams(void* h, int* out) {
   auto* m = (Model*)h;
   for (int i = 0; i < 11; ++i) out[i] = m->hp[i];

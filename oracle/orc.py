@@ -21,6 +21,8 @@ LIB_PATH = os.path.join(HERE, "liborc.so")
 ORC_EXACT = 1
 
 _lib = None
+EXT_ENC = C.CFUNCTYPE(None, C.c_void_p, C.c_int)
+EXT_LOGITS = C.CFUNCTYPE(None, C.c_void_p, C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_float))
 
 
 def build() -> None:
@@ -41,6 +43,7 @@ def lib() -> C.CDLL:
     L.orc_free.argtypes = [P]
     L.orc_set_threads.argtypes = [C.c_int]
     L.orc_set_enc_layer_limit.argtypes = [C.c_int]
+    L.orc_set_external.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     L.orc_hparams.argtypes = [P, C.POINTER(C.c_int)]
     L.orc_wtype.restype = C.c_int
     L.orc_wtype.argtypes = [P]
@@ -217,6 +220,26 @@ class Oracle:
         lib().orc_decode_seq(self.h, _fp(np.ascontiguousarray(k)), _fp(np.ascontiguousarray(v)),
                              toks.ctypes.data_as(C.POINTER(C.c_int)), len(toks), _fp(out))
         return out
+
+    def full_external(self, pcm: np.ndarray, opt: FullOptions, encode_fn, logits_fn):
+        """full() with every decode answered by callbacks: encode_fn(seek) and
+        logits_fn(tokens) -> last-token logits [n_vocab] (e.g. from the device)."""
+        V = self.n_vocab
+
+        def _enc(user, seek):
+            encode_fn(int(seek))
+
+        def _lg(user, toks, n, out):
+            lg = logits_fn([toks[i] for i in range(n)])
+            C.memmove(out, np.ascontiguousarray(lg, np.float32).ctypes.data, V * 4)
+
+        enc_cb = EXT_ENC(_enc)
+        lg_cb = EXT_LOGITS(_lg)
+        lib().orc_set_external(C.cast(enc_cb, C.c_void_p), C.cast(lg_cb, C.c_void_p), None)
+        try:
+            return self.full(pcm, opt)
+        finally:
+            lib().orc_set_external(None, None, None)
 
     def full(self, pcm: np.ndarray, opt: FullOptions):
         pcm = np.ascontiguousarray(pcm, dtype=np.float32)

@@ -119,6 +119,7 @@ struct State {
   DBuf xd, hd, qd, od, ffd, logits, kself, vself, stepin, ctl, tokout, probs, logprobs, smask;
   DBuf pqkv, pres, pq;  // split-K partial slabs of the decode GEMMs
   DBuf lpflt, lpparts, lpres;  // logits-processing scratch
+  DBuf kvpairs, kvstage;       // beam search KV hand-over
   int cross_cap = 0;  // cross cache slots
   int row_cap = 0;    // self cache rows
   std::vector<Segment> result_all;
@@ -692,6 +693,19 @@ struct Driver {
     S.stepin.get((size_t)R * 4 * 4);
     S.ctl.get((size_t)R * sizeof(RowCtl));
     S.tokout.get((size_t)R * sizeof(TokOut));
+  }
+
+  // beam search: rows take over other rows' self KV caches (triples dst, src, npos)
+  void copy_kv_rows(const std::vector<int>& triples) {
+    const int n = (int)triples.size() / 3;
+    if (n == 0) return;
+    int npos = 1;
+    for (int i = 0; i < n; ++i) npos = std::max(npos, triples[3 * i + 2]);
+    int* dp = (int*)S.kvpairs.get(triples.size() * 4);
+    _Float16* stage = (_Float16*)S.kvstage.get((size_t)n * 2 * L_dec * H * npos * 64 * 2);
+    HIPC(hipMemcpyAsync(dp, triples.data(), triples.size() * 4, hipMemcpyHostToDevice, st));
+    kv_rows_copy((_Float16*)S.kself.p, (_Float16*)S.vself.p, (long)S.row_cap * H * Tctx * 64,
+                 L_dec, H, Tctx, dp, n, stage, npos, st);
   }
 
   // one decoder step for R rows; inputs already in S.stepin / S.ctl

@@ -420,6 +420,44 @@ if (fixed_len == 0)
                                                  kv_len_cap, o, H, scale);
 }
 
+// ---------------------------------------------------------------------------
+// beam search: decoder rows take over another row's self-attention KV cache
+// (whisper_kv_cache_seq_cp via a temporary sequence). Phase 0 copies every
+// source row's first npos positions into staging, phase 1 staging into the
+// destination rows, so any permutation of rows is safe.
+// pairs: [n][3] = (dst row, src row, npos); cache layout [L][row][H][Tctx][64].
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void kv_rows_copy_kernel(_Float16* __restrict__ kc,
+                                                           _Float16* __restrict__ vc,
+                                                           long layer_stride, int H, int Tctx,
+                                                           const int* __restrict__ pairs,
+                                                           _Float16* __restrict__ stage,
+                                                           int stage_pos, int L, int phase) {
+  const int l = blockIdx.x / H, h = blockIdx.x % H, p = blockIdx.y;
+  const int dst = pairs[3 * p], src = pairs[3 * p + 1], npos = pairs[3 * p + 2];
+  const int nvec = npos * 8;  // 16-B vectors
+#pragma unroll
+  for (int kv = 0; kv < 2; ++kv) {
+    _Float16* cache = (kv ? vc : kc) + l * layer_stride;
+    _Float16* sg = stage + ((((long)p * 2 + kv) * L + l) * H + h) * (long)stage_pos * 64;
+    const _Float16* from = phase == 0 ? cache + ((long)src * H + h) * Tctx * 64 : sg;
+    _Float16* to = phase == 0 ? sg : cache + ((long)dst * H + h) * Tctx * 64;
+    for (int i = threadIdx.x; i < nvec; i += 256)
+      reinterpret_cast<f16x8*>(to)[i] = reinterpret_cast<const f16x8*>(from)[i];
+  }
+}
+
+void kv_rows_copy(_Float16* kc, _Float16* vc, long layer_stride, int L, int H, int Tctx,
+                  const int* d_pairs, int n_pairs, _Float16* stage, int stage_pos,
+                  hipStream_t st) {
+  if (n_pairs <= 0) return;
+  const dim3 g(L * H, n_pairs);
+  kv_rows_copy_kernel<<<g, 256, 0, st>>>(kc, vc, layer_stride, H, Tctx, d_pairs, stage,
+                                         stage_pos, L, 0);
+  kv_rows_copy_kernel<<<g, 256, 0, st>>>(kc, vc, layer_stride, H, Tctx, d_pairs, stage,
+                                         stage_pos, L, 1);
+}
+
 template void enc_attention<_Float16>(const _Float16*, const _Float16*, const _Float16*, _Float16*,
                                       int, int, int, float, hipStream_t);
 template void enc_attention<__bf16>(const _Float16*, const _Float16*, const _Float16*, __bf16*, int,

@@ -124,6 +124,13 @@ void dec_attention(const float* P, int KS, int pcols, const float* bias, float q
                    const int* pos, const int* active, int fixed_len, int kv_len_cap, T* o, int R,
                    int H, float scale, hipStream_t st);
 
+// Beam search KV hand-over: for each (dst, src, npos) triple in d_pairs, the
+// first npos positions of row src's self KV cache (all layers, heads) are
+// copied to row dst, through `stage` ([n_pairs][2][L][H][stage_pos][64]).
+void kv_rows_copy(_Float16* kc, _Float16* vc, long layer_stride, int L, int H, int Tctx,
+                  const int* d_pairs, int n_pairs, _Float16* stage, int stage_pos,
+                  hipStream_t st);
+
 struct RowCtl {
   int active;        // row participates in this step
   int sample;        // logits of this step are processed (last prompt token or generated)

@@ -10,6 +10,7 @@
 #include <cstdarg>
 #include <cstring>
 #include <fstream>
+#include <functional>
 #include <regex>
 
 #include "common.h"
@@ -472,8 +473,17 @@ struct Writer {
   }
 
   // ne in numpy order (outermost first); written reversed (ggml order).
+  // the seeded value of element i of tensor `name` (uniform center +- scale)
+  float gen(const std::string& name, int64_t i, float center, float scale) const {
+    const uint64_t key = fnv1a64(name) ^ seed;
+    const uint64_t r = splitmix64(key + (uint64_t)i * 0xD1B54A32D192ED03ull);
+    const float u = (float)((double)(r >> 40) * (1.0 / 8388608.0) - 1.0);
+    return center + scale * u;
+  }
+
   void tensor(const std::string& name, std::vector<int64_t> shape, int ttype,
-              float center, float scale, const float* explicit_vals = nullptr) {
+              float center, float scale, const float* explicit_vals = nullptr,
+              const std::function<float(int64_t, float)>& adjust = nullptr) {
     const int32_t nd = (int32_t)shape.size();
     put(nd);
     put((int32_t)name.size());
@@ -497,6 +507,7 @@ struct Writer {
           const float u = (float)((double)(r >> 40) * (1.0 / 8388608.0) - 1.0);
           v = center + scale * u;
         }
+        if (adjust) v = adjust(i, v);
         uint8_t* p = buf.data() + (size_t)(i - i0) * esz;
         if (ttype == GGML_F32) {
           memcpy(p, &v, 4);
@@ -517,7 +528,10 @@ extern "C" int mwx_write_synthetic_model(const char* path, const char* arch,
                                          int wtype, uint64_t seed) {
   using namespace mwx;
   Hparams hp;
-  if (!arch_hparams(arch ? arch : "", hp)) {
+  std::string an = arch ? arch : "";
+  const bool rich = an.size() > 5 && an.compare(an.size() - 5, 5, "-rich") == 0;
+  if (rich) an.resize(an.size() - 5);
+  if (!arch_hparams(an, hp)) {
     MWX_LOG_ERROR("mwx_write_synthetic_model: unknown arch '%s'\n",
                   arch ? arch : "(null)");
     return -1;
@@ -591,11 +605,37 @@ extern "C" int mwx_write_synthetic_model(const char* path, const char* arch,
     ln(p + ".mlp_ln", da);
   }
   ln("encoder.ln_post", da);
-  // tied token embedding: logit std ~8 for unit-variance final activations
+  // tied token embedding: logit std ~8 for unit-variance final activations.
+  // "-rich" test variants: the final LayerNorm bias b is large and the
+  // timestamp / EOT embeddings get +beta / +gamma * b/|b|^2, so timestamp and
+  // EOT logits are lifted by about beta / gamma: the token loop then emits
+  // timestamps, segment splits, EOT and seeks (with peaked, well-separated
+  // logits, so device and oracle agree token for token).
+  const float ln_b_scale = rich ? 1.0f : 0.05f;
+  const float beta = 12.0f, gamma = 30.0f;
+  std::vector<float> bdir(dt, 0.0f);
+  if (rich) {
+    double nb = 0.0;
+    for (int64_t j = 0; j < dt; ++j) {
+      bdir[j] = w.gen("decoder.ln.bias", j, 0.0f, ln_b_scale);
+      nb += (double)bdir[j] * bdir[j];
+    }
+    for (auto& x : bdir) x = (float)(x / nb);
+  }
+  const int64_t beg_id = hp.n_vocab >= 51866 ? 50365 : hp.n_vocab == 51865 ? 50364 : 50363;
+  const int64_t eot_id = hp.n_vocab >= 51865 ? 50257 : 50256;
+  std::function<float(int64_t, float)> boost = nullptr;
+  if (rich)
+    boost = [&](int64_t i, float v) {
+      const int64_t row = i / dt, col = i % dt;
+      if (row >= beg_id) return v + beta * bdir[col];
+      if (row == eot_id) return v + gamma * bdir[col];
+      return v;
+    };
   w.tensor("decoder.token_embedding.weight", {hp.n_vocab, dt}, wtype, 0.0f,
-           8.0f * std::sqrt(3.0f / (float)dt));
-  w.tensor("decoder.positional_embedding", {hp.n_text_ctx, dt}, GGML_F32, 0.0f,
-           0.2f);
+           8.0f * std::sqrt(3.0f / (float)dt), nullptr, boost);
+  const float pos_std = rich ? 1.5f : 0.2f;
+  w.tensor("decoder.positional_embedding", {hp.n_text_ctx, dt}, GGML_F32, 0.0f, pos_std);
   for (int l = 0; l < hp.n_text_layer; ++l) {
     const std::string p = "decoder.blocks." + std::to_string(l);
     lin(p + ".attn.query", dt, dt, true);
@@ -612,7 +652,8 @@ extern "C" int mwx_write_synthetic_model(const char* path, const char* arch,
     lin(p + ".mlp.2", dt, 4 * dt, true, 3.0f);
     ln(p + ".mlp_ln", dt);
   }
-  ln("decoder.ln", dt);
+  w.tensor("decoder.ln.weight", {dt}, GGML_F32, 1.0f, 0.1f);
+  w.tensor("decoder.ln.bias", {dt}, GGML_F32, 0.0f, ln_b_scale);
   w.f.close();
   return w.f ? 0 : -4;
 }

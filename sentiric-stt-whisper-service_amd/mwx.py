@@ -143,6 +143,8 @@ def lib() -> C.CDLL:
                                   C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float)]
     L.mwx_test_decode.restype = C.c_int
     L.mwx_test_decode.argtypes = [P, P, C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_float)]
+    L.mwx_test_decode_last.restype = C.c_int
+    L.mwx_test_decode_last.argtypes = [P, P, C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_float)]
     _lib = L
     return L
 
@@ -299,7 +301,8 @@ class Context:
             raise RuntimeError(f"mwx_test_mel returned {r}")
         return out
 
-    def test_encode(self, pcm: np.ndarray, seek: int = 0, cross: bool = True):
+    def test_encode(self, pcm: np.ndarray, seek: int = 0, cross: bool = True,
+                    state_index: int = 0):
         pcm = np.ascontiguousarray(pcm, dtype=np.float32)
         L_a = self.hparam("n_audio_ctx")
         d = self.d
@@ -308,7 +311,8 @@ class Context:
         k = np.empty((nl, L_a, d), dtype=np.float32) if cross else None
         v = np.empty((nl, L_a, d), dtype=np.float32) if cross else None
         null = C.POINTER(C.c_float)()
-        r = lib().mwx_test_encode(self.ctx, self.state(), fptr(pcm), len(pcm), seek, fptr(enc),
+        r = lib().mwx_test_encode(self.ctx, self.state(state_index), fptr(pcm), len(pcm), seek,
+                                  fptr(enc),
                                   fptr(k) if cross else null, fptr(v) if cross else null)
         if r != 0:
             raise RuntimeError(f"mwx_test_encode returned {r}")
@@ -322,6 +326,17 @@ class Context:
                                   len(toks), fptr(out))
         if r != 0:
             raise RuntimeError(f"mwx_test_decode returned {r}")
+        return out
+
+    def test_decode_last(self, tokens: Sequence[int], out: Optional[np.ndarray] = None,
+                         state_index: int = 0) -> np.ndarray:
+        toks = np.ascontiguousarray(tokens, dtype=np.int32)
+        if out is None:
+            out = np.empty(self.hparam("n_vocab"), dtype=np.float32)
+        r = lib().mwx_test_decode_last(self.ctx, self.state(state_index),
+                                       toks.ctypes.data_as(C.POINTER(C.c_int)), len(toks), fptr(out))
+        if r != 0:
+            raise RuntimeError(f"mwx_test_decode_last returned {r}")
         return out
 
     @property

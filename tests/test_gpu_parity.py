@@ -73,7 +73,9 @@ def run_both(ctx, o, pcm, opt: orc.FullOptions, p: mwx.FullParams):
 
 
 def service_params(ctx, beam=1, temperature_inc=0.2, language=b"auto"):
-    p = ctx.default_params(mwx.SAMPLING_GREEDY)
+    p = ctx.default_params(mwx.SAMPLING_BEAM_SEARCH if beam > 1 else mwx.SAMPLING_GREEDY)
+    if beam > 1:
+        p.beam_search.beam_size = beam
     p.token_timestamps = True
     p.suppress_nst = True
     p.no_speech_thold = 0.85
@@ -203,4 +205,113 @@ def test_fallback_batch_over_64_rows_equals_single(micro):
     for i, pcm in enumerate(pcms):
         assert ctx.full(pcm, p, state_index=base + 14 + i) == 0
         singles.append(mwx.token_ids(ctx.segments(base + 14 + i)))
+    assert batched == singles
+
+
+# ---------------------------------------------------------------- beam search
+def run_fresh(ctx, pcm, p):
+    """Run on a state never used before (decoder 0's RNG lives in the state)."""
+    idx = len(ctx.states)
+    assert ctx.full(pcm, p, state_index=idx) == 0
+    return ctx.segments(idx)
+
+
+@pytest.fixture(scope="module")
+def rich(make_model):
+    """micro weights whose token loop emits timestamps, segment splits, EOT and
+    window seeks (the plain micro model repeats one token for 220 steps)."""
+    path = make_model("micro-rich")
+    ctx = mwx.Context.open(path)
+    yield ctx, orc.Oracle(path), path
+    ctx.close()
+
+
+def test_rich_greedy_matches_oracle(rich):
+    ctx, o, _ = rich
+    for k in (0, 2):
+        pcm = pcm_clip(k)
+        opt = orc.FullOptions.service_defaults()
+        opt.temperature_inc = 0.0
+        opt.language = "en"
+        segs = run_fresh(ctx, pcm, service_params(ctx, temperature_inc=0.0, language=b"en"))
+        _, osegs, _, windows = o.full(pcm, opt)
+        assert len(segs) > 3 and len(windows) > 1  # the token loop is exercised
+        assert_same(segs, osegs)
+
+
+def test_rich_fallback_matches_oracle(rich):
+    ctx, o, _ = rich
+    pcm = pcm_clip(3)
+    opt = orc.FullOptions.service_defaults()
+    opt.language = "en"
+    segs = run_fresh(ctx, pcm, service_params(ctx, language=b"en"))
+    _, osegs, _, _ = o.full(pcm, opt)
+    assert_same(segs, osegs)
+
+
+def beam_params(ctx, temperature_inc):
+    return service_params(ctx, beam=5, temperature_inc=temperature_inc, language=b"en")
+
+
+def beam_opt(temperature_inc):
+    opt = orc.FullOptions.service_defaults(beam_size=5)
+    opt.temperature_inc = temperature_inc
+    opt.language = "en"
+    return opt
+
+
+def replay(ctx, o, pcm, opt):
+    """The oracle's whisper_full logic (logits rules, draws, beam ranking,
+    fallback, segments) run on logits the device computes for each prefix
+    (teacher-forced through the C ABI): isolates the token-loop logic from the
+    f16 noise of the logits, which can reorder beam hypotheses whose summed
+    log-probs differ by less than ~1e-2."""
+    idx = len(ctx.states)
+    ctx.state(idx)
+
+    def enc(seek):
+        ctx.test_encode(pcm, seek=seek, cross=False, state_index=idx)
+
+    def logits(tokens):
+        return ctx.test_decode_last(tokens, state_index=idx)
+
+    _, segs, _, _ = o.full_external(pcm, opt, enc, logits)
+    return segs
+
+
+@pytest.mark.parametrize("temperature_inc", [0.0, 0.2])
+def test_beam_search_replay_exact(rich, temperature_inc):
+    """The service default (src/config.h:52): beam_size 5 -> whisper.cpp beam
+    search (beam_size draws per decoder, candidates sorted by
+    sum_logprobs_all, de-duplicated, KV caches handed over between decoders),
+    with and without temperature fallback: token for token identical to the
+    oracle's beam search run on the device's logits."""
+    ctx, o, _ = rich
+    pcm = pcm_clip(0, 14.0)
+    segs = run_fresh(ctx, pcm, beam_params(ctx, temperature_inc))
+    osegs = replay(ctx, o, pcm, beam_opt(temperature_inc))
+    assert len(segs) > 1
+    assert_same(segs, osegs, p_tol=1e-4)
+
+
+def test_beam_search_tracks_oracle(rich):
+    """Against the oracle's own arithmetic: the first tokens agree until two
+    hypotheses come within float noise of each other."""
+    ctx, o, _ = rich
+    pcm = pcm_clip(0)
+    segs = run_fresh(ctx, pcm, beam_params(ctx, 0.0))
+    _, osegs, _, _ = o.full(pcm, beam_opt(0.0))
+    ids = [t.id for s in segs for t in s.tokens]
+    oids = [t.id for s in osegs for t in s.tokens]
+    assert ids[:12] == oids[:12]
+
+
+def test_beam_search_batch_equals_single(rich):
+    ctx, o, _ = rich
+    p = service_params(ctx, beam=5, language=b"en")
+    pcms = [pcm_clip(30 + k, 12.0 + 5 * k) for k in range(3)]
+    base = len(ctx.states)
+    assert ctx.full_batch_states(pcms, p, range(base, base + 3)) == 0
+    batched = [mwx.token_ids(ctx.segments(base + i)) for i in range(3)]
+    singles = [mwx.token_ids(run_fresh(ctx, pcm, p)) for pcm in pcms]
     assert batched == singles

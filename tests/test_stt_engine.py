@@ -81,7 +81,7 @@ def test_transcribe_pcm16_matches_oracle(tmp_path):
     import mwx
     import orc
     path = str(tmp_path / "ggml-micro.bin")
-    mwx.write_synthetic_model(path, "micro", mwx.GGML_F16, 11)
+    mwx.write_synthetic_model(path, "micro-rich", mwx.GGML_F16, 0)
     L = lib()
     o = orc.Oracle(path)
     try:
