@@ -18,6 +18,7 @@
 //                 K (or N for wide outputs), LDS reduction, one 16-column
 //                 strip per wave.
 #include <algorithm>
+#include <stdexcept>
 
 #include "kcommon.h"
 #include "kernels.h"
@@ -95,106 +96,247 @@ __device__ __forceinline__ typename Elt<T>::v8 ld8(const T* p) {
 }
 
 // ---------------------------------------------------------------------------
-// big tile GEMM
+// big tile GEMM (encoder, conv stem, cross K/V: M = clips x 1500 rows)
+//
+// 256x256 output tile per 512-thread workgroup (one per CU, 128 KB LDS), 8
+// waves as 2 (M) x 4 (N), each wave 128x64 outputs = 8x4 MFMA 16x16 fragments.
+// K advances in 64-deep tiles through a 2-stage LDS ring filled by LDS DMA
+// (global_load_lds, 16 B per lane): while the MFMAs of tile k run, tile k+1
+// lands in the other stage; one counted wait + raw barrier per tile. Measured
+// on the large-v3 encoder shapes (scripts/probe/gemm_variants.hip): 0.92-1.07
+// PFLOP/s vs 0.37-0.63 for a 128x128 register-staged tile.
 // ---------------------------------------------------------------------------
-constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int GWM = 2, GWN = 4;                  // wave grid
+constexpr int GFM = BM / GWM / 16, GFN = BN / GWN / 16;  // 8 x 4 fragments per wave
+constexpr int GDA = BM / 8 / 8, GDB = BN / 8 / 8;  // DMA instructions per wave per tile
 
 template <typename T, int EPI, bool OUT16>
-__global__ __launch_bounds__(256, 2) void gemm_big(const T* __restrict__ A, long lda,
+__global__ __launch_bounds__(512, 1) void gemm_big(const T* __restrict__ A, long lda,
                                                    long a_bstride, const T* __restrict__ W,
                                                    long ldw, int M, int N, int K, EpiParams P) {
   using V8 = typename Elt<T>::v8;
-  __shared__ __attribute__((aligned(16))) T lds[2][2][BM * BK];
+  // one __shared__ array only (a second one can make hipcc drain the LDS DMA
+  // before every ds_read): [stage][A rows 0..255 | W rows 0..255][64 k]
+  __shared__ __attribute__((aligned(16))) T lds[2][(BM + BN) * BK];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int bz = blockIdx.z;
+  const int wm = wid / GWN, wn = wid % GWN;
+  const int nbn = (N + BN - 1) / BN;
+  const int m0 = (blockIdx.x / nbn) * BM, n0 = (blockIdx.x % nbn) * BN;
+  const int bz = blockIdx.y;
   A += (long)bz * a_bstride;
-
-  // staging: thread t moves 16-B chunk (row = t/8 + 32 i, kc = t%8) of both
-  // 128x64 tiles; rows past M / N are clamped (their outputs are discarded)
-  const int srow = tid >> 3, kc0 = tid & 7;
-  const T* a0 = A + (long)min(m0 + srow, M - 1) * lda + kc0 * 8;
-  const T* a1 = A + (long)min(m0 + srow + 32, M - 1) * lda + kc0 * 8;
-  const T* a2 = A + (long)min(m0 + srow + 64, M - 1) * lda + kc0 * 8;
-  const T* a3 = A + (long)min(m0 + srow + 96, M - 1) * lda + kc0 * 8;
-  const T* w0 = W + (long)min(n0 + srow, N - 1) * ldw + kc0 * 8;
-  const T* w1 = W + (long)min(n0 + srow + 32, N - 1) * ldw + kc0 * 8;
-  const T* w2 = W + (long)min(n0 + srow + 64, N - 1) * ldw + kc0 * 8;
-  const T* w3 = W + (long)min(n0 + srow + 96, N - 1) * ldw + kc0 * 8;
-  // swizzled LDS offsets: (row & 7) is the same for rows srow + 32 i
-  const int soff0 = srow * BK + ((kc0 ^ (srow & 7)) << 3);
-  constexpr int SROW32 = 32 * BK;
-  uint4 ra0, ra1, ra2, ra3, rw0, rw1, rw2, rw3;
-#define GLOAD(kt)                                                   \
-  do {                                                              \
-    const int ko = (kt) * BK;                                       \
-    ra0 = *reinterpret_cast<const uint4*>(a0 + ko);                 \
-    ra1 = *reinterpret_cast<const uint4*>(a1 + ko);                 \
-    ra2 = *reinterpret_cast<const uint4*>(a2 + ko);                 \
-    ra3 = *reinterpret_cast<const uint4*>(a3 + ko);                 \
-    rw0 = *reinterpret_cast<const uint4*>(w0 + ko);                 \
-    rw1 = *reinterpret_cast<const uint4*>(w1 + ko);                 \
-    rw2 = *reinterpret_cast<const uint4*>(w2 + ko);                 \
-    rw3 = *reinterpret_cast<const uint4*>(w3 + ko);                 \
-  } while (0)
-#define SSTORE(buf)                                                                 \
-  do {                                                                              \
-    *reinterpret_cast<uint4*>(&lds[buf][0][soff0]) = ra0;                           \
-    *reinterpret_cast<uint4*>(&lds[buf][0][soff0 + SROW32]) = ra1;                  \
-    *reinterpret_cast<uint4*>(&lds[buf][0][soff0 + 2 * SROW32]) = ra2;              \
-    *reinterpret_cast<uint4*>(&lds[buf][0][soff0 + 3 * SROW32]) = ra3;              \
-    *reinterpret_cast<uint4*>(&lds[buf][1][soff0]) = rw0;                           \
-    *reinterpret_cast<uint4*>(&lds[buf][1][soff0 + SROW32]) = rw1;                  \
-    *reinterpret_cast<uint4*>(&lds[buf][1][soff0 + 2 * SROW32]) = rw2;              \
-    *reinterpret_cast<uint4*>(&lds[buf][1][soff0 + 3 * SROW32]) = rw3;              \
+  // LDS DMA: one wave instruction fills 1 KB = 8 rows x 128 B of the tile
+  // image linearly in lane order; the XOR swizzle (16-B chunk slot =
+  // kc ^ (row & 7), conflict-free fragment reads) is applied on the SOURCE
+  // address. Rows past M / N are clamped (their outputs are discarded).
+  const int lr = lane >> 3, ls = lane & 7;
+  const T* asrc[GDA];
+  const T* wsrc[GDB];
+#pragma unroll
+  for (int i = 0; i < GDA; ++i) {
+    const int r = (wid * GDA + i) * 8 + lr;
+    asrc[i] = A + (long)min(m0 + r, M - 1) * lda + (ls ^ (r & 7)) * 8;
+  }
+#pragma unroll
+  for (int i = 0; i < GDB; ++i) {
+    const int r = (wid * GDB + i) * 8 + lr;
+    wsrc[i] = W + (long)min(n0 + r, N - 1) * ldw + (ls ^ (r & 7)) * 8;
+  }
+#define GLDS(kt, st)                                                                        \
+  do {                                                                                      \
+    const int ko = (kt) * BK;                                                               \
+    _Pragma("unroll") for (int i = 0; i < GDA; ++i) __builtin_amdgcn_global_load_lds(       \
+        (const void __attribute__((address_space(1)))*)(asrc[i] + ko),                      \
+        (void __attribute__((address_space(3)))*)(&lds[st][((wid * GDA + i) * 8) * BK]), 16, \
+        0, 0);                                                                              \
+    _Pragma("unroll") for (int i = 0; i < GDB; ++i) __builtin_amdgcn_global_load_lds(       \
+        (const void __attribute__((address_space(1)))*)(wsrc[i] + ko),                      \
+        (void __attribute__((address_space(3)))*)(&lds[st][(BM + (wid * GDB + i) * 8) * BK]), \
+        16, 0, 0);                                                                          \
   } while (0)
 
-  f32x4 acc[4][4];
+  f32x4 acc[GFM][GFN];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < GFM; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
-
-  GLOAD(0);
-  SSTORE(0);
-  __syncthreads();
+    for (int j = 0; j < GFN; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
   const int nk = K / BK;
+  GLDS(0, 0);
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) GLOAD(kt + 1);
+    // tile kt has landed (this wave's DMA), then the barrier makes every
+    // wave's part visible and orders all reads of the other stage (tile kt-1)
+    // before it is refilled below
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + 1 < nk) GLDS(kt + 1, cur ^ 1);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      V8 af[4], bf[4];
+      V8 af[GFM], bf[GFN];
       const int kc = s * 4 + (lane >> 4);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = wm * 64 + i * 16 + (lane & 15);
-        af[i] = *reinterpret_cast<const V8*>(&lds[cur][0][row * BK + ((kc ^ (row & 7)) << 3)]);
+      for (int i = 0; i < GFM; ++i) {
+        const int row = wm * (BM / GWM) + i * 16 + (lane & 15);
+        af[i] = *reinterpret_cast<const V8*>(&lds[cur][row * BK + ((kc ^ (row & 7)) << 3)]);
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = wn * 64 + j * 16 + (lane & 15);
-        bf[j] = *reinterpret_cast<const V8*>(&lds[cur][1][row * BK + ((kc ^ (row & 7)) << 3)]);
+      for (int j = 0; j < GFN; ++j) {
+        const int row = BM + wn * (BN / GWN) + j * 16 + (lane & 15);
+        bf[j] = *reinterpret_cast<const V8*>(&lds[cur][row * BK + ((kc ^ (row & 7)) << 3)]);
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < GFM; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = Elt<T>::mfma(af[i], bf[j], acc[i][j]);
+        for (int j = 0; j < GFN; ++j) acc[i][j] = Elt<T>::mfma(af[i], bf[j], acc[i][j]);
     }
-    if (kt + 1 < nk) SSTORE(cur ^ 1);
-    __syncthreads();
+    // this wave's reads of `cur` have returned before its next barrier
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
-#undef GLOAD
-#undef SSTORE
+#undef GLDS
+  const int wr0 = m0 + wm * (BM / GWM), wc0 = n0 + wn * (BN / GWN);
+  constexpr bool STAGED16 = EPI == EPI_GELU || EPI == EPI_ENC_QKV || EPI == EPI_CROSS_KV;
+  constexpr bool STAGED32 = EPI == EPI_RES || EPI == EPI_CONV2;
+  if ((STAGED16 || STAGED32) && (N & 63) == 0 && !P.pack_out) {
+    // Epilogue through LDS: the ring is idle now; each wave stages its 128x64
+    // tile (16 KB) so every global store is a 16-B (8-B for V^T) vector.
+    __builtin_amdgcn_s_barrier();  // all waves are past their last ring read
+    if (wc0 >= N) return;          // (N % 64 == 0: a wave's 64 columns are all in or all out)
+    uint16_t* wl = reinterpret_cast<uint16_t*>(&lds[0][0]) + wid * 8192;
+    float* wlf = reinterpret_cast<float*>(wl);
+    if constexpr (STAGED16) {
+      // a wave's 64 columns are one head (d % 64 == 0): part / layer / head / k|v
+      int part = 0, h = 0, layer = 0;
+      if constexpr (EPI == EPI_ENC_QKV) {
+        part = wc0 / P.d;
+        h = (wc0 - part * P.d) >> 6;
+      } else if constexpr (EPI == EPI_CROSS_KV) {
+        layer = wc0 / (2 * P.d);
+        const int rr = wc0 - layer * 2 * P.d;
+        part = rr >= P.d;
+        h = (rr - part * P.d) >> 6;
+      }
+      const bool transposed = EPI == EPI_ENC_QKV && part == 2;  // V^T [e][t]
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < GFM; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+        for (int j = 0; j < GFN; ++j) {
+          const int lc = j * 16 + (lane & 15);
+          const int n = wc0 + lc;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int lr = i * 16 + (lane >> 4) * 4 + r;
+            const float a = acc[i][j][r];
+            uint16_t bits;
+            if constexpr (EPI == EPI_GELU) {
+              const float g = gelu_ggml(a + P.bias[n]);
+              if constexpr (OUT16) {
+                const _Float16 hv = (_Float16)g;
+                bits = __builtin_bit_cast(uint16_t, hv);
+              } else {
+                const T tv = to_t<T>(g);
+                bits = __builtin_bit_cast(uint16_t, tv);
+              }
+            } else if constexpr (EPI == EPI_ENC_QKV) {
+              const _Float16 hv = (_Float16)(a + P.bias[n]);
+              bits = __builtin_bit_cast(uint16_t, hv);
+            } else {  // cross K: f16(acc * kscale); V: f16(acc + b)
+              const _Float16 hv = part ? (_Float16)(a + P.bias[n]) : (_Float16)(a * P.kscale);
+              bits = __builtin_bit_cast(uint16_t, hv);
+            }
+            wl[transposed ? lc * 128 + lr : lr * 64 + lc] = bits;
+          }
+        }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (!transposed) {
+        // 128 rows x 128 B: 8 rows per wave instruction
+#pragma unroll 4
+        for (int it = 0; it < 16; ++it) {
+          const int row = it * 8 + (lane >> 3), ch = lane & 7;
+          const int m = wr0 + row;
+          if (m >= M) continue;
+          const uint4 v = *reinterpret_cast<const uint4*>(&wl[row * 64 + ch * 8]);
+          _Float16* dst;
+          if constexpr (EPI == EPI_GELU) {
+            dst = reinterpret_cast<_Float16*>(P.c16) + (long)bz * P.c_bstride + (long)m * P.ldc +
+                  wc0 + ch * 8;
+          } else {
+            const int b = m / P.L, t = m - b * P.L;
+            if constexpr (EPI == EPI_ENC_QKV) {
+              dst = (part == 0 ? P.q : P.k) + (((long)b * P.H + h) * P.L + t) * 64 + ch * 8;
+            } else {
+              const long idx =
+                  ((((long)layer * P.ncap + P.slot[b]) * P.H + h) * P.L + t) * 64 + ch * 8;
+              dst = (part ? P.v : P.k) + idx;
+            }
+          }
+          *reinterpret_cast<uint4*>(dst) = v;
+        }
+      } else {
+        // V^T: 64 rows (e) x 128 t; 4-t groups (8 B) never straddle a clip
+        // (L % 4 == 0, m0 % 4 == 0)
+#pragma unroll 4
+        for (int it = 0; it < 32; ++it) {
+          const int e = it * 2 + (lane >> 5), tg = lane & 31;
+          const int m = wr0 + tg * 4;
+          if (m >= M) continue;
+          const uint2 v = *reinterpret_cast<const uint2*>(&wl[e * 128 + tg * 4]);
+          const int b = m / P.L, t = m - b * P.L;
+          *reinterpret_cast<uint2*>(P.v + (((long)b * P.H + h) * 64 + e) * P.ldv + t) = v;
+        }
+      }
+    } else {
+      // f32 outputs (residual stream): two 64-row halves of the wave tile
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+#pragma unroll
+        for (int i = hh * (GFM / 2); i < (hh + 1) * (GFM / 2); ++i)
+#pragma unroll
+          for (int j = 0; j < GFN; ++j) {
+            const int lc = j * 16 + (lane & 15);
+            const float bv = P.bias ? P.bias[wc0 + lc] : 0.0f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int lr = (i - hh * (GFM / 2)) * 16 + (lane >> 4) * 4 + r;
+              const float a = acc[i][j][r] + bv;
+              wlf[lr * 64 + lc] = EPI == EPI_CONV2 ? gelu_ggml(a) : a;
+            }
+          }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 4
+        for (int it = 0; it < 16; ++it) {
+          const int row = it * 4 + (lane >> 4), ch = lane & 15;
+          const int m = wr0 + hh * 64 + row;
+          if (m >= M) continue;
+          const f32x4 v = *reinterpret_cast<const f32x4*>(&wlf[row * 64 + ch * 4]);
+          const long idx = (long)bz * P.c_bstride + (long)m * P.ldc + wc0 + ch * 4;
+          f32x4 o;
+          if constexpr (EPI == EPI_RES) {
+            const f32x4 res = *reinterpret_cast<const f32x4*>(P.r32 + idx);
+            o = v + res;  // (acc + bias) + residual
+          } else {
+            const f32x4 pe = *reinterpret_cast<const f32x4*>(P.pe + (long)m * P.ldc + wc0 + ch * 4);
+            o = pe + v;  // pe + gelu(acc + bias)
+          }
+          *reinterpret_cast<f32x4*>(P.c32 + idx) = o;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < GFM; ++i)
+#pragma unroll
+    for (int j = 0; j < GFN; ++j) {
+      const int n = wc0 + j * 16 + (lane & 15);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        const int m = wr0 + i * 16 + (lane >> 4) * 4 + r;
         if (m < M && n < N) epi_store<EPI, T, OUT16>(P, bz, m, n, acc[i][j][r]);
       }
     }
@@ -408,8 +550,9 @@ template bool gemm_decode<__bf16>(int, const __bf16*, const __bf16*, int, int, i
 template <typename T, int EPI, bool OUT16>
 static void gemm_dispatch(const T* A, long lda, long a_bstride, const T* W, long ldw, int M,
                           int N, int K, int batch, const EpiParams& P, hipStream_t st) {
-  dim3 g((N + BN - 1) / BN, (M + BM - 1) / BM, batch);
-  gemm_big<T, EPI, OUT16><<<g, 256, 0, st>>>(A, lda, a_bstride, W, ldw, M, N, K, P);
+  if (K % BK) throw std::runtime_error("mwx: gemm K must be a multiple of 64");
+  dim3 g(((N + BN - 1) / BN) * ((M + BM - 1) / BM), batch);
+  gemm_big<T, EPI, OUT16><<<g, 512, 0, st>>>(A, lda, a_bstride, W, ldw, M, N, K, P);
 }
 
 template <typename T>
