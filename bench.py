@@ -50,7 +50,7 @@ def kernel_model(arch, kclass, clips, rows, launches, prompt_len, steps):
     if kclass == "dec_attn_cross":
         # every active row reads its clip's cross K and V for one layer (f16)
         b = rows * (L * d * 2 * 2 + d * 2 * 2)
-        return "hbm", b, f"{rows} rows x (K+V 1500x{d} f16 + q/o) per launch"
+        return "hbm", b, f"{rows:g} rows x (K+V 1500x{d} f16 + q/o) per launch"
     if kclass == "enc_gemm":
         conv = 2 * T * d * 3 * n_mels + 2 * L * d * 3 * d
         layer = 2 * L * d * (3 * d + d + 4 * d + 4 * d)
@@ -203,7 +203,13 @@ def main():
     if rank == 0:
         launches = max(1, nl.value)
         avg_s = tot_ms.value / 1e3 / launches
-        bound, work, desc = kernel_model(args.arch, args.perf_class, args.clips, args.clips,
+        # decode kernels run per row group (MWX_DECODE_GROUPS chains on their
+        # own streams): rows per launch from the launch count of the timed steps
+        n_dec_steps = prompt_len + args.decode_steps - 1
+        rows = args.clips
+        if args.perf_class.startswith("dec_attn"):
+            rows = args.clips * ARCH[args.arch][4] * n_dec_steps * args.steps / launches
+        bound, work, desc = kernel_model(args.arch, args.perf_class, args.clips, rows,
                                          launches // max(1, args.steps), prompt_len,
                                          args.decode_steps)
         traffic = None

@@ -108,9 +108,15 @@ struct Segment {
   bool speaker_turn_next;
 };
 
+constexpr int MWX_MAX_GROUPS = 4;
+
 struct State {
   Context* ctx = nullptr;
   hipStream_t stream = nullptr;
+  // decode row groups: group g > 0 runs on gstream[g] (group 0 on `stream`);
+  // ev_in orders the groups after the step inputs, ev_done joins them
+  hipStream_t gstream[MWX_MAX_GROUPS] = {};
+  hipEvent_t ev_in = nullptr, ev_done[MWX_MAX_GROUPS] = {};
   // encoder workspace (clip-batched)
   DBuf pcm, mel, melmax, melT, h1p, x, h, q, k, vt, o, ff, enc, cross_k, cross_v;
   DBuf energy;
@@ -152,7 +158,9 @@ struct PerfScope {
   State& S;
   bool on;
   hipEvent_t stop = nullptr;
-  PerfScope(State& s, const char* cls) : S(s), on(!s.perf_class.empty() && s.perf_class == cls) {
+  hipStream_t stream;
+  PerfScope(State& s, const char* cls, hipStream_t strm = nullptr)
+      : S(s), on(!s.perf_class.empty() && s.perf_class == cls), stream(strm ? strm : s.stream) {
     if (!on) return;
     std::vector<hipEvent_t>& ev = S.capturing ? S.perf_gev : S.perf_ev;
     size_t& used = S.capturing ? S.perf_gused : S.perf_used;
@@ -170,7 +178,7 @@ struct PerfScope {
   // cannot time events recorded *through* capture; explicit nodes time fine).
   void record(hipEvent_t e) {
     if (!S.capturing) {
-      HIPC(hipEventRecord(e, S.stream));
+      HIPC(hipEventRecord(e, stream));
       return;
     }
     hipStreamCaptureStatus cs;
@@ -178,10 +186,10 @@ struct PerfScope {
     hipGraph_t g = nullptr;
     const hipGraphNode_t* deps = nullptr;
     size_t ndeps = 0;
-    HIPC(hipStreamGetCaptureInfo_v2(S.stream, &cs, &cid, &g, &deps, &ndeps));
+    HIPC(hipStreamGetCaptureInfo_v2(stream, &cs, &cid, &g, &deps, &ndeps));
     hipGraphNode_t node;
     HIPC(hipGraphAddEventRecordNode(&node, g, deps, ndeps, e));
-    HIPC(hipStreamUpdateCaptureDependencies(S.stream, &node, 1, hipStreamSetCaptureDependencies));
+    HIPC(hipStreamUpdateCaptureDependencies(stream, &node, 1, hipStreamSetCaptureDependencies));
   }
   ~PerfScope() {
     if (!on) return;
@@ -682,7 +690,8 @@ struct Driver {
     S.pq.get((size_t)8 * R * d * 4);
     S.xd.get((size_t)R * d * 4, true);
     // decode-GEMM A operands (fragment tiles), rows padded to the 64-row block
-    const size_t R64 = (size_t)(R + 63) / 64 * 64;
+    // (+ one 64-row block per decode group: each group's region is padded)
+    const size_t R64 = (size_t)(R + 63) / 64 * 64 + 64 * MWX_MAX_GROUPS;
     S.hd.get(R64 * d * sizeof(T), true);
     S.od.get(R64 * d * sizeof(T), true);
     S.ffd.get(R64 * 4 * d * sizeof(T), true);
@@ -708,24 +717,56 @@ struct Driver {
                  L_dec, H, Tctx, dp, n, stage, npos, st);
   }
 
-  // one decoder step for R rows; inputs already in S.stepin / S.ctl
-  void decode_step(int R, bool want_probs) {
+  // one decoder step for all R rows on the state's stream; inputs already in
+  // S.stepin / S.ctl
+  void decode_step(int R, bool want_probs) { decode_group(R, 0, R, 0, want_probs, st); }
+
+  // Row groups of a step: with MWX_DECODE_GROUPS=G > 1 the rows are split into
+  // G groups that run as independent launch chains (one hipGraph each) on
+  // their own streams, so the latency-bound projections / LayerNorms of one
+  // group can overlap the HBM-bound cross-attention of another. Every kernel
+  // is row-blocked, so a row's arithmetic is the same in any group. Measured
+  // on MI355X (large-v3, 32 rows): G=2 is 8% slower than G=1 (the split
+  // doubles the weight stream and a stream beside a chain keeps only part of
+  // its rate), so the default is one group.
+  struct Group {
+    int r0, n;
+    size_t prow;  // first row of the group's region in the packed A buffers
+  };
+  std::vector<Group> groups_for(int R) const {
+    int G = 1;
+    if (const char* e = getenv("MWX_DECODE_GROUPS")) G = atoi(e);
+    G = std::max(1, std::min(G, MWX_MAX_GROUPS));
+    if (R < 16 * G) G = std::max(1, R / 16);
+    std::vector<Group> gs;
+    size_t prow = 0;
+    for (int g = 0; g < G; ++g) {
+      const int r0 = (int)((long)R * g / G), r1 = (int)((long)R * (g + 1) / G);
+      gs.push_back(Group{r0, r1 - r0, prow});
+      prow += (size_t)(r1 - r0 + 63) / 64 * 64;
+    }
+    return gs;
+  }
+
+  // decoder step for rows [r0, r0+n) of an R-row step, launched on `s`
+  void decode_group(int R, int r0, int n, size_t prow, bool want_probs, hipStream_t s) {
     int* si = (int*)S.stepin.p;
-    const int* tok = si;
-    const int* pos = si + R;
-    const int* act = si + 2 * R;
-    const int* xidx = si + 3 * R;
-    float* xd = (float*)S.xd.p;
-    T* hd = (T*)S.hd.p;
-    T* od = (T*)S.od.p;
-    T* ffd = (T*)S.ffd.p;
+    const int* tok = si + r0;
+    const int* pos = si + R + r0;
+    const int* act = si + 2 * R + r0;
+    const int* xidx = si + 3 * R + r0;
+    float* xd = (float*)S.xd.p + (size_t)r0 * d;
+    T* hd = (T*)S.hd.p + prow * d;
+    T* od = (T*)S.od.p + prow * d;
+    T* ffd = (T*)S.ffd.p + prow * 4 * d;
     const float kqs = powf(64.0f, -0.25f);
-    embed<T>(Wt(C.tok_emb), C.dec_pe, tok, pos, act, xd, R, d, st);
+    embed<T>(Wt(C.tok_emb), C.dec_pe, tok, pos, act, xd, n, d, s);
     const size_t layer_self = (size_t)S.row_cap * H * Tctx * 64;
     const size_t layer_cross = (size_t)S.cross_cap * H * hp.n_audio_ctx * 64;
-    float* Pqkv = (float*)S.pqkv.p;
-    float* Pres = (float*)S.pres.p;
-    float* Pq = (float*)S.pq.p;
+    // the group's split-K slabs [KS][n][N] live inside the R-row slab buffers
+    float* Pqkv = (float*)S.pqkv.p + (size_t)8 * r0 * 3 * d;
+    float* Pres = (float*)S.pres.p + (size_t)8 * r0 * d;
+    float* Pq = (float*)S.pq.p + (size_t)8 * r0 * d;
     // The d- and 3d-wide projections run as split-K GEMMs writing f32 partial
     // slabs; each consumer (LN: bias + residual, attention: bias/scale/f16 and
     // the KV-cache append) folds the slabs in, so no launch is added.
@@ -733,62 +774,64 @@ struct Driver {
     const float* bias_prev = nullptr;
     for (int l = 0; l < L_dec; ++l) {
       const DecLayerW& W = C.dec[l];
-      _Float16* ks = (_Float16*)S.kself.p + l * layer_self;
-      _Float16* vs = (_Float16*)S.vself.p + l * layer_self;
-      layer_norm_dec<T>(xd, W.ln1_w, W.ln1_b, hd, R, d, act, st, ks_prev ? Pres : nullptr,
+      _Float16* ks = (_Float16*)S.kself.p + l * layer_self + (size_t)r0 * H * Tctx * 64;
+      _Float16* vs = (_Float16*)S.vself.p + l * layer_self + (size_t)r0 * H * Tctx * 64;
+      layer_norm_dec<T>(xd, W.ln1_w, W.ln1_b, hd, n, d, act, s, ks_prev ? Pres : nullptr,
                         ks_prev, bias_prev);
       int k1;
-      { PerfScope ps(S, "dec_gemm");
-        k1 = gemm_splitk_partials<T>(hd, Wt(W.qkv_w), R, 3 * d, d, Pqkv, st); }
-      { PerfScope ps(S, "dec_attn_self");
+      { PerfScope ps(S, "dec_gemm", s);
+        k1 = gemm_splitk_partials<T>(hd, Wt(W.qkv_w), n, 3 * d, d, Pqkv, s); }
+      { PerfScope ps(S, "dec_attn_self", s);
         dec_attention<T>(Pqkv, k1, 3 * d, W.qkv_b, kqs, kqs, ks, vs, nullptr, pos, act, 0, Tctx,
-                         od, R, H, 1.0f, st); }
+                         od, n, H, 1.0f, s); }
       int k2;
-      { PerfScope ps(S, "dec_gemm");
-        k2 = gemm_splitk_partials<T>(od, Wt(W.o_w), R, d, d, Pres, st); }
-      layer_norm_dec<T>(xd, W.lnc_w, W.lnc_b, hd, R, d, act, st, Pres, k2, W.o_b);
+      { PerfScope ps(S, "dec_gemm", s);
+        k2 = gemm_splitk_partials<T>(od, Wt(W.o_w), n, d, d, Pres, s); }
+      layer_norm_dec<T>(xd, W.lnc_w, W.lnc_b, hd, n, d, act, s, Pres, k2, W.o_b);
       int k3;
-      { PerfScope ps(S, "dec_gemm");
-        k3 = gemm_splitk_partials<T>(hd, Wt(W.cq_w), R, d, d, Pq, st); }
-      { PerfScope ps(S, "dec_attn_cross");
+      { PerfScope ps(S, "dec_gemm", s);
+        k3 = gemm_splitk_partials<T>(hd, Wt(W.cq_w), n, d, d, Pq, s); }
+      { PerfScope ps(S, "dec_attn_cross", s);
         dec_attention<T>(Pq, k3, d, W.cq_b, 1.0f, 1.0f,
                          (_Float16*)S.cross_k.p + l * layer_cross,
                          (_Float16*)S.cross_v.p + l * layer_cross, xidx, pos, act,
-                         hp.n_audio_ctx, hp.n_audio_ctx, od, R, H, kqs, st); }
+                         hp.n_audio_ctx, hp.n_audio_ctx, od, n, H, kqs, s); }
       int k4;
-      { PerfScope ps(S, "dec_gemm");
-        k4 = gemm_splitk_partials<T>(od, Wt(W.co_w), R, d, d, Pres, st); }
-      layer_norm_dec<T>(xd, W.ln2_w, W.ln2_b, hd, R, d, act, st, Pres, k4, W.co_b);
+      { PerfScope ps(S, "dec_gemm", s);
+        k4 = gemm_splitk_partials<T>(od, Wt(W.co_w), n, d, d, Pres, s); }
+      layer_norm_dec<T>(xd, W.ln2_w, W.ln2_b, hd, n, d, act, s, Pres, k4, W.co_b);
       EpiParams e;
       e.bias = W.fc1_b;
       e.c16 = ffd;
       e.ldc = 4 * d;
       e.pack_out = true;
       bool k5;
-      { PerfScope ps(S, "dec_gemm");
-        k5 = gemm_decode<T>(EPI_GELU, hd, Wt(W.fc1_w), R, 4 * d, d, e, st); }
-      { PerfScope ps(S, "dec_gemm");
-        ks_prev = gemm_splitk_partials<T>(ffd, Wt(W.fc2_w), R, d, 4 * d, Pres, st); }
+      { PerfScope ps(S, "dec_gemm", s);
+        k5 = gemm_decode<T>(EPI_GELU, hd, Wt(W.fc1_w), n, 4 * d, d, e, s); }
+      { PerfScope ps(S, "dec_gemm", s);
+        ks_prev = gemm_splitk_partials<T>(ffd, Wt(W.fc2_w), n, d, 4 * d, Pres, s); }
       bias_prev = W.fc2_b;
       if (!k1 || !k2 || !k3 || !k4 || !k5 || !ks_prev) throw std::runtime_error("mwx: unsupported split-K shape");
     }
-    layer_norm_dec<T>(xd, C.dec_ln_w, C.dec_ln_b, hd, R, d, act, st, Pres, ks_prev, bias_prev);
+    layer_norm_dec<T>(xd, C.dec_ln_w, C.dec_ln_b, hd, n, d, act, s, Pres, ks_prev, bias_prev);
     EpiParams e;
-    e.c32 = (float*)S.logits.p;
+    e.c32 = (float*)S.logits.p + (size_t)r0 * V;
     e.ldc = V;
-    { PerfScope ps(S, "logits_gemm");
-    if (!gemm_decode<T>(EPI_F32, hd, Wt(C.tok_emb_p), R, V, d, e, st))
+    { PerfScope ps(S, "logits_gemm", s);
+    if (!gemm_decode<T>(EPI_F32, hd, Wt(C.tok_emb_p), n, V, d, e, s))
       throw std::runtime_error("mwx: unsupported logits GEMM shape"); }
     float* pr = nullptr;
     float* lp = nullptr;
     if (want_probs) {
-      pr = (float*)S.probs.get((size_t)R * V * 4);
-      lp = (float*)S.logprobs.get((size_t)R * V * 4);
+      pr = (float*)S.probs.get((size_t)R * V * 4) + (size_t)r0 * V;
+      lp = (float*)S.logprobs.get((size_t)R * V * 4) + (size_t)r0 * V;
     }
-    PerfScope ps(S, "logits_proc");
-    logits_process((float*)S.logits.p, (const float*)S.smask.p, (const RowCtl*)S.ctl.p,
-                   (TokOut*)S.tokout.p, pr, lp, LC, R,
-                   LPScratch{(float*)S.lpflt.p, (LPPart*)S.lpparts.p, (LPRes*)S.lpres.p}, st);
+    PerfScope ps(S, "logits_proc", s);
+    logits_process((float*)S.logits.p + (size_t)r0 * V, (const float*)S.smask.p,
+                   (const RowCtl*)S.ctl.p + r0, (TokOut*)S.tokout.p + r0, pr, lp, LC, n,
+                   LPScratch{(float*)S.lpflt.p + (size_t)r0 * V, (LPPart*)S.lpparts.p + r0 * LP_G,
+                             (LPRes*)S.lpres.p + r0 * LP_G},
+                   s);
   }
 };
 
