@@ -186,6 +186,48 @@ static int lang_id(const std::string& s) {
   return -1;
 }
 
+// ggml legacy block quantizations (ggml-common.h block_q4_0 .. block_q8_0;
+// type ids Q4_0 = 2, Q4_1 = 3, Q5_0 = 6, Q5_1 = 7, Q8_0 = 8): 32 elements per
+// block, f16 scale d (and min m for the _1 variants), ggml dequantize_row_q*.
+static int quant_block_bytes(int tt) {
+  switch (tt) {
+    case 2: return 18;
+    case 3: return 20;
+    case 6: return 22;
+    case 7: return 24;
+    case 8: return 34;
+    default: return 0;
+  }
+}
+static void dequant_blocks(int tt, const uint8_t* q, float* y, int64_t n) {
+  const int bb = quant_block_bytes(tt);
+  for (int64_t b = 0; b < n / 32; ++b, q += bb, y += 32) {
+    uint16_t hd, hm = 0;
+    memcpy(&hd, q, 2);
+    const float d = h2f(hd);
+    const bool has_min = tt == 3 || tt == 7;
+    if (has_min) memcpy(&hm, q + 2, 2);
+    const float m = has_min ? h2f(hm) : 0.0f;
+    for (int j = 0; j < 32; ++j) {
+      int v;  // the quantized integer of element j
+      if (tt == 8) {
+        v = (int8_t)q[2 + j];
+      } else {
+        const int hi = j >= 16;
+        const uint8_t* qs = q + (tt == 2 ? 2 : tt == 3 ? 4 : tt == 6 ? 6 : 8);
+        v = hi ? (qs[j - 16] >> 4) : (qs[j] & 0x0F);
+        if (tt == 6 || tt == 7) {  // fifth bit from qh, element j at bit j
+          uint32_t qh;
+          memcpy(&qh, q + (tt == 6 ? 2 : 4), 4);
+          v |= (int)((qh >> j) & 1u) << 4;
+        }
+      }
+      if (has_min) y[j] = (float)v * d + m;
+      else y[j] = (float)(v - (tt == 2 ? 8 : tt == 6 ? 16 : 0)) * d;
+    }
+  }
+}
+
 static bool load(const char* path, Model& m) {
   std::ifstream f(path, std::ios::binary);
   if (!f) return false;
@@ -272,6 +314,15 @@ static bool load(const char* path, Model& m) {
     T.v.resize(n);
     if (tt == T_F32) {
       f.read((char*)T.v.data(), n * 4);
+    } else if (quant_block_bytes(tt) > 0) {
+      // whisper.cpp quantize-tool output: dequantized (ggml dequantize_row_q*)
+      // and rounded once to f16, the engine's compute type for these files
+      if (T.ne[0] % 32) return false;
+      std::vector<uint8_t> q((size_t)(n / 32) * quant_block_bytes(tt));
+      f.read((char*)q.data(), q.size());
+      dequant_blocks(tt, q.data(), T.v.data(), n);
+      for (int64_t i = 0; i < n; ++i) T.v[i] = f16_round(T.v[i]);
+      if (name == "decoder.token_embedding.weight") m.wtype = T_F16;
     } else {
       std::vector<uint16_t> h(n);
       f.read((char*)h.data(), n * 2);
@@ -1529,6 +1580,15 @@ void orc_hparams(void* h, int* out) {
   for (int i = 0; i < 11; ++i) out[i] = m->hp[i];
 }
 int orc_wtype(void* h) { return ((Model*)h)->wtype; }
+// copies the (loaded, dequantized) values of tensor `name`; returns its size
+long orc_tensor(void* h, const char* name, float* out, long cap) {
+  const Model* m = (const Model*)h;
+  auto it = m->t.find(name);
+  if (it == m->t.end()) return -1;
+  const long n = (long)it->second.v.size();
+  if (out) memcpy(out, it->second.v.data(), sizeof(float) * std::min(n, cap));
+  return n;
+}
 void orc_special(void* h, int* out) {
   auto* m = (Model*)h;
   int v[9] = {m->eot, m->sot, m->translate, m->transcribe, m->solm, m->prev, m->nosp, m->not_, m->beg};

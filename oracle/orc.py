@@ -48,6 +48,8 @@ def lib() -> C.CDLL:
     L.orc_wtype.restype = C.c_int
     L.orc_wtype.argtypes = [P]
     L.orc_special.argtypes = [P, C.POINTER(C.c_int)]
+    L.orc_tensor.restype = C.c_long
+    L.orc_tensor.argtypes = [P, C.c_char_p, fp, C.c_long]
     L.orc_token_str.restype = C.c_char_p
     L.orc_token_str.argtypes = [P, C.c_int]
     L.orc_filters.restype = fp
@@ -181,6 +183,16 @@ class Oracle:
     @property
     def n_text_layer(self):
         return self.hp[8]
+
+    def tensor(self, name: str) -> np.ndarray:
+        """Loaded values of one tensor (quantized types: dequantized, f16-rounded)."""
+        L = lib()
+        n = L.orc_tensor(self.h, name.encode(), None, 0)
+        if n < 0:
+            raise KeyError(name)
+        out = np.empty(n, np.float32)
+        L.orc_tensor(self.h, name.encode(), _fp(out), n)
+        return out
 
     def filters(self) -> np.ndarray:
         p = lib().orc_filters(self.h)

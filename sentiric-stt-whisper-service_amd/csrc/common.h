@@ -13,8 +13,28 @@
 
 namespace mwx {
 
-// ggml tensor types used by whisper .bin files (ggml.h enum ggml_type values).
-enum GgmlType : int32_t { GGML_F32 = 0, GGML_F16 = 1, GGML_BF16 = 30 };
+// ggml tensor types used by whisper .bin files (ggml.h enum ggml_type values):
+// f32 / f16 / bf16 and the legacy 32-element block quantizations written by
+// whisper.cpp's quantize tool.
+enum GgmlType : int32_t {
+  GGML_F32 = 0,
+  GGML_F16 = 1,
+  GGML_Q4_0 = 2,
+  GGML_Q4_1 = 3,
+  GGML_Q5_0 = 6,
+  GGML_Q5_1 = 7,
+  GGML_Q8_0 = 8,
+  GGML_BF16 = 30
+};
+
+// quant.cpp: block formats (ggml-common.h) and ggml's reference (de)quantizers
+bool ggml_type_is_quant(int type);
+// bytes of an n-element tensor with inner dim ne0 (0: unsupported type/shape)
+size_t ggml_tensor_bytes(int type, int64_t ne0, int64_t n);
+void ggml_dequantize(int type, const uint8_t* src, float* dst, int64_t n);
+void ggml_quantize(int type, const float* src, uint8_t* dst, int64_t n);
+// whisper hparams.ftype (ggml_ftype) of a file whose 2-D weights are `type`
+int ggml_ftype_of(int type);
 
 // The 11 int32 header fields of a whisper ggml .bin file, in file order
 // (whisper.cpp whisper_model_load; upstream converter convert-pt-to-ggml.py).

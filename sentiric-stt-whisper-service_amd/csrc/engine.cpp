@@ -208,24 +208,24 @@ static const FileTensor* find_t(const ModelFile& mf, const std::string& n) {
   return it == mf.tensors.end() ? nullptr : &it->second;
 }
 
-static float elem_f32(const FileTensor& t, size_t i) {
+// f32 values of a whole tensor: f32 / f16 / bf16 exactly, block-quantized
+// types through ggml's dequantize_row_q* (quant.cpp)
+static std::vector<float> tensor_f32(const FileTensor& t) {
+  const int64_t n = t.nelements();
+  std::vector<float> v(n);
   switch (t.type) {
-    case GGML_F32: {
-      float f;
-      memcpy(&f, t.data.data() + i * 4, 4);
-      return f;
-    }
-    case GGML_F16: {
-      uint16_t h;
-      memcpy(&h, t.data.data() + i * 2, 2);
-      return f16_to_f32(h);
-    }
-    default: {
-      uint16_t h;
-      memcpy(&h, t.data.data() + i * 2, 2);
-      return bf16_to_f32(h);
-    }
+    case GGML_F32: memcpy(v.data(), t.data.data(), n * 4); break;
+    case GGML_F16:
+    case GGML_BF16:
+      for (int64_t i = 0; i < n; ++i) {
+        uint16_t h;
+        memcpy(&h, t.data.data() + i * 2, 2);
+        v[i] = t.type == GGML_F16 ? f16_to_f32(h) : bf16_to_f32(h);
+      }
+      break;
+    default: ggml_dequantize(t.type, t.data.data(), v.data(), n); break;
   }
+  return v;
 }
 
 namespace {
@@ -276,8 +276,7 @@ static bool upload_model(Context& C, const ModelFile& mf) {
       ok = false;
       return;
     }
-    std::vector<float> v(expect);
-    for (int64_t i = 0; i < expect; ++i) v[i] = elem_f32(*t, i);
+    const std::vector<float> v = tensor_f32(*t);
     A.add(v.data(), v.size() * 4, (const void**)slot);
   };
   // 16-bit weight rows in the model type, concatenated from several tensors
@@ -304,11 +303,9 @@ static bool upload_model(Context& C, const ModelFile& mf) {
       const int want = bf ? GGML_BF16 : GGML_F16;
       if (t->type == want) {
         memcpy(dst, t->data.data(), n * 2);
-      } else {
-        for (int64_t i = 0; i < n; ++i) {
-          const float f = elem_f32(*t, i);
-          dst[i] = bf ? f32_to_bf16(f) : f32_to_f16(f);
-        }
+      } else {  // (quantized files: dequantized once, computed in f16)
+        const std::vector<float> f = tensor_f32(*t);
+        for (int64_t i = 0; i < n; ++i) dst[i] = bf ? f32_to_bf16(f[i]) : f32_to_f16(f[i]);
       }
       dst += n;
     }
@@ -354,15 +351,16 @@ static bool upload_model(Context& C, const ModelFile& mf) {
     const FileTensor* c2 = need("encoder.conv2.weight");
     if (!c1 || !c2) return false;
     const int nm = hp.n_mels, cp = C.cpad;
+    const std::vector<float> f1 = tensor_f32(*c1), f2 = tensor_f32(*c2);
     std::vector<uint16_t> w1((size_t)d * 3 * cp, 0), w2((size_t)d * 3 * d);
     for (int o = 0; o < d; ++o)
       for (int c = 0; c < nm; ++c)
         for (int kk = 0; kk < 3; ++kk)
-          w1[((size_t)o * 3 + kk) * cp + c] = f32_to_f16(elem_f32(*c1, ((size_t)o * nm + c) * 3 + kk));
+          w1[((size_t)o * 3 + kk) * cp + c] = f32_to_f16(f1[((size_t)o * nm + c) * 3 + kk]);
     for (int o = 0; o < d; ++o)
       for (int c = 0; c < d; ++c)
         for (int kk = 0; kk < 3; ++kk)
-          w2[((size_t)o * 3 + kk) * d + c] = f32_to_f16(elem_f32(*c2, ((size_t)o * d + c) * 3 + kk));
+          w2[((size_t)o * 3 + kk) * d + c] = f32_to_f16(f2[((size_t)o * d + c) * 3 + kk]);
     A.add(w1.data(), w1.size() * 2, (const void**)&C.conv1_w);
     A.add(w2.data(), w2.size() * 2, (const void**)&C.conv2_w);
   }
@@ -383,9 +381,10 @@ static bool upload_model(Context& C, const ModelFile& mf) {
       const FileTensor* vb = need(p + ".attn.value.bias");
       if (!qb || !vb) return false;
       std::vector<float> b(3 * d, 0.0f);
+      const std::vector<float> fq = tensor_f32(*qb), fv = tensor_f32(*vb);
       for (int i = 0; i < d; ++i) {
-        b[i] = elem_f32(*qb, i);
-        b[2 * d + i] = elem_f32(*vb, i);
+        b[i] = fq[i];
+        b[2 * d + i] = fv[i];
       }
       A.add(b.data(), b.size() * 4, (const void**)&L.qkv_b);
     }
@@ -419,9 +418,10 @@ static bool upload_model(Context& C, const ModelFile& mf) {
       const FileTensor* vb = need(p + ".attn.value.bias");
       if (!qb || !vb) return false;
       std::vector<float> b(3 * dt, 0.0f);
+      const std::vector<float> fq = tensor_f32(*qb), fv = tensor_f32(*vb);
       for (int i = 0; i < dt; ++i) {
-        b[i] = elem_f32(*qb, i);
-        b[2 * dt + i] = elem_f32(*vb, i);
+        b[i] = fq[i];
+        b[2 * dt + i] = fv[i];
       }
       A.add(b.data(), b.size() * 4, (const void**)&L.qkv_b);
     }
@@ -440,7 +440,8 @@ static bool upload_model(Context& C, const ModelFile& mf) {
     const FileTensor* vb = need(p + ".cross_attn.value.bias");
     if (!vb) return false;
     for (int i = 0; i < dt; ++i) cross_b.push_back(0.0f);
-    for (int i = 0; i < dt; ++i) cross_b.push_back(elem_f32(*vb, i));
+    const std::vector<float> fv = tensor_f32(*vb);
+    for (int i = 0; i < dt; ++i) cross_b.push_back(fv[i]);
   }
   w16(cross_names, d, &C.cross_w);
   A.add(cross_b.data(), cross_b.size() * 4, (const void**)&C.cross_b);

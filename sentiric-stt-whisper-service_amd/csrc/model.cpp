@@ -309,17 +309,13 @@ bool read_model_file(const char* path, ModelFile& mf) {
     }
     t.name.resize(name_len);
     f.read(&t.name[0], name_len);
-    size_t esz = 0;
-    switch (ttype) {
-      case GGML_F32: esz = 4; break;
-      case GGML_F16: esz = 2; break;
-      case GGML_BF16: esz = 2; break;
-      default:
-        MWX_LOG_ERROR("mwx: tensor '%s' has unsupported type %d\n",
-                      t.name.c_str(), ttype);
-        return false;
+    const size_t bytes = ggml_tensor_bytes(ttype, t.ne[0], t.nelements());
+    if (bytes == 0) {
+      MWX_LOG_ERROR("mwx: tensor '%s' has unsupported type %d (or inner dim %lld)\n",
+                    t.name.c_str(), ttype, (long long)t.ne[0]);
+      return false;
     }
-    t.data.resize((size_t)t.nelements() * esz);
+    t.data.resize(bytes);
     f.read(reinterpret_cast<char*>(t.data.data()), t.data.size());
     if (!f) {
       MWX_LOG_ERROR("mwx: truncated tensor '%s'\n", t.name.c_str());
@@ -493,9 +489,10 @@ struct Writer {
     int64_t n = 1;
     for (auto s : shape) n *= s;
     const uint64_t key = fnv1a64(name) ^ seed;
+    const bool quant = ggml_type_is_quant(ttype);
     const size_t esz = ttype == GGML_F32 ? 4 : 2;
-    const int64_t chunk = 1 << 20;
-    buf.resize((size_t)std::min<int64_t>(n, chunk) * esz);
+    const int64_t chunk = 1 << 20;  // a multiple of the 32-element quant block
+    buf.resize((size_t)std::min<int64_t>(n, chunk) * (quant ? 4 : esz));
     for (int64_t i0 = 0; i0 < n; i0 += chunk) {
       const int64_t i1 = std::min(n, i0 + chunk);
       for (int64_t i = i0; i < i1; ++i) {
@@ -508,6 +505,10 @@ struct Writer {
           v = center + scale * u;
         }
         if (adjust) v = adjust(i, v);
+        if (quant) {
+          reinterpret_cast<float*>(buf.data())[i - i0] = v;
+          continue;
+        }
         uint8_t* p = buf.data() + (size_t)(i - i0) * esz;
         if (ttype == GGML_F32) {
           memcpy(p, &v, 4);
@@ -515,6 +516,12 @@ struct Writer {
           const uint16_t h = ttype == GGML_F16 ? f32_to_f16(v) : f32_to_bf16(v);
           memcpy(p, &h, 2);
         }
+      }
+      if (quant) {
+        std::vector<uint8_t> q(ggml_tensor_bytes(ttype, shape.back(), i1 - i0));
+        ggml_quantize(ttype, reinterpret_cast<const float*>(buf.data()), q.data(), i1 - i0);
+        f.write(reinterpret_cast<const char*>(q.data()), q.size());
+        continue;
       }
       f.write(reinterpret_cast<const char*>(buf.data()), (size_t)(i1 - i0) * esz);
     }
@@ -536,8 +543,11 @@ extern "C" int mwx_write_synthetic_model(const char* path, const char* arch,
                   arch ? arch : "(null)");
     return -1;
   }
-  if (wtype != GGML_F16 && wtype != GGML_BF16) return -2;
-  hp.ftype = wtype == GGML_F16 ? 1 : 24;  // GGML_FTYPE_MOSTLY_F16 / _BF16
+  hp.ftype = ggml_ftype_of(wtype);
+  if (hp.ftype < 0) return -2;
+  // quantized files keep the 3-D conv kernels in f16 (the quantize tool only
+  // rewrites 2-D tensors)
+  const int conv_type = ggml_type_is_quant(wtype) ? GGML_F16 : wtype;
   Writer w;
   w.f.open(path, std::ios::binary | std::ios::trunc);
   if (!w.f) return -3;
@@ -587,10 +597,10 @@ extern "C" int mwx_write_synthetic_model(const char* path, const char* arch,
     w.tensor("encoder.positional_embedding", {hp.n_audio_ctx, da}, GGML_F32,
              0, 0, pe.data());
   }
-  w.tensor("encoder.conv1.weight", {da, hp.n_mels, 3}, wtype, 0.0f,
+  w.tensor("encoder.conv1.weight", {da, hp.n_mels, 3}, conv_type, 0.0f,
            std::sqrt(3.0f / (float)(hp.n_mels * 3)));
   w.tensor("encoder.conv1.bias", {da, 1}, GGML_F32, 0.0f, 0.05f);
-  w.tensor("encoder.conv2.weight", {da, da, 3}, wtype, 0.0f,
+  w.tensor("encoder.conv2.weight", {da, da, 3}, conv_type, 0.0f,
            std::sqrt(3.0f / (float)(da * 3)));
   w.tensor("encoder.conv2.bias", {da, 1}, GGML_F32, 0.0f, 0.05f);
   for (int l = 0; l < hp.n_audio_layer; ++l) {

@@ -24,6 +24,14 @@ LIB_PATH = os.path.join(HERE, "libmwx.so")
 
 GGML_F16 = 1
 GGML_BF16 = 30
+# ggml block-quantized types written by whisper.cpp's quantize tool
+GGML_Q4_0 = 2
+GGML_Q4_1 = 3
+GGML_Q5_0 = 6
+GGML_Q5_1 = 7
+GGML_Q8_0 = 8
+GGML_QUANT_TYPES = {"q4_0": GGML_Q4_0, "q4_1": GGML_Q4_1, "q5_0": GGML_Q5_0,
+                    "q5_1": GGML_Q5_1, "q8_0": GGML_Q8_0}
 SAMPLING_GREEDY = 0
 SAMPLING_BEAM_SEARCH = 1
 

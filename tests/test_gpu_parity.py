@@ -315,3 +315,22 @@ def test_beam_search_batch_equals_single(rich):
     batched = [mwx.token_ids(ctx.segments(base + i)) for i in range(3)]
     singles = [mwx.token_ids(run_fresh(ctx, pcm, p)) for pcm in pcms]
     assert batched == singles
+
+
+# ---------------------------------------------------------------- quantized files
+@pytest.mark.parametrize("qname", ["q5_0", "q8_0", "q4_1"])
+def test_quantized_model_greedy_matches_oracle(make_model, qname):
+    """whisper.cpp quantize-tool files (block formats dequantized at load, f16
+    compute): tokens, timestamps and probabilities against the oracle reading
+    the same file."""
+    path = make_model("micro-rich", mwx.GGML_QUANT_TYPES[qname])
+    o = orc.Oracle(path)
+    with mwx.Context.open(path) as ctx:
+        pcm = pcm_clip(0)
+        opt = orc.FullOptions.service_defaults()
+        opt.temperature_inc = 0.0
+        opt.language = "en"
+        segs = run_fresh(ctx, pcm, service_params(ctx, temperature_inc=0.0, language=b"en"))
+        _, osegs, _, windows = o.full(pcm, opt)
+        assert len(segs) > 3 and len(windows) > 1
+        assert_same(segs, osegs)
