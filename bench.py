@@ -124,6 +124,10 @@ def main():
     ap.add_argument("--wtype", default="bf16", choices=["bf16", "f16"])
     ap.add_argument("--clips", type=int, default=32, help="30-s clips per GPU")
     ap.add_argument("--decode-steps", type=int, default=220)
+    ap.add_argument("--beam", type=int, default=0,
+                    help="beam size (0: greedy; the service default is 5)")
+    ap.add_argument("--clip-seconds", type=float, default=30.0,
+                    help="clip length (> 30: long-form, windows decoded one after another)")
     ap.add_argument("--perf-class", default="dec_attn_cross")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -152,8 +156,11 @@ def main():
     barrier()
     ctx = mwx.Context.open(path, device=local)
     import shard
-    pcms = [mwx.pcm16_to_f32(mwx.synth_pcm16(k)) for k in shard.clip_ids(rank, args.clips)]
-    p = ctx.default_params(mwx.SAMPLING_GREEDY)
+    n_samp = int(args.clip_seconds * 16000)
+    pcms = [mwx.pcm16_to_f32(mwx.synth_pcm16(k, n_samp)) for k in shard.clip_ids(rank, args.clips)]
+    p = ctx.default_params(mwx.SAMPLING_BEAM_SEARCH if args.beam > 1 else mwx.SAMPLING_GREEDY)
+    if args.beam > 1:
+        p.beam_search.beam_size = args.beam
     p.language = b"en"
     p.temperature = 0.0
     p.temperature_inc = 0.0
@@ -161,7 +168,8 @@ def main():
     p.suppress_nst = True
     p.bench_fixed_steps = args.decode_steps
     prompt_len = 3 if ARCH[args.arch][5] >= 51865 else 1
-    max_tok = args.decode_steps
+    n_windows = max(1, int(np.ceil(args.clip_seconds / 30.0 - 1e-9)))
+    max_tok = args.decode_steps * n_windows
     gathered = {}
 
     def step():
@@ -198,17 +206,17 @@ def main():
         e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
-    audio_s = world * args.clips * 30.0 * args.steps
+    audio_s = world * args.clips * args.clip_seconds * args.steps
     value = audio_s / elapsed
     if rank == 0:
         launches = max(1, nl.value)
         avg_s = tot_ms.value / 1e3 / launches
         # decode kernels run per row group (MWX_DECODE_GROUPS chains on their
         # own streams): rows per launch from the launch count of the timed steps
-        n_dec_steps = prompt_len + args.decode_steps - 1
-        rows = args.clips
+        n_dec_steps = (prompt_len + args.decode_steps - 1) * n_windows
+        rows = args.clips * max(1, args.beam)
         if args.perf_class.startswith("dec_attn"):
-            rows = args.clips * ARCH[args.arch][4] * n_dec_steps * args.steps / launches
+            rows = rows * ARCH[args.arch][4] * n_dec_steps * args.steps / launches
         bound, work, desc = kernel_model(args.arch, args.perf_class, args.clips, rows,
                                          launches // max(1, args.steps), prompt_len,
                                          args.decode_steps)
@@ -252,9 +260,10 @@ def main():
             "dtype": args.wtype,
             "data": "synthetic (seeded 30-s 16 kHz PCM16 clips; seeded weights in the ggml .bin layout)",
             "config": {
-                "workload": (f"whisper-{args.arch} {args.wtype}: {args.clips} x 30 s clips per GPU, "
-                             f"mel + encoder + cross-KV + {args.decode_steps} greedy KV-cached "
-                             f"decode steps per clip, RCCL token gather to rank 0"),
+                "workload": (f"whisper-{args.arch} {args.wtype}: {args.clips} x {args.clip_seconds:g} s "
+                             f"clips per GPU, mel + encoder + cross-KV + {args.decode_steps} "
+                             f"{'beam-%d' % args.beam if args.beam > 1 else 'greedy'} KV-cached "
+                             f"decode steps per 30-s window, RCCL token gather to rank 0"),
                 "global_batch": world * args.clips,
                 "seq_len": 1500,
                 "parallelism": f"dp{world}",

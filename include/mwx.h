@@ -149,9 +149,11 @@ struct mwx_full_params {
   mwx_abort_callback abort_callback;
   void* abort_callback_user_data;
 
-  /* Engine extension (benchmark workload only): when > 0 every clip is decoded
-   * as exactly one 30-s window of greedy steps with EOT and timestamp tokens
-   * suppressed, so each clip costs the same fixed number of decode steps. */
+  /* Engine extension (benchmark workload only): when > 0 every 30-s window of
+   * every clip is decoded for exactly this many steps (greedy or beam) with EOT
+   * and timestamp tokens suppressed, and the clip then advances by a whole
+   * window, so each window costs the same fixed number of decode steps and a
+   * long clip runs window after window. */
   int bench_fixed_steps;
 };
 

@@ -125,13 +125,19 @@ struct State {
   DBuf xd, hd, qd, od, ffd, logits, kself, vself, stepin, ctl, tokout, probs, logprobs, smask;
   DBuf pqkv, pres, pq;  // split-K partial slabs of the decode GEMMs
   DBuf lpflt, lpparts, lpres;  // logits-processing scratch
-  DBuf kvpairs, kvstage;       // beam search KV hand-over
+  // beam search KV hand-over without copies: per row, positions below
+  // kvown[row] are read from row kvmap[row][pos] (host copies in kvmap_h/kvown_h)
+  DBuf kvmap, kvown;
+  std::vector<int> kvmap_h, kvown_h;
   int cross_cap = 0;  // cross cache slots
   int row_cap = 0;    // self cache rows
   std::vector<Segment> result_all;
   int lang_id = 0;
   std::mt19937 rng0 = std::mt19937(0);  // decoders[0].rng persists per state
-  std::vector<float> probs_h, logprobs_h;
+  // sampling / beam search: u of every draw (host RNG) in, draws out
+  DBuf du, dnd, ddraw, dneed;
+  int draw_k = 1;  // draws per row slot (KD)
+  std::vector<Draw> draws_h;
   // perf: event pairs around launches of one kernel class. Eager launches
   // use perf_ev; launches captured into a decode-step graph use perf_gev (the
   // graph re-records them on every replay; harvested after each replay).
@@ -509,6 +515,9 @@ struct Driver {
   const Hparams& hp;
   int d, H, L_enc, L_dec, V, Tctx, Lp;
   LogitsConst LC;
+  // rows per clip in the current decode run (beam_size / best_of decoders are
+  // consecutive rows of one clip); decode groups never split such a run
+  int xgroup = 1;
 
   Driver(Context& c, State& s, const mwx_full_params& p)
       : C(c), S(s), st(s.stream), P(p), hp(c.hp) {
@@ -701,21 +710,44 @@ struct Driver {
     S.lpparts.get((size_t)R * LP_G * sizeof(LPPart));
     S.lpres.get((size_t)R * LP_G * sizeof(LPRes));
     S.stepin.get((size_t)R * 4 * 4);
+    S.kvmap.get((size_t)R * Tctx * 4, true);
+    S.kvown.get((size_t)R * 4);
+    // no taken-over histories: every row reads only its own cache
+    HIPC(hipMemsetAsync(S.kvown.p, 0, (size_t)R * 4, st));
     S.ctl.get((size_t)R * sizeof(RowCtl));
     S.tokout.get((size_t)R * sizeof(TokOut));
   }
 
-  // beam search: rows take over other rows' self KV caches (triples dst, src, npos)
+  // beam search: rows take over other rows' self-attention histories
+  // (triples dst, src, npos; whisper.cpp copies the KV cells). Histories are
+  // immutable, so the hand-over only rewrites the destination's position map:
+  // kvmap[dst][0..npos) = where src reads those positions (pre-move state,
+  // so any permutation is safe), kvown[dst] = npos.
+  void reset_kv_maps(int R) {
+    HIPC(hipStreamSynchronize(st));  // no map upload may still read the host arrays
+    S.kvmap_h.assign((size_t)R * Tctx, 0);
+    S.kvown_h.assign(R, 0);
+    HIPC(hipMemsetAsync(S.kvown.p, 0, (size_t)R * 4, st));
+  }
   void copy_kv_rows(const std::vector<int>& triples) {
     const int n = (int)triples.size() / 3;
     if (n == 0) return;
-    int npos = 1;
-    for (int i = 0; i < n; ++i) npos = std::max(npos, triples[3 * i + 2]);
-    int* dp = (int*)S.kvpairs.get(triples.size() * 4);
-    _Float16* stage = (_Float16*)S.kvstage.get((size_t)n * 2 * L_dec * H * npos * 64 * 2);
-    HIPC(hipMemcpyAsync(dp, triples.data(), triples.size() * 4, hipMemcpyHostToDevice, st));
-    kv_rows_copy((_Float16*)S.kself.p, (_Float16*)S.vself.p, (long)S.row_cap * H * Tctx * 64,
-                 L_dec, H, Tctx, dp, n, stage, npos, st);
+    const std::vector<int> map0 = S.kvmap_h, own0 = S.kvown_h;
+    int lo = 1 << 30, hi = -1;
+    for (int i = 0; i < n; ++i) {
+      const int dst = triples[3 * i], src = triples[3 * i + 1], npos = triples[3 * i + 2];
+      for (int j = 0; j < npos; ++j)
+        S.kvmap_h[(size_t)dst * Tctx + j] = j < own0[src] ? map0[(size_t)src * Tctx + j] : src;
+      S.kvown_h[dst] = npos;
+      lo = std::min(lo, dst);
+      hi = std::max(hi, dst);
+    }
+    HIPC(hipMemcpyAsync((int*)S.kvmap.p + (size_t)lo * Tctx, S.kvmap_h.data() + (size_t)lo * Tctx,
+                        (size_t)(hi - lo + 1) * Tctx * 4, hipMemcpyHostToDevice, st));
+    HIPC(hipMemcpyAsync((int*)S.kvown.p + lo, S.kvown_h.data() + lo, (size_t)(hi - lo + 1) * 4,
+                        hipMemcpyHostToDevice, st));
+    // (ordered before the next step on this stream; the host arrays are next
+    // written after that step's synchronize, or in reset_kv_maps)
   }
 
   // one decoder step for all R rows on the state's stream; inputs already in
@@ -741,8 +773,10 @@ struct Driver {
     if (R < 16 * G) G = std::max(1, R / 16);
     std::vector<Group> gs;
     size_t prow = 0;
+    const int xg = std::max(1, xgroup);
     for (int g = 0; g < G; ++g) {
-      const int r0 = (int)((long)R * g / G), r1 = (int)((long)R * (g + 1) / G);
+      const int r0 = (int)((long)R * g / G) / xg * xg;
+      const int r1 = g == G - 1 ? R : (int)((long)R * (g + 1) / G) / xg * xg;
       gs.push_back(Group{r0, r1 - r0, prow});
       prow += (size_t)(r1 - r0 + 63) / 64 * 64;
     }
@@ -784,7 +818,8 @@ struct Driver {
         k1 = gemm_splitk_partials<T>(hd, Wt(W.qkv_w), n, 3 * d, d, Pqkv, s); }
       { PerfScope ps(S, "dec_attn_self", s);
         dec_attention<T>(Pqkv, k1, 3 * d, W.qkv_b, kqs, kqs, ks, vs, nullptr, pos, act, 0, Tctx,
-                         od, n, H, 1.0f, s); }
+                         od, n, H, 1.0f, s, (const int*)S.kvmap.p + (size_t)r0 * Tctx,
+                         (const int*)S.kvown.p + r0, r0, xgroup); }
       int k2;
       { PerfScope ps(S, "dec_gemm", s);
         k2 = gemm_splitk_partials<T>(od, Wt(W.o_w), n, d, d, Pres, s); }
@@ -793,10 +828,19 @@ struct Driver {
       { PerfScope ps(S, "dec_gemm", s);
         k3 = gemm_splitk_partials<T>(hd, Wt(W.cq_w), n, d, d, Pq, s); }
       { PerfScope ps(S, "dec_attn_cross", s);
-        dec_attention<T>(Pq, k3, d, W.cq_b, 1.0f, 1.0f,
-                         (_Float16*)S.cross_k.p + l * layer_cross,
-                         (_Float16*)S.cross_v.p + l * layer_cross, xidx, pos, act,
-                         hp.n_audio_ctx, hp.n_audio_ctx, od, n, H, kqs, s); }
+        // the decoders of a beam / best-of group share their clip's cross K/V:
+        // stream it once per group
+        if (xgroup < 2 ||
+            !dec_cross_attention_grouped<T>(Pq, k3, d, W.cq_b,
+                                            (const _Float16*)S.cross_k.p + l * layer_cross,
+                                            (const _Float16*)S.cross_v.p + l * layer_cross, xidx,
+                                            act, hp.n_audio_ctx, hp.n_audio_ctx, od, n, H, kqs,
+                                            xgroup, s))
+          dec_attention<T>(Pq, k3, d, W.cq_b, 1.0f, 1.0f,
+                           (_Float16*)S.cross_k.p + l * layer_cross,
+                           (_Float16*)S.cross_v.p + l * layer_cross, xidx, pos, act,
+                           hp.n_audio_ctx, hp.n_audio_ctx, od, n, H, kqs, s, nullptr, nullptr, 0,
+                           xgroup); }
       int k4;
       { PerfScope ps(S, "dec_gemm", s);
         k4 = gemm_splitk_partials<T>(od, Wt(W.co_w), n, d, d, Pres, s); }
@@ -833,6 +877,11 @@ struct Driver {
                    LPScratch{(float*)S.lpflt.p + (size_t)r0 * V, (LPPart*)S.lpparts.p + r0 * LP_G,
                              (LPRes*)S.lpres.p + r0 * LP_G},
                    s);
+    if (want_probs) {  // std::discrete_distribution draws of the sampling rows
+      const int KD = S.draw_k;
+      sample_draws(pr, lp, V, (const double*)S.du.p + (size_t)r0 * KD, (const int*)S.dnd.p + r0,
+                   KD, (Draw*)S.ddraw.p + (size_t)r0 * KD, (int*)S.dneed.p + r0, n, s);
+    }
   }
 };
 

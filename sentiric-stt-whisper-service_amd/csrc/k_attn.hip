@@ -247,13 +247,28 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
     const float* __restrict__ P, int KS, int pcols, const float* __restrict__ bias, float qscale,
     float kscale, _Float16* __restrict__ kbase, _Float16* __restrict__ vbase,
     const int* __restrict__ kv_index, const int* __restrict__ pos, const int* __restrict__ active,
-    int fixed_len, int cap, T* __restrict__ o, int H, float scale) {
+    int fixed_len, int cap, T* __restrict__ o, int H, float scale,
+    const int* __restrict__ kvmap, const int* __restrict__ own_from, int map_row0, int nq,
+    int R) {
   __shared__ float sc[DEC_MAX_KEYS];
   __shared__ float redf[4];
   __shared__ double redd[4];
   __shared__ float pv[4][64][9];
   __shared__ float sq[64], snk[64], snv[64];
-  const int row = blockIdx.y, h = blockIdx.x;
+  int row = blockIdx.y, h = blockIdx.x;
+  if (nq > 1) {
+    // nq rows per clip (beam / best-of decoders: cross, the same K/V; self,
+    // histories taken over from each other): 1-D grid where the nq
+    // workgroups of one (clip, head) are dispatched within a window of 8*nq
+    // ids with equal id % 8 -- one XCD under the round-robin placement, so
+    // the rows they share are read from HBM about once and served to the
+    // others from that XCD's L2
+    const int L = blockIdx.x, W = 8 * nq;
+    const int q = (L % W) / 8, g = (L / W) * 8 + L % 8;
+    if (g >= (R / nq) * H) return;
+    row = (g / H) * nq + q;
+    h = g % H;
+  }
   if (!active[row]) return;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int kg = lane >> 3, c = lane & 7;
@@ -264,6 +279,13 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
   const int D = H * 64;
   _Float16* K = kbase + (((long)slot * H + h) * cap) * 64;
   _Float16* V = vbase + (((long)slot * H + h) * cap) * 64;
+  // self (beam search): positions below own_from[row] were taken over from
+  // other rows' histories; kvmap[row][j] names the row (numbered from
+  // -map_row0 relative to kbase) whose cache holds position j (histories are
+  // never overwritten, so no KV is copied)
+  const int own0 = SELF && own_from ? own_from[row] : 0;
+  const int* mrow = SELF && kvmap ? kvmap + (long)row * cap : nullptr;
+  const long rstride = (long)H * cap * 64;
   constexpr int UB = 8;
   const int nb = (n + 255) >> 8;
   // rows past the end are clamped to the last OLD row (self: the new row is
@@ -274,12 +296,15 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
 #define LOADROWS(buf, base, bidx)                                                  \
   _Pragma("unroll") for (int u = 0; u < UB; ++u) {                               \
     const int j = min((bidx) * 256 + wid * 64 + u * 8 + kg, jmax);                \
-    buf[u] = *reinterpret_cast<const f16x8*>(base + (long)j * 64 + c * 8);        \
+    const _Float16* src = base + (long)j * 64 + c * 8;                            \
+    if (SELF && j < own0)                                                         \
+      src += ((long)mrow[j] - map_row0 - slot) * rstride;                         \
+    buf[u] = *reinterpret_cast<const f16x8*>(src);                                \
   }
   // reduce the projections of this head from the split-K slabs (KS <= 8):
   // the slab loads are issued first, then the first key batch, so the
   // reduction waits only for its own loads
-  const long pstride = (long)gridDim.y * pcols;
+  const long pstride = (long)R * pcols;
   const bool red = tid < (SELF ? 192 : 64);
   const int part = tid >> 6, e = tid & 63;
   const int col = part * D + h * 64 + e;
@@ -404,58 +429,235 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
   }
 }
 
+// Cross-attention of NQ rows that share one clip's cross K/V (the decoders
+// of a beam search / best-of group: rows g*NQ .. g*NQ+NQ-1): one workgroup per
+// (group, head) streams the clip's K and V once for all NQ queries instead of
+// once per row. Every row's arithmetic (scores, softmax, P.V reduction order)
+// is exactly that of dec_attn_kernel<T, false>, so results do not depend on
+// the grouping.
+template <typename T, int NQ>
+__global__ __launch_bounds__(256, 2) void dec_xattn_kernel(
+    const float* __restrict__ P, int KS, int pcols, const float* __restrict__ bias,
+    const _Float16* __restrict__ kbase, const _Float16* __restrict__ vbase,
+    const int* __restrict__ kv_index, const int* __restrict__ active, int n, int cap, int R,
+    T* __restrict__ o, int H, float scale) {
+  __shared__ float sc[NQ][DEC_MAX_KEYS];
+  __shared__ float redf[4][NQ];
+  __shared__ double redd[4][NQ];
+  __shared__ float pv[4][64][9];
+  __shared__ float sq[NQ][64];
+  const int g = blockIdx.y, h = blockIdx.x, row0 = g * NQ;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int kg = lane >> 3, c = lane & 7;
+  bool act[NQ];
+  bool any = false;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    act[q] = row0 + q < R && active[row0 + q];
+    any |= act[q];
+  }
+  if (!any) return;
+  const int slot = kv_index ? kv_index[row0] : row0;
+  const int D = H * 64;
+  const _Float16* K = kbase + (((long)slot * H + h) * cap) * 64;
+  const _Float16* V = vbase + (((long)slot * H + h) * cap) * 64;
+  // the key/value rows of a batch are those of dec_attn_kernel (row
+  // bidx*256 + wid*64 + u*8 + kg, u < 8) but are streamed in halves of 4 rows
+  // per lane group (u = 4*half + uu), so fewer registers hold loads in flight
+  constexpr int UH = 4;
+  const int nb = (n + 255) >> 8;
+  const int jmax = n - 1;
+  f16x8 ka[UH], kb2[UH];
+#define LOADROWS(buf, base, bidx, half)                                        \
+  _Pragma("unroll") for (int uu = 0; uu < UH; ++uu) {                         \
+    const int j = min((bidx) * 256 + wid * 64 + ((half) * UH + uu) * 8 + kg, jmax); \
+    buf[uu] = *reinterpret_cast<const f16x8*>(base + (long)j * 64 + c * 8);   \
+  }
+  // queries: q = f16(sum of the split-K slabs + bias), head h's 64 columns
+  const long pstride = (long)R * pcols;
+  for (int t = tid; t < NQ * 64; t += 256) {
+    const int q = t >> 6, e = t & 63;
+    const int col = h * 64 + e;
+    const int r = min(row0 + q, R - 1);
+    const float* pp = P + (long)r * pcols + col;
+    float acc = pp[0];
+    for (int k = 1; k < KS; ++k) acc += pp[k * pstride];
+    sq[q][e] = (float)(_Float16)(acc + bias[col]);
+  }
+  LOADROWS(ka, K, 0, 0)
+  __syncthreads();
+  float qv[NQ][8];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) qv[q][e] = sq[q][c * 8 + e];
+  auto score_batch = [&](const f16x8* kk, int bidx, int half) {
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int uu = 0; uu < UH; ++uu) {
+      const int u = half * UH + uu;
+      const int j = bidx * 256 + wid * 64 + u * 8 + kg;
+      float kf[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) kf[e] = (float)kk[uu][e];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        float d = 0.0f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d += qv[q][e] * kf[e];
+        d = dpp_sum8(d);
+        if (c == 0 && j < n) sc[q][j] = d * scale;
+      }
+      __builtin_amdgcn_sched_barrier(0);  // one key row's conversions live at a time
+    }
+  };
+  for (int b = 0; b < nb; ++b) {
+    LOADROWS(kb2, K, b, 1)
+    score_batch(ka, b, 0);
+    LOADROWS(ka, K, b + 1, 0)
+    score_batch(kb2, b, 1);
+  }
+  LOADROWS(ka, V, 0, 0)
+  __syncthreads();
+  // softmax per query (block_max_256 / block_sum_256d order)
+  float mx[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    float m = -INFINITY;
+    for (int j = tid; j < n; j += 256) m = fmaxf(m, sc[q][j]);
+    mx[q] = wave_max(m);
+  }
+  if (lane == 0)
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) redf[wid][q] = mx[q];
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+    mx[q] = fmaxf(fmaxf(redf[0][q], redf[1][q]), fmaxf(redf[2][q], redf[3][q]));
+  double sum[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    double sm = 0.0;
+    for (int j = tid; j < n; j += 256) {
+      const float e = expf(sc[q][j] - mx[q]);
+      sc[q][j] = e;
+      sm += (double)e;
+    }
+    sum[q] = wave_sum_d(sm);
+  }
+  if (lane == 0)
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) redd[wid][q] = sum[q];
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const double t = (redd[0][q] + redd[1][q]) + (redd[2][q] + redd[3][q]);
+    const float inv = (float)(1.0 / t);
+    for (int j = tid; j < n; j += 256) sc[q][j] = (float)(_Float16)(sc[q][j] * inv);
+  }
+  __syncthreads();
+  float acc[NQ][8];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[q][e] = 0.0f;
+  auto pv_batch = [&](const f16x8* vv, int bidx, int half) {
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int uu = 0; uu < UH; ++uu) {
+      const int j = bidx * 256 + wid * 64 + (half * UH + uu) * 8 + kg;
+      float vf[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) vf[e] = (float)vv[uu][e];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const float p = j < n ? sc[q][min(j, n - 1)] : 0.0f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[q][e] += p * vf[e];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  for (int b = 0; b < nb; ++b) {
+    LOADROWS(kb2, V, b, 1)
+    pv_batch(ka, b, 0);
+    LOADROWS(ka, V, b + 1, 0)
+    pv_batch(kb2, b, 1);
+  }
+#undef LOADROWS
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float a = acc[q][e];
+      a += __shfl_xor(a, 8, 64);
+      a += __shfl_xor(a, 16, 64);
+      a += __shfl_xor(a, 32, 64);
+      acc[q][e] = a;
+    }
+    if (kg == 0) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) pv[wid][c][e] = acc[q][e];
+    }
+    __syncthreads();
+    if (tid < 64 && act[q]) {
+      const int cc = tid >> 3, e = tid & 7;
+      const float r = (pv[0][cc][e] + pv[1][cc][e]) + (pv[2][cc][e] + pv[3][cc][e]);
+      o[pack_index(row0 + q, h * 64 + cc * 8 + e, D)] = to_t<T>(r);
+    }
+    __syncthreads();
+  }
+}
+
+template <typename T>
+bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float* bias,
+                                 const _Float16* kbase, const _Float16* vbase,
+                                 const int* kv_index, const int* active, int n_keys, int cap,
+                                 T* o, int R, int H, float scale, int nq, hipStream_t st) {
+  if (n_keys > DEC_MAX_KEYS || KS > 8) return false;
+  const dim3 g(H, (R + nq - 1) / nq);
+  switch (nq) {
+#define XQ(N)                                                                                 \
+  case N:                                                                                     \
+    dec_xattn_kernel<T, N><<<g, 256, 0, st>>>(P, KS, pcols, bias, kbase, vbase, kv_index,   \
+                                              active, n_keys, cap, R, o, H, scale);           \
+    return true;
+    XQ(2) XQ(3) XQ(4) XQ(5) XQ(6) XQ(8)
+#undef XQ
+    default: return false;
+  }
+}
+template bool dec_cross_attention_grouped<_Float16>(const float*, int, int, const float*,
+                                                    const _Float16*, const _Float16*, const int*,
+                                                    const int*, int, int, _Float16*, int, int,
+                                                    float, int, hipStream_t);
+template bool dec_cross_attention_grouped<__bf16>(const float*, int, int, const float*,
+                                                  const _Float16*, const _Float16*, const int*,
+                                                  const int*, int, int, __bf16*, int, int, float,
+                                                  int, hipStream_t);
+
 template <typename T>
 void dec_attention(const float* P, int KS, int pcols, const float* bias, float qscale,
                    float kscale, _Float16* kbase, _Float16* vbase, const int* kv_index,
                    const int* pos, const int* active, int fixed_len, int kv_len_cap, T* o, int R,
-                   int H, float scale, hipStream_t st) {
+                   int H, float scale, hipStream_t st, const int* kvmap, const int* own_from,
+                   int map_row0, int nq) {
   dim3 g(H, R);
-if (fixed_len == 0)
+  if (nq > 1 && R % nq == 0) {
+    const int groups = (R / nq) * H;
+    g = dim3((groups + 7) / 8 * 8 * nq, 1);
+  } else {
+    nq = 1;
+  }
+  if (fixed_len == 0)
     dec_attn_kernel<T, true><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale, kbase, vbase,
                                                 kv_index, pos, active, fixed_len, kv_len_cap, o,
-                                                H, scale);
+                                                H, scale, kvmap, own_from, map_row0, nq, R);
   else
     dec_attn_kernel<T, false><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale, kbase,
                                                  vbase, kv_index, pos, active, fixed_len,
-                                                 kv_len_cap, o, H, scale);
-}
-
-// ---------------------------------------------------------------------------
-// beam search: decoder rows take over another row's self-attention KV cache
-// (whisper_kv_cache_seq_cp via a temporary sequence). Phase 0 copies every
-// source row's first npos positions into staging, phase 1 staging into the
-// destination rows, so any permutation of rows is safe.
-// pairs: [n][3] = (dst row, src row, npos); cache layout [L][row][H][Tctx][64].
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void kv_rows_copy_kernel(_Float16* __restrict__ kc,
-                                                           _Float16* __restrict__ vc,
-                                                           long layer_stride, int H, int Tctx,
-                                                           const int* __restrict__ pairs,
-                                                           _Float16* __restrict__ stage,
-                                                           int stage_pos, int L, int phase) {
-  const int l = blockIdx.x / H, h = blockIdx.x % H, p = blockIdx.y;
-  const int dst = pairs[3 * p], src = pairs[3 * p + 1], npos = pairs[3 * p + 2];
-  const int nvec = npos * 8;  // 16-B vectors
-#pragma unroll
-  for (int kv = 0; kv < 2; ++kv) {
-    _Float16* cache = (kv ? vc : kc) + l * layer_stride;
-    _Float16* sg = stage + ((((long)p * 2 + kv) * L + l) * H + h) * (long)stage_pos * 64;
-    const _Float16* from = phase == 0 ? cache + ((long)src * H + h) * Tctx * 64 : sg;
-    _Float16* to = phase == 0 ? sg : cache + ((long)dst * H + h) * Tctx * 64;
-    for (int i = threadIdx.x; i < nvec; i += 256)
-      reinterpret_cast<f16x8*>(to)[i] = reinterpret_cast<const f16x8*>(from)[i];
-  }
-}
-
-void kv_rows_copy(_Float16* kc, _Float16* vc, long layer_stride, int L, int H, int Tctx,
-                  const int* d_pairs, int n_pairs, _Float16* stage, int stage_pos,
-                  hipStream_t st) {
-  if (n_pairs <= 0) return;
-  const dim3 g(L * H, n_pairs);
-  kv_rows_copy_kernel<<<g, 256, 0, st>>>(kc, vc, layer_stride, H, Tctx, d_pairs, stage,
-                                         stage_pos, L, 0);
-  kv_rows_copy_kernel<<<g, 256, 0, st>>>(kc, vc, layer_stride, H, Tctx, d_pairs, stage,
-                                         stage_pos, L, 1);
+                                                 kv_len_cap, o, H, scale, nullptr, nullptr, 0, nq,
+                                                 R);
 }
 
 template void enc_attention<_Float16>(const _Float16*, const _Float16*, const _Float16*, _Float16*,
@@ -464,9 +666,10 @@ template void enc_attention<__bf16>(const _Float16*, const _Float16*, const _Flo
                                     int, int, float, hipStream_t);
 template void dec_attention<_Float16>(const float*, int, int, const float*, float, float,
                                       _Float16*, _Float16*, const int*, const int*, const int*, int,
-                                      int, _Float16*, int, int, float, hipStream_t);
+                                      int, _Float16*, int, int, float, hipStream_t, const int*,
+                                      const int*, int, int);
 template void dec_attention<__bf16>(const float*, int, int, const float*, float, float, _Float16*,
                                     _Float16*, const int*, const int*, const int*, int, int,
-                                    __bf16*, int, int, float, hipStream_t);
+                                    __bf16*, int, int, float, hipStream_t, const int*, const int*, int, int);
 
 }  // namespace mwx

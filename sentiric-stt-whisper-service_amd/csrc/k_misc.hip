@@ -8,6 +8,8 @@
 // does every pass with wave-shuffle + LDS reductions.
 #include <type_traits>
 
+#include <cstdlib>
+
 #include "kcommon.h"
 #include "kernels.h"
 
@@ -517,6 +519,227 @@ void logits_process(float* logits, const float* static_mask, const RowCtl* ctl, 
   lp_filter_kernel<<<g, LP_T, 0, st>>>(logits, static_mask, ctl, ws.flt, ws.parts, C);
   lp_probs_kernel<<<g, LP_T, 0, st>>>(ws.flt, ws.parts, ctl, ws.res, probs, logprobs, C);
   lp_pick_kernel<<<R, 64, 0, st>>>(logits, ws.flt, ws.parts, ws.res, ctl, out, C);
+}
+
+
+// ---------------------------------------------------------------------------
+// std::discrete_distribution draws on the device (whisper_sample_token with
+// temperature > 0 and whisper_sample_token_topk: `std::discrete_distribution<>
+// dist(probs.begin(), probs.end()); id = dist(rng)`), bit-exact to libstdc++:
+//   param:  sum = accumulate(double(p_i)) (sequential), q_i = p_i / sum,
+//           cp = partial_sum(q) (sequential), cp[V-1] = 1.0;
+//   draw:   u = generate_canonical<double, 53>(rng), id = lower_bound(cp, u).
+// The u of every draw are produced on the host from the row's std::mt19937
+// (the RNG stream stays on the host, consumed in the same order). The two
+// running sums are inherently sequential (their rounding is the result), so
+// one lane performs the adds while the wave stages each chunk through LDS
+// (converted / divided in parallel) and searches the chunk's cumulative
+// values in parallel for the threshold crossings.
+// ---------------------------------------------------------------------------
+constexpr int DR_CH = 1024;  // elements per staged chunk
+
+// s = (((s + q[0]) + q[1]) + ...) in index order (one lane); the LDS reads are
+// issued 16 elements ahead of the dependent adds. cp (optional) receives
+// every running value.
+__device__ __forceinline__ double seq_sum(const double* q, int n, double s, double* cp) {
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  const d2* q2 = reinterpret_cast<const d2*>(q);
+  d2* c2 = reinterpret_cast<d2*>(cp);
+  int j = 0;
+  for (; j + 16 <= n; j += 16) {
+    d2 a[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) a[t] = q2[(j >> 1) + t];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const double s0 = s + a[t].x;
+      s = s0 + a[t].y;
+      if (cp) c2[(j >> 1) + t] = d2{s0, s};
+    }
+  }
+  for (; j < n; ++j) {
+    s += q[j];
+    if (cp) cp[j] = s;
+  }
+  return s;
+}
+
+__global__ __launch_bounds__(64) void sample_draws_exact_kernel(const float* __restrict__ probs,
+                                                                const float* __restrict__ logprobs,
+                                                                int V, const double* __restrict__ u,
+                                                                const int* __restrict__ ndraw, int KD,
+                                                                Draw* __restrict__ out,
+                                                                const int* __restrict__ need) {
+  __shared__ double q[DR_CH];
+  __shared__ double cp[DR_CH];
+  const int row = blockIdx.x, lane = threadIdx.x;
+  const int nd = ndraw[row];
+  if (nd <= 0 || (need && !need[row])) return;
+  const float* P = probs + (long)row * V;
+  constexpr int PL = DR_CH / 64;  // elements per lane per chunk
+  // pass 1: sum in index order
+  double sum = 0.0;
+  float nx[PL];
+  auto load = [&](int c0) {
+#pragma unroll
+    for (int t = 0; t < PL; ++t) {
+      const int i = c0 + t * 64 + lane;
+      nx[t] = i < V ? P[i] : 0.0f;
+    }
+  };
+  load(0);
+  for (int c0 = 0; c0 < V; c0 += DR_CH) {
+#pragma unroll
+    for (int t = 0; t < PL; ++t) q[t * 64 + lane] = (double)nx[t];
+    __syncthreads();
+    if (c0 + DR_CH < V) load(c0 + DR_CH);  // in flight during the sequential adds
+    if (lane == 0) sum = seq_sum(q, min(DR_CH, V - c0), sum, nullptr);
+    __syncthreads();
+  }
+  sum = __shfl(sum, 0, 64);
+  // pass 2: cumulative of p_i / sum; each draw takes the first index whose
+  // cumulative value is >= u (cp[V-1] is 1.0, so a draw not taken earlier
+  // takes V-1)
+  double ud[16];
+  int id[16];
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    ud[d] = d < nd ? u[(long)row * KD + d] : 2.0;
+    id[d] = d < nd ? -1 : 0;
+  }
+  double run = 0.0;
+  load(0);
+  for (int c0 = 0; c0 < V; c0 += DR_CH) {
+#pragma unroll
+    for (int t = 0; t < PL; ++t) q[t * 64 + lane] = (double)nx[t] / sum;
+    __syncthreads();
+    if (c0 + DR_CH < V) load(c0 + DR_CH);
+    const int n = min(DR_CH, V - c0);
+    if (lane == 0) {
+      run = seq_sum(q, n, run, cp);
+      if (c0 + n == V) cp[n - 1] = 1.0;
+    }
+    __syncthreads();
+    // lane owns the contiguous slots [lane*PL, lane*PL + PL)
+#pragma unroll
+    for (int d = 0; d < 16; ++d) {
+      if (d >= nd) break;
+      if (__shfl(id[d], 0, 64) >= 0) continue;  // taken in an earlier chunk
+      int first = 0x7fffffff;
+      for (int t = 0; t < PL; ++t) {
+        const int j = lane * PL + t;
+        if (j < n && cp[j] >= ud[d]) {
+          first = j;
+          break;
+        }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) first = min(first, __shfl_xor(first, o, 64));
+      if (first != 0x7fffffff) id[d] = c0 + first;
+    }
+    run = __shfl(run, 0, 64);
+    __syncthreads();
+  }
+  if (lane < nd) {
+    int my = 0;
+#pragma unroll
+    for (int d = 0; d < 16; ++d)
+      if (d == lane) my = id[d];
+    Draw r;
+    r.id = my;
+    r.p = P[my];
+    r.plog = logprobs[(long)row * V + my];
+    r.pad = 0;
+    out[(long)row * KD + lane] = r;
+  }
+}
+
+// Fast path: the same draws from a parallel evaluation. S = sum p_i (any
+// order), q_i = p_i / S, cumulative values by per-thread chunks + a block scan.
+// Sequential rounding (the exact kernel) and this evaluation differ by at most
+// ~2.4e-11 in any cumulative value (n * 2^-53 for each running sum, plus the
+// relative difference of the two S through q), so when u lies more than
+// DR_MARGIN from the cumulative values on both sides of the crossing the
+// exact kernel would pick the same index. Rows with a draw inside the margin
+// are flagged and redone by sample_draws_exact_kernel.
+constexpr double DR_MARGIN = 2e-10;
+constexpr int DR_T = 256;
+
+__global__ __launch_bounds__(DR_T) void sample_draws_kernel(const float* __restrict__ probs,
+                                                            const float* __restrict__ logprobs,
+                                                            int V, const double* __restrict__ u,
+                                                            const int* __restrict__ ndraw, int KD,
+                                                            Draw* __restrict__ out,
+                                                            int* __restrict__ need) {
+  __shared__ double red[DR_T / 64];
+  __shared__ double scan[DR_T];
+  __shared__ int ids[16];
+  __shared__ int bad;
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nd = ndraw[row];
+  if (nd <= 0) return;
+  const float* P = probs + (long)row * V;
+  if (tid < 16) ids[tid] = -1;
+  if (tid == 0) bad = 0;
+  double s = 0.0;
+  for (int i = tid; i < V; i += DR_T) s += (double)P[i];
+  s = wave_sum_d(s);
+  if (lane == 0) red[wid] = s;
+  __syncthreads();
+  const double S = (red[0] + red[1]) + (red[2] + red[3]);
+  const int CH = (V + DR_T - 1) / DR_T;
+  const int a = min(V, tid * CH), b = min(V, a + CH);
+  double loc = 0.0;
+  for (int i = a; i < b; ++i) loc += (double)P[i] / S;
+  // inclusive scan of the chunk totals (Hillis-Steele over DR_T threads)
+  scan[tid] = loc;
+  __syncthreads();
+  for (int o = 1; o < DR_T; o <<= 1) {
+    const double v = tid >= o ? scan[tid - o] : 0.0;
+    __syncthreads();
+    scan[tid] += v;
+    __syncthreads();
+  }
+  const double base = scan[tid] - loc;  // cumulative value before element a
+  // the thread whose chunk holds the crossing of u finds its index
+  for (int d = 0; d < nd; ++d) {
+    const double ud = u[(long)row * KD + d];
+    if (a >= b || !(ud > base - DR_MARGIN)) continue;       // crossing before this chunk
+    if (b < V && scan[tid] + DR_MARGIN < ud) continue;     // ... or after it
+    double prev = base, c = base;
+    for (int i = a; i < b; ++i) {
+      c = i == V - 1 ? 1.0 : c + (double)P[i] / S;  // cp[V-1] = 1.0
+      if (c >= ud) {
+        if (i == a && !(ud > base)) break;  // crossing in an earlier chunk
+        ids[d] = i;
+        if (!(ud - prev > DR_MARGIN && c - ud > DR_MARGIN)) bad = 1;
+        break;
+      }
+      prev = c;
+    }
+  }
+  __syncthreads();
+  if (tid < nd) {
+    const int id = ids[tid];
+    Draw r;
+    r.id = id < 0 ? V - 1 : id;
+    r.p = P[r.id];
+    r.plog = logprobs[(long)row * V + r.id];
+    r.pad = 0;
+    out[(long)row * KD + tid] = r;
+    if (id < 0) bad = 1;  // (cannot happen: cp[V-1] = 1 > u) -> exact path
+  }
+  __syncthreads();
+  if (tid == 0) need[row] = bad;
+}
+
+void sample_draws(const float* probs, const float* logprobs, int V, const double* u,
+                  const int* ndraw, int KD, Draw* out, int* need, int R, hipStream_t st) {
+  static const bool exact_only = getenv("MWX_DRAW_EXACT") != nullptr;
+  if (!exact_only)
+    sample_draws_kernel<<<R, DR_T, 0, st>>>(probs, logprobs, V, u, ndraw, KD, out, need);
+  sample_draws_exact_kernel<<<R, 64, 0, st>>>(probs, logprobs, V, u, ndraw, KD, out,
+                                              exact_only ? nullptr : need);
 }
 
 }  // namespace mwx

@@ -118,18 +118,26 @@ void enc_attention(const _Float16* q, const _Float16* k, const _Float16* vt, T* 
 // self (fixed_len == 0): the slabs hold Q|K|V (pcols = 3d); the kernel also
 // forms k = f16(sum * kscale), v = f16(sum + bias) for the row's position and
 // appends them to the KV cache before attending over positions 0..pos.
+// self (beam search): with own_from != nullptr, position j < own_from[row] of
+// row `row` is read from the cache of row kvmap[row * kv_len_cap + j] - map_row0.
+// cross: nq > 1 = rows come in groups of nq sharing one slot (beam / best-of
+// decoders of a clip); their workgroups are co-scheduled on one XCD.
 template <typename T>
 void dec_attention(const float* P, int KS, int pcols, const float* bias, float qscale,
                    float kscale, _Float16* kbase, _Float16* vbase, const int* kv_index,
                    const int* pos, const int* active, int fixed_len, int kv_len_cap, T* o, int R,
-                   int H, float scale, hipStream_t st);
+                   int H, float scale, hipStream_t st, const int* kvmap = nullptr,
+                   const int* own_from = nullptr, int map_row0 = 0, int nq = 1);
 
-// Beam search KV hand-over: for each (dst, src, npos) triple in d_pairs, the
-// first npos positions of row src's self KV cache (all layers, heads) are
-// copied to row dst, through `stage` ([n_pairs][2][L][H][stage_pos][64]).
-void kv_rows_copy(_Float16* kc, _Float16* vc, long layer_stride, int L, int H, int Tctx,
-                  const int* d_pairs, int n_pairs, _Float16* stage, int stage_pos,
-                  hipStream_t st);
+// Cross-attention for groups of nq consecutive rows that share one cross
+// slot (beam-search / best-of decoders of a clip; kv_index[row] equal within a
+// group): K/V of the slot are streamed once per group. Same per-row results as
+// dec_attention. Returns false if nq is not supported (2, 3, 4, 5, 6, 8).
+template <typename T>
+bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float* bias,
+                                 const _Float16* kbase, const _Float16* vbase,
+                                 const int* kv_index, const int* active, int n_keys, int cap,
+                                 T* o, int R, int H, float scale, int nq, hipStream_t st);
 
 struct RowCtl {
   int active;        // row participates in this step
@@ -185,5 +193,20 @@ struct LPScratch {
 void logits_process(float* logits, const float* static_mask, const RowCtl* ctl, TokOut* out,
                     float* probs, float* logprobs, const LogitsConst& C, int R, LPScratch ws,
                     hipStream_t st);
+
+// std::discrete_distribution draws from the probs rows (k_misc.hip):
+// out[row][d] for d < ndraw[row] (<= KD <= 16), u[row][d] =
+// generate_canonical<double, 53> of the row's RNG.
+struct Draw {
+  int id;
+  float p;
+  float plog;
+  int pad;
+};
+// need: [R] scratch (rows whose fast-path draw lies within the rounding
+// margin and is redone by the sequential libstdc++-order kernel).
+// MWX_DRAW_EXACT=1 runs the sequential kernel for every row.
+void sample_draws(const float* probs, const float* logprobs, int V, const double* u,
+                  const int* ndraw, int KD, Draw* out, int* need, int R, hipStream_t st);
 
 }  // namespace mwx

@@ -189,6 +189,24 @@ def test_bench_fixed_steps_workload(micro):
     assert sum(len(s.tokens) for s in ctx.segments()) == 40
 
 
+def test_bench_fixed_steps_long_form(micro):
+    """Benchmark workload on a long clip: every 30-s window decodes the fixed
+    step count, then the clip advances by a whole window (oracle: same rule)."""
+    ctx, o, _ = micro
+    pcm = pcm_clip(4, 75.0)
+    p = service_params(ctx, temperature_inc=0.0, language=b"en")
+    p.bench_fixed_steps = 20
+    assert ctx.full(pcm, p) == 0
+    got = mwx.token_ids(ctx.segments())
+    assert len(got) == 3 * 20
+    opt = orc.FullOptions.service_defaults()
+    opt.temperature_inc = 0.0
+    opt.language = "en"
+    opt.bench_fixed_steps = 20
+    _, osegs, _, _ = o.full(pcm, opt)
+    assert got == [t.id for sg in osegs for t in sg.tokens]
+
+
 def test_fallback_batch_over_64_rows_equals_single(micro):
     """Temperature fallback on 14 clips at once runs 14 x best_of(5) = 70
     decoder rows (row blocks > 64 in every split-K GEMM); each clip must decode
@@ -294,6 +312,20 @@ def test_beam_search_replay_exact(rich, temperature_inc):
     assert_same(segs, osegs, p_tol=1e-4)
 
 
+def test_beam_search_replay_exact_split_k(make_model):
+    """As above on tiny.en shapes (d 384: the decoder projections run split-K
+    with 3 slabs, so the grouped cross-attention / remapped self-attention
+    reduce multi-slab queries)."""
+    path = make_model("tiny.en-rich")
+    o = orc.Oracle(path)
+    with mwx.Context.open(path) as ctx:
+        pcm = pcm_clip(2, 30.0)  # (oracle: 5 segments, 4 windows)
+        segs = run_fresh(ctx, pcm, beam_params(ctx, 0.0))
+        osegs = replay(ctx, o, pcm, beam_opt(0.0))
+        assert len(segs) >= 3
+        assert_same(segs, osegs, p_tol=1e-4)
+
+
 def test_beam_search_tracks_oracle(rich):
     """Against the oracle's own arithmetic: the first tokens agree until two
     hypotheses come within float noise of each other."""
@@ -334,3 +366,40 @@ def test_quantized_model_greedy_matches_oracle(make_model, qname):
         _, osegs, _, windows = o.full(pcm, opt)
         assert len(segs) > 3 and len(windows) > 1
         assert_same(segs, osegs)
+
+
+def test_draws_fast_path_equals_sequential(rich, monkeypatch):
+    """The parallel draw kernel (margin-checked) and the sequential
+    libstdc++-order kernel give identical beam search / fallback results."""
+    import subprocess, sys, os, json
+    code = r'''
+import json, sys
+sys.path.insert(0, "sentiric-stt-whisper-service_amd")
+import mwx
+path = sys.argv[1]
+ctx = mwx.Context.open(path)
+out = []
+for k, beam in ((0, True), (3, False)):
+    pcm = mwx.pcm16_to_f32(mwx.synth_pcm16(k, 30 * 16000))
+    p = ctx.default_params(mwx.SAMPLING_BEAM_SEARCH if beam else mwx.SAMPLING_GREEDY)
+    p.language = b"en"
+    if not beam:
+        p.temperature = 0.4
+    assert ctx.full(pcm, p, state_index=len(ctx.states)) == 0
+    out.append(mwx.token_ids(ctx.segments(len(ctx.states) - 1)))
+print(json.dumps(out))
+'''
+    _, _, path = rich
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = []
+    for exact in (False, True):
+        env = dict(os.environ)
+        env.pop("MWX_DRAW_EXACT", None)
+        if exact:
+            env["MWX_DRAW_EXACT"] = "1"
+        r = subprocess.run([sys.executable, "-c", code, path], cwd=root, env=env,
+                           capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    assert res[0] == res[1]
+    assert all(len(t) > 0 for t in res[0])
