@@ -48,9 +48,11 @@ def kernel_model(arch, kclass, clips, rows, launches, prompt_len, steps):
     n_mels, d, H, Le, Ld, V = ARCH[arch]
     L, T = 1500, 3000
     if kclass == "dec_attn_cross":
-        # every active row reads its clip's cross K and V for one layer (f16)
-        b = rows * (L * d * 2 * 2 + d * 2 * 2)
-        return "hbm", b, f"{rows:g} rows x (K+V 1500x{d} f16 + q/o) per launch"
+        # every clip's cross K and V for one layer (f16) is read once per launch
+        # (greedy: one row per clip; beam / best-of: the clip's decoders share
+        # it), plus q in / o out per row
+        b = clips * L * d * 2 * 2 + rows * d * 2 * 2
+        return "hbm", b, f"{clips:g} clips x K+V 1500x{d} f16 + {rows:g} rows x q/o per launch"
     if kclass == "enc_gemm":
         conv = 2 * T * d * 3 * n_mels + 2 * L * d * 3 * d
         layer = 2 * L * d * (3 * d + d + 4 * d + 4 * d)
@@ -130,6 +132,8 @@ def main():
                     help="clip length (> 30: long-form, windows decoded one after another)")
     ap.add_argument("--perf-class", default="dec_attn_cross")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--host-input", action="store_true",
+                    help="PCM in host memory, uploaded inside each step (PCIe-inclusive rate)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -172,8 +176,16 @@ def main():
     max_tok = args.decode_steps * n_windows
     gathered = {}
 
+    # inputs resident in HBM before the timed region (the PCIe-inclusive rate,
+    # host buffers uploaded inside the step, is --host-input)
+    if args.host_input:
+        run_batch = lambda: ctx.full_batch(pcms, p)  # noqa: E731
+    else:
+        dev = [ctx.upload(x) for x in pcms]
+        run_batch = lambda: ctx.full_batch_device(dev, p)  # noqa: E731
+
     def step():
-        rc = ctx.full_batch(pcms, p)
+        rc = run_batch()
         if rc != 0:
             raise RuntimeError(f"mwx_full_batch rc={rc}")
         block = shard.pack_tokens([mwx.token_ids(ctx.segments(c)) for c in range(args.clips)],
@@ -217,7 +229,8 @@ def main():
         rows = args.clips * max(1, args.beam)
         if args.perf_class.startswith("dec_attn"):
             rows = rows * ARCH[args.arch][4] * n_dec_steps * args.steps / launches
-        bound, work, desc = kernel_model(args.arch, args.perf_class, args.clips, rows,
+        clips_per_launch = args.clips * (rows / (args.clips * max(1, args.beam)))
+        bound, work, desc = kernel_model(args.arch, args.perf_class, clips_per_launch, rows,
                                          launches // max(1, args.steps), prompt_len,
                                          args.decode_steps)
         traffic = None
@@ -258,7 +271,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": args.wtype,
-            "data": "synthetic (seeded 30-s 16 kHz PCM16 clips; seeded weights in the ggml .bin layout)",
+            "data": ("synthetic (seeded 16 kHz PCM16 clips, "
+                     + ("host memory, uploaded per step" if args.host_input else "resident in HBM")
+                     + "; seeded weights in the ggml .bin layout)"),
             "config": {
                 "workload": (f"whisper-{args.arch} {args.wtype}: {args.clips} x {args.clip_seconds:g} s "
                              f"clips per GPU, mel + encoder + cross-KV + {args.decode_steps} "

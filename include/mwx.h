@@ -174,11 +174,20 @@ int mwx_full_with_state(struct mwx_context* ctx, struct mwx_state* state,
                         int n_samples);
 
 /* Batched variant: clip b (f32 PCM @16 kHz, n_samples[b] samples) is decoded
- * into states[b]. All clips share params. Returns 0 or the first error. */
+ * into states[b]. All clips share params. Returns 0 or the first error.
+ * samples[b] may be host memory or device memory of the context's GPU
+ * (HBM-resident input: copied device-to-device, no PCIe transfer). */
 int mwx_full_batch(struct mwx_context* ctx, struct mwx_state* const* states,
                    struct mwx_full_params params,
                    const float* const* samples, const int* n_samples,
                    int n_clips);
+
+/* Device input buffers on the context's GPU (for mwx_full_batch over
+ * HBM-resident PCM): allocate n floats, upload n floats from host memory
+ * (synchronous), free. NULL / <0 on failure. */
+float* mwx_device_buffer(struct mwx_context* ctx, size_t n);
+int mwx_device_upload(struct mwx_context* ctx, float* dst, const float* src, size_t n);
+void mwx_device_buffer_free(struct mwx_context* ctx, float* p);
 
 /* --- results ------------------------------------------------------------ */
 int mwx_full_n_segments_from_state(struct mwx_state* state);

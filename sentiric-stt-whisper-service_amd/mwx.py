@@ -105,6 +105,13 @@ def lib() -> C.CDLL:
     L.mwx_full_default_params.argtypes = [C.c_int]
     L.mwx_full_with_state.restype = C.c_int
     L.mwx_full_with_state.argtypes = [P, P, FullParams, C.POINTER(C.c_float), C.c_int]
+    fpp = C.POINTER(C.c_float)
+    L.mwx_device_buffer.restype = fpp
+    L.mwx_device_buffer.argtypes = [P, C.c_size_t]
+    L.mwx_device_upload.restype = C.c_int
+    L.mwx_device_upload.argtypes = [P, fpp, fpp, C.c_size_t]
+    L.mwx_device_buffer_free.restype = None
+    L.mwx_device_buffer_free.argtypes = [P, fpp]
     L.mwx_full_batch.restype = C.c_int
     L.mwx_full_batch.argtypes = [P, C.POINTER(P), FullParams, C.POINTER(C.POINTER(C.c_float)),
                                  C.POINTER(C.c_int), C.c_int]
@@ -159,6 +166,24 @@ def lib() -> C.CDLL:
 
 def fptr(a: np.ndarray):
     return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+class DevicePCM:
+    """f32 PCM in a device buffer of the context's GPU (mwx_device_buffer)."""
+
+    def __init__(self, ctx: "Context", pcm: np.ndarray):
+        a = np.ascontiguousarray(pcm, dtype=np.float32)
+        self.ctx, self.n = ctx, len(a)
+        self.ptr = lib().mwx_device_buffer(ctx.ctx, max(1, self.n))
+        if not self.ptr:
+            raise MemoryError("mwx_device_buffer failed")
+        if lib().mwx_device_upload(ctx.ctx, self.ptr, fptr(a), self.n) != 0:
+            raise RuntimeError("mwx_device_upload failed")
+
+    def free(self):
+        if self.ptr:
+            lib().mwx_device_buffer_free(self.ctx.ctx, self.ptr)
+            self.ptr = None
 
 
 def write_synthetic_model(path: str, arch: str, wtype: int = GGML_F16, seed: int = 0) -> None:
@@ -271,6 +296,18 @@ class Context:
         lens = (C.c_int * n)(*[len(a) for a in arrs])
         self._keep = arrs
         return lib().mwx_full_batch(self.ctx, states, params, ptrs, lens, n)
+
+    def upload(self, pcm: np.ndarray) -> "DevicePCM":
+        """Copies PCM into a buffer on this context's GPU (HBM-resident input)."""
+        return DevicePCM(self, pcm)
+
+    def full_batch_device(self, bufs: Sequence["DevicePCM"], params: FullParams) -> int:
+        """Batch over PCM already resident in this GPU's memory: no PCIe transfer."""
+        n = len(bufs)
+        states = (C.c_void_p * n)(*[self.state(i) for i in range(n)])
+        ptrs = (C.POINTER(C.c_float) * n)(*[b.ptr for b in bufs])
+        ln = (C.c_int * n)(*[b.n for b in bufs])
+        return lib().mwx_full_batch(self.ctx, states, params, ptrs, ln, n)
 
     def segments(self, state_index: int = 0) -> List[Segment]:
         L = lib()

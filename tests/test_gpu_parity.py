@@ -189,6 +189,24 @@ def test_bench_fixed_steps_workload(micro):
     assert sum(len(s.tokens) for s in ctx.segments()) == 40
 
 
+def test_device_resident_input_equals_host_input(micro):
+    """mwx_full_batch over PCM already in HBM (mwx_device_buffer) gives the
+    same transcripts as over host PCM."""
+    ctx, o, _ = micro
+    p = service_params(ctx, temperature_inc=0.0, language=b"en")
+    pcms = [pcm_clip(30 + k, 6.0 + 3 * k) for k in range(3)]
+    assert ctx.full_batch(pcms, p) == 0
+    host = [mwx.token_ids(ctx.segments(i)) for i in range(3)]
+    bufs = [ctx.upload(x) for x in pcms]
+    try:
+        assert ctx.full_batch_device(bufs, p) == 0
+        dev = [mwx.token_ids(ctx.segments(i)) for i in range(3)]
+    finally:
+        for b in bufs:
+            b.free()
+    assert dev == host and all(len(t) > 0 for t in host)
+
+
 def test_bench_fixed_steps_long_form(micro):
     """Benchmark workload on a long clip: every 30-s window decodes the fixed
     step count, then the clip advances by a whole window (oracle: same rule)."""
