@@ -132,6 +132,8 @@ def main():
                     help="clip length (> 30: long-form, windows decoded one after another)")
     ap.add_argument("--perf-class", default="dec_attn_cross")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--fp8", action="store_true",
+                    help="MX-fp8 compute for the encoder / cross-K/V GEMMs (C5)")
     ap.add_argument("--host-input", action="store_true",
                     help="PCM in host memory, uploaded inside each step (PCIe-inclusive rate)")
     args = ap.parse_args()
@@ -158,7 +160,8 @@ def main():
         mwx.write_synthetic_model(tmp, args.arch, wt, 0)
         os.replace(tmp, path)
     barrier()
-    ctx = mwx.Context.open(path, device=local)
+    ctx = mwx.Context.open(path, device=local,
+                           compute=mwx.COMPUTE_MXFP8 if args.fp8 else mwx.COMPUTE_MODEL)
     import shard
     n_samp = int(args.clip_seconds * 16000)
     pcms = [mwx.pcm16_to_f32(mwx.synth_pcm16(k, n_samp)) for k in shard.clip_ids(rank, args.clips)]
@@ -270,7 +273,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": args.wtype,
+            "dtype": (f"mxfp8 encoder/cross GEMMs + {args.wtype}" if args.fp8 else args.wtype),
             "data": ("synthetic (seeded 16 kHz PCM16 clips, "
                      + ("host memory, uploaded per step" if args.host_input else "resident in HBM")
                      + "; seeded weights in the ggml .bin layout)"),

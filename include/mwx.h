@@ -69,6 +69,15 @@ struct mwx_context_params {
   bool use_gpu;     /* must be true: the engine has no CPU path */
   bool flash_attn;  /* accepted for API parity; attention is always fused */
   int gpu_device;   /* HIP device ordinal */
+  /* Engine extension: MWX_COMPUTE_MXFP8 runs the encoder and cross-K/V GEMMs
+   * on MX-fp8 operands (e4m3 + one E8M0 scale per 32 k; weights quantized at
+   * load, activations by the producer step) with gfx950's block-scaled fp8
+   * MFMA. MWX_COMPUTE_MODEL (default) computes in the model's 16-bit type. */
+  int compute;
+};
+enum mwx_compute {
+  MWX_COMPUTE_MODEL = 0,
+  MWX_COMPUTE_MXFP8 = 1,
 };
 
 enum mwx_sampling_strategy {

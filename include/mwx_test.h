@@ -36,6 +36,13 @@ int mwx_test_decode(struct mwx_context* ctx, struct mwx_state* state, const int*
 int mwx_test_decode_last(struct mwx_context* ctx, struct mwx_state* state, const int* tokens,
                          int n, float* logits_last);
 
+/* One MX-fp8 GEMM as the fp8 compute mode runs it: a [M][K] is rounded to
+ * bf16 and quantized by the device kernel, w [N][K] by the load-time host
+ * quantizer, c [M][N] = the block-scaled fp8 MFMA product (f32). K % 128 == 0.
+ * Returns 0 or <0. */
+int mwx_test_gemm_mx(struct mwx_context* ctx, int M, int N, int K, const float* a,
+                     const float* w, float* c);
+
 #ifdef __cplusplus
 }
 #endif

@@ -124,7 +124,7 @@ static inline float b2f(uint16_t h) {
 }
 
 enum { T_F32 = 0, T_F16 = 1, T_BF16 = 30 };
-enum { ORC_EXACT = 1 };
+enum { ORC_EXACT = 1, ORC_MXFP8 = 2 };
 
 // ---------------------------------------------------------------------------
 // model
@@ -348,11 +348,45 @@ static inline float dotf(const float* a, const float* b, int n) {
   return s;
 }
 
-// y[M][N] = round_w(x)[M][K] . W[N][K]^T  (ggml_mul_mat, src0 = W)
+// ---------------------------------------------------------------------------
+// MX-fp8 (engine compute mode MWX_COMPUTE_MXFP8; not a whisper.cpp mode):
+// every 32 consecutive k of a row share a power-of-two scale 2^E, E the
+// smallest integer with max|x| <= 448 * 2^E (no clipping); elements are
+// rounded to e4m3fn (round to nearest even, subnormal step 2^-9).
+// ---------------------------------------------------------------------------
+static float e4m3_round(float v) {
+  const float a = fabsf(v);
+  if (a == 0.0f) return v;
+  const int e = ilogbf(a);
+  const float step = e < -6 ? ldexpf(1.0f, -9) : ldexpf(1.0f, e - 3);
+  const float q = rintf(a / step) * step;
+  return v < 0.0f ? -q : q;
+}
+static void mx_round_rows(float* x, size_t rows, int K) {
+  for (size_t r = 0; r < rows; ++r)
+    for (int b = 0; b < K / 32; ++b) {
+      float* p = x + r * K + b * 32;
+      float amax = 0.0f;
+      for (int j = 0; j < 32; ++j) amax = std::max(amax, fabsf(p[j]));
+      int E = 0;
+      if (amax > 0.0f) {
+        E = ilogbf(amax) - 8;
+        while (amax > 448.0f * ldexpf(1.0f, E)) ++E;
+        while (amax <= 448.0f * ldexpf(1.0f, E - 1)) --E;
+        E = std::max(-127, std::min(127, E));
+      }
+      const float X = ldexpf(1.0f, E);
+      for (int j = 0; j < 32; ++j) p[j] = e4m3_round(p[j] / X) * X;
+    }
+}
+
+// y[M][N] = round_w(x)[M][K] . W[N][K]^T  (ggml_mul_mat, src0 = W); mx: the
+// rounded input is further MX-fp8 quantized (W was quantized at load)
 static void matmul(const Model& m, const float* W, const float* x, int M, int N,
-                   int K, float* y) {
+                   int K, float* y, bool mx = false) {
   std::vector<float> xr((size_t)M * K);
   for (size_t i = 0; i < xr.size(); ++i) xr[i] = m.rw(x[i]);
+  if (mx) mx_round_rows(xr.data(), M, K);
 #pragma omp parallel for schedule(static)
   for (int n = 0; n < N; ++n) {
     const float* wr = W + (size_t)n * K;
@@ -630,23 +664,24 @@ static void encode(const Model& m, const Mel& mel, int seek, std::vector<float>&
   const float KQscale = 1.0f / sqrtf((float)(D / H));
   const int n_layers = g_enc_layer_limit >= 0 ? std::min(g_enc_layer_limit, m.n_audio_layer)
                                              : m.n_audio_layer;
+  const bool mx = (m.flags & ORC_MXFP8) != 0;
   for (int il = 0; il < n_layers; ++il) {
     const std::string p = "encoder.blocks." + std::to_string(il);
     layer_norm(inp.data(), m.w(p + ".attn_ln.weight"), m.w(p + ".attn_ln.bias"), M, D, cur.data());
-    matmul(m, m.w(p + ".attn.query.weight"), cur.data(), M, D, D, q.data());
+    matmul(m, m.w(p + ".attn.query.weight"), cur.data(), M, D, D, q.data(), mx);
     add_bias(q.data(), m.w(p + ".attn.query.bias"), M, D);
-    matmul(m, m.w(p + ".attn.key.weight"), cur.data(), M, D, D, k.data());
-    matmul(m, m.w(p + ".attn.value.weight"), cur.data(), M, D, D, v.data());
+    matmul(m, m.w(p + ".attn.key.weight"), cur.data(), M, D, D, k.data(), mx);
+    matmul(m, m.w(p + ".attn.value.weight"), cur.data(), M, D, D, v.data(), mx);
     add_bias(v.data(), m.w(p + ".attn.value.bias"), M, D);
     attention(m, q.data(), k.data(), v.data(), M, M, D, H, KQscale, -1, o.data());
-    matmul(m, m.w(p + ".attn.out.weight"), o.data(), M, D, D, cur.data());
+    matmul(m, m.w(p + ".attn.out.weight"), o.data(), M, D, D, cur.data(), mx);
     add_bias(cur.data(), m.w(p + ".attn.out.bias"), M, D);
     for (size_t i = 0; i < inp.size(); ++i) inp[i] = cur[i] + inp[i];
     layer_norm(inp.data(), m.w(p + ".mlp_ln.weight"), m.w(p + ".mlp_ln.bias"), M, D, cur.data());
-    matmul(m, m.w(p + ".mlp.0.weight"), cur.data(), M, 4 * D, D, ff.data());
+    matmul(m, m.w(p + ".mlp.0.weight"), cur.data(), M, 4 * D, D, ff.data(), mx);
     add_bias(ff.data(), m.w(p + ".mlp.0.bias"), M, 4 * D);
     for (auto& e : ff) e = gelu(m, e);
-    matmul(m, m.w(p + ".mlp.2.weight"), ff.data(), M, D, 4 * D, cur.data());
+    matmul(m, m.w(p + ".mlp.2.weight"), ff.data(), M, D, 4 * D, cur.data(), mx);
     add_bias(cur.data(), m.w(p + ".mlp.2.bias"), M, D);
     for (size_t i = 0; i < inp.size(); ++i) inp[i] = cur[i] + inp[i];
   }
@@ -666,9 +701,11 @@ static void cross(const Model& m, const std::vector<float>& enc, Cross& c) {
   std::vector<float> tmp((size_t)M * D);
   for (int il = 0; il < L; ++il) {
     const std::string p = "decoder.blocks." + std::to_string(il);
-    matmul(m, m.w(p + ".cross_attn.key.weight"), enc.data(), M, D, m.n_audio_state, tmp.data());
+    matmul(m, m.w(p + ".cross_attn.key.weight"), enc.data(), M, D, m.n_audio_state, tmp.data(),
+           m.flags & ORC_MXFP8);
     for (size_t i = 0; i < tmp.size(); ++i) c.k[(size_t)il * M * D + i] = m.r16(tmp[i] * Kscale);
-    matmul(m, m.w(p + ".cross_attn.value.weight"), enc.data(), M, D, m.n_audio_state, tmp.data());
+    matmul(m, m.w(p + ".cross_attn.value.weight"), enc.data(), M, D, m.n_audio_state, tmp.data(),
+           m.flags & ORC_MXFP8);
     add_bias(tmp.data(), m.w(p + ".cross_attn.value.bias"), M, D);
     for (size_t i = 0; i < tmp.size(); ++i) c.v[(size_t)il * M * D + i] = m.r16(tmp[i]);
   }
@@ -1560,6 +1597,25 @@ void* orc_load(const char* path, int flags) {
   if (!load(path, *m)) {
     delete m;
     return nullptr;
+  }
+  if (flags & ORC_MXFP8) {
+    // the engine quantizes these (16-bit) weights to MX-fp8 at load
+    for (auto& kv : m->t) {
+      const std::string& n = kv.first;
+      const bool enc = n.rfind("encoder.blocks.", 0) == 0 &&
+                       (n.find(".attn.") != std::string::npos || n.find(".mlp.") != std::string::npos) &&
+                       n.size() > 7 && n.compare(n.size() - 7, 7, ".weight") == 0;
+      const bool cross = n.find(".cross_attn.key.weight") != std::string::npos ||
+                         n.find(".cross_attn.value.weight") != std::string::npos;
+      if (!enc && !cross) continue;
+      Tensor& t = kv.second;
+      const int K = (int)t.ne[0];
+      if (K % 32) {
+        delete m;
+        return nullptr;
+      }
+      mx_round_rows(t.v.data(), t.v.size() / K, K);
+    }
   }
   return m;
 }

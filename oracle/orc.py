@@ -19,6 +19,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liborc.so")
 ORC_EXACT = 1
+ORC_MXFP8 = 2  # encoder / cross-K/V matmuls on MX-fp8 operands (engine MWX_COMPUTE_MXFP8)
 
 _lib = None
 EXT_ENC = C.CFUNCTYPE(None, C.c_void_p, C.c_int)
@@ -142,11 +143,12 @@ class FullOptions:
 
 
 class Oracle:
-    def __init__(self, path: str, exact: bool = False, threads: Optional[int] = None):
+    def __init__(self, path: str, exact: bool = False, threads: Optional[int] = None,
+                 mxfp8: bool = False):
         L = lib()
         if threads:
             L.orc_set_threads(threads)
-        self.h = L.orc_load(path.encode(), ORC_EXACT if exact else 0)
+        self.h = L.orc_load(path.encode(), (ORC_EXACT if exact else 0) | (ORC_MXFP8 if mxfp8 else 0))
         if not self.h:
             raise RuntimeError(f"oracle failed to load {path}")
         hp = (C.c_int * 11)()

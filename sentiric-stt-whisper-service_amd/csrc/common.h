@@ -35,6 +35,8 @@ void ggml_dequantize(int type, const uint8_t* src, float* dst, int64_t n);
 void ggml_quantize(int type, const float* src, uint8_t* dst, int64_t n);
 // whisper hparams.ftype (ggml_ftype) of a file whose 2-D weights are `type`
 int ggml_ftype_of(int type);
+// one row of K (multiple of 32) values -> MX-fp8 codes q[K] + E8M0 scales s[K/32]
+void mx_quantize_row(const float* x, int K, uint8_t* q, uint8_t* s);
 
 // The 11 int32 header fields of a whisper ggml .bin file, in file order
 // (whisper.cpp whisper_model_load; upstream converter convert-pt-to-ggml.py).

@@ -61,10 +61,16 @@ struct DBuf {
   }
 };
 
+// MX-fp8 weight: e4m3 codes [N][K] + E8M0 scales [N][K/32]
+struct MxW {
+  const uint8_t* q = nullptr;
+  const uint8_t* s = nullptr;
+};
 struct EncLayerW {
   const float *ln1_w, *ln1_b, *ln2_w, *ln2_b;
   const void *qkv_w, *o_w, *fc1_w, *fc2_w;
   const float *qkv_b, *o_b, *fc1_b, *fc2_b;
+  MxW qkv_x, o_x, fc1_x, fc2_x;  // compute = MXFP8
 };
 struct DecLayerW {
   const float *ln1_w, *ln1_b, *lnc_w, *lnc_b, *ln2_w, *ln2_b;
@@ -95,6 +101,8 @@ struct Context {
   std::vector<DecLayerW> dec;
   const void* cross_w = nullptr;
   const float* cross_b = nullptr;
+  bool mx = false;  // MX-fp8 encoder / cross-K/V GEMMs
+  MxW cross_x;
   const float *dec_ln_w = nullptr, *dec_ln_b = nullptr;
   int space_id = -1;
   std::vector<int> nst_ids;  // suppress_nst token ids
@@ -120,6 +128,7 @@ struct State {
   // encoder workspace (clip-batched)
   DBuf pcm, mel, melmax, melT, h1p, x, h, q, k, vt, o, ff, enc, cross_k, cross_v;
   DBuf energy;
+  DBuf aq, as;  // MX-fp8 activations (codes [rows][K], scales [rows][K/32])
   DBuf ibuf;  // small int arrays (slot maps)
   // decoder workspace (row-batched)
   DBuf xd, hd, qd, od, ffd, logits, kself, vself, stepin, ctl, tokout, probs, logprobs, smask;
@@ -317,11 +326,29 @@ static bool upload_model(Context& C, const ModelFile& mf) {
     }
     return true;
   };
-  // row layout [N][K] (encoder GEMMs, embedding gather)
-  auto w16 = [&](const std::vector<std::string>& names, int64_t K, const void** slot) {
+  // row layout [N][K] (encoder GEMMs, embedding gather); with `mx`, also the
+  // MX-fp8 quantization of the same 16-bit values (fp8 compute mode)
+  auto w16 = [&](const std::vector<std::string>& names, int64_t K, const void** slot,
+                 MxW* mx = nullptr) {
     std::vector<uint16_t> w;
     int64_t rows = 0;
-    if (rows16(names, K, w, rows)) A.add(w.data(), w.size() * 2, slot);
+    if (!rows16(names, K, w, rows)) return;
+    A.add(w.data(), w.size() * 2, slot);
+    if (!mx || !C.mx) return;
+    if (K % 128) {
+      MWX_LOG_ERROR("mwx: MX-fp8 compute needs inner dims that are multiples of 128\n");
+      ok = false;
+      return;
+    }
+    std::vector<uint8_t> q((size_t)rows * K), sc((size_t)rows * (K / 32));
+    std::vector<float> row(K);
+    for (int64_t n = 0; n < rows; ++n) {
+      for (int64_t k = 0; k < K; ++k)
+        row[k] = bf ? bf16_to_f32(w[(size_t)n * K + k]) : f16_to_f32(w[(size_t)n * K + k]);
+      mx_quantize_row(row.data(), (int)K, q.data() + (size_t)n * K, sc.data() + (size_t)n * (K / 32));
+    }
+    A.add(q.data(), q.size(), (const void**)&mx->q);
+    A.add(sc.data(), sc.size(), (const void**)&mx->s);
   };
   // decode-GEMM fragment tiles (see kernels.h: pack_index)
   auto w16p = [&](const std::vector<std::string>& names, int64_t K, const void** slot) {
@@ -381,7 +408,8 @@ static bool upload_model(Context& C, const ModelFile& mf) {
     f32v(p + ".attn_ln.bias", &L.ln1_b, d);
     f32v(p + ".mlp_ln.weight", &L.ln2_w, d);
     f32v(p + ".mlp_ln.bias", &L.ln2_b, d);
-    w16({p + ".attn.query.weight", p + ".attn.key.weight", p + ".attn.value.weight"}, d, &L.qkv_w);
+    w16({p + ".attn.query.weight", p + ".attn.key.weight", p + ".attn.value.weight"}, d, &L.qkv_w,
+        &L.qkv_x);
     {
       const FileTensor* qb = need(p + ".attn.query.bias");
       const FileTensor* vb = need(p + ".attn.value.bias");
@@ -394,11 +422,11 @@ static bool upload_model(Context& C, const ModelFile& mf) {
       }
       A.add(b.data(), b.size() * 4, (const void**)&L.qkv_b);
     }
-    w16({p + ".attn.out.weight"}, d, &L.o_w);
+    w16({p + ".attn.out.weight"}, d, &L.o_w, &L.o_x);
     f32v(p + ".attn.out.bias", &L.o_b, d);
-    w16({p + ".mlp.0.weight"}, d, &L.fc1_w);
+    w16({p + ".mlp.0.weight"}, d, &L.fc1_w, &L.fc1_x);
     f32v(p + ".mlp.0.bias", &L.fc1_b, 4 * d);
-    w16({p + ".mlp.2.weight"}, 4 * d, &L.fc2_w);
+    w16({p + ".mlp.2.weight"}, 4 * d, &L.fc2_w, &L.fc2_x);
     f32v(p + ".mlp.2.bias", &L.fc2_b, d);
   }
   f32v("encoder.ln_post.weight", &C.enc_ln_w, d);
@@ -449,7 +477,7 @@ static bool upload_model(Context& C, const ModelFile& mf) {
     const std::vector<float> fv = tensor_f32(*vb);
     for (int i = 0; i < dt; ++i) cross_b.push_back(fv[i]);
   }
-  w16(cross_names, d, &C.cross_w);
+  w16(cross_names, d, &C.cross_w, &C.cross_x);
   A.add(cross_b.data(), cross_b.size() * 4, (const void**)&C.cross_b);
   f32v("decoder.ln.weight", &C.dec_ln_w, dt);
   f32v("decoder.ln.bias", &C.dec_ln_b, dt);
@@ -621,6 +649,21 @@ struct Driver {
     gemm<_Float16>(EPI_CONV2, false, h1p, 2 * d, (long)(T2 + 2) * d, C.conv2_w, 3 * d, Lc, d,
                    3 * d, nb, e, st); }
     const float kq_scale = 1.0f / sqrtf(64.0f);
+    // fp8 compute: the A operand of every encoder / cross GEMM is the 16-bit
+    // activation quantized to MX-fp8 (as the oracle's ORC_MXFP8 mode)
+    uint8_t* aq = C.mx ? (uint8_t*)S.aq.get((size_t)M * 4 * d) : nullptr;
+    uint8_t* as = C.mx ? (uint8_t*)S.as.get((size_t)M * 4 * d / 32) : nullptr;
+    auto mgemm = [&](int epi, const T* a, int Kd, const MxW& w, const void* w16, int N,
+                     EpiParams ep, bool out_f16 = false) {
+      if (C.mx) {
+        mx_quantize<T>(a, Kd, M, Kd, aq, as, st);
+        ep.sa = as;
+        ep.sw = w.s;
+        gemm_mx<T>(epi, aq, Kd, 0, w.q, Kd, M, N, Kd, 1, ep, st);
+      } else {
+        gemm<T>(epi, out_f16, a, Kd, 0, Wt(w16), Kd, M, N, Kd, 1, ep, st);
+      }
+    };
     for (int l = 0; l < L_enc; ++l) {
       const EncLayerW& W = C.enc[l];
       layer_norm<T>(x, W.ln1_w, W.ln1_b, h, M, d, nullptr, st);
@@ -634,7 +677,7 @@ struct Driver {
       e.d = d;
       e.ldv = Lp;  // V^T rows are padded to Lp (16-B aligned tile loads)
       { PerfScope ps(S, "enc_gemm");
-      gemm<T>(EPI_ENC_QKV, false, h, d, 0, Wt(W.qkv_w), d, M, 3 * d, d, 1, e, st); }
+      mgemm(EPI_ENC_QKV, h, d, W.qkv_x, W.qkv_w, 3 * d, e); }
       { PerfScope ps(S, "enc_attn");
       enc_attention<T>(q, k, vt, o, nb, H, Lc, kq_scale, st); }
       e = EpiParams();
@@ -643,21 +686,21 @@ struct Driver {
       e.r32 = x;
       e.ldc = d;
       { PerfScope ps(S, "enc_gemm");
-      gemm<T>(EPI_RES, false, o, d, 0, Wt(W.o_w), d, M, d, d, 1, e, st); }
+      mgemm(EPI_RES, o, d, W.o_x, W.o_w, d, e); }
       layer_norm<T>(x, W.ln2_w, W.ln2_b, h, M, d, nullptr, st);
       e = EpiParams();
       e.bias = W.fc1_b;
       e.c16 = ff;
       e.ldc = 4 * d;
       { PerfScope ps(S, "enc_gemm");
-      gemm<T>(EPI_GELU, false, h, d, 0, Wt(W.fc1_w), d, M, 4 * d, d, 1, e, st); }
+      mgemm(EPI_GELU, h, d, W.fc1_x, W.fc1_w, 4 * d, e); }
       e = EpiParams();
       e.bias = W.fc2_b;
       e.c32 = x;
       e.r32 = x;
       e.ldc = d;
       { PerfScope ps(S, "enc_gemm");
-      gemm<T>(EPI_RES, false, ff, 4 * d, 0, Wt(W.fc2_w), 4 * d, M, d, 4 * d, 1, e, st); }
+      mgemm(EPI_RES, ff, 4 * d, W.fc2_x, W.fc2_w, d, e); }
     }
     layer_norm<T>(x, C.enc_ln_w, C.enc_ln_b, enc, M, d, nullptr, st);
     // cross K/V of every decoder layer in one GEMM
@@ -672,7 +715,7 @@ struct Driver {
     e.slot = ib + 3 * 4096;
     e.kscale = powf(64.0f, -0.25f);
     PerfScope ps(S, "cross_gemm");
-    gemm<T>(EPI_CROSS_KV, false, enc, d, 0, Wt(C.cross_w), d, M, L_dec * 2 * d, d, 1, e, st);
+    mgemm(EPI_CROSS_KV, enc, d, C.cross_x, C.cross_w, L_dec * 2 * d, e);
   }
 
   void ensure_cross(int n_slots) {

@@ -19,6 +19,7 @@
 //                 strip per wave.
 #include <algorithm>
 #include <stdexcept>
+#include <type_traits>
 
 #include "kcommon.h"
 #include "kernels.h"
@@ -111,14 +112,28 @@ constexpr int GWM = 2, GWN = 4;                  // wave grid
 constexpr int GFM = BM / GWM / 16, GFN = BN / GWN / 16;  // 8 x 4 fragments per wave
 constexpr int GDA = BM / 8 / 8, GDB = BN / 8 / 8;  // DMA instructions per wave per tile
 
-template <typename T, int EPI, bool OUT16>
-__global__ __launch_bounds__(512, 1) void gemm_big(const T* __restrict__ A, long lda,
-                                                   long a_bstride, const T* __restrict__ W,
+// MX = true: A and W are MX-fp8 (e4m3 bytes, one E8M0 scale per 32 k of a row:
+// P.sa [M][K/32], P.sw [N][K/32]); a K tile is 128 deep (the same 128 B per
+// row as a 64-deep 16-bit tile, so staging and swizzle are unchanged) and is
+// one v_mfma_scale_f32_16x16x128_f8f6f4 per fragment pair. Operand layout of
+// that instruction (pinned on the GPU, scripts/probe/mfma_scale_probe2.hip):
+// lane l holds row l&15, k = 16*(l>>4) + [0,16) in bytes 0-15 and
+// 64 + 16*(l>>4) + [0,16) in bytes 16-31 -- exactly the 16-B chunks (l>>4)
+// and 4+(l>>4) of the row -- and its scale operand is that row's scale of
+// k block l>>4.
+template <typename T, int EPI, bool OUT16, bool MX = false>
+__global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, long lda,
+                                                   long a_bstride, const void* __restrict__ Wv,
                                                    long ldw, int M, int N, int K, EpiParams P) {
   using V8 = typename Elt<T>::v8;
+  using TE = typename std::conditional<MX, uint8_t, T>::type;  // operand element
+  constexpr int CE = 16 / sizeof(TE);                          // elements per 16-B chunk
+  constexpr int BKE = 8 * CE;                                   // K-tile depth (128 B / row)
+  const TE* A = reinterpret_cast<const TE*>(Av);
+  const TE* W = reinterpret_cast<const TE*>(Wv);
   // one __shared__ array only (a second one can make hipcc drain the LDS DMA
-  // before every ds_read): [stage][A rows 0..255 | W rows 0..255][64 k]
-  __shared__ __attribute__((aligned(16))) T lds[2][(BM + BN) * BK];
+  // before every ds_read): [stage][A rows 0..255 | W rows 0..255][128 B]
+  __shared__ __attribute__((aligned(16))) TE lds[2][(BM + BN) * BKE];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / GWN, wn = wid % GWN;
   const int nbn = (N + BN - 1) / BN;
@@ -130,28 +145,42 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const T* __restrict__ A, long
   // kc ^ (row & 7), conflict-free fragment reads) is applied on the SOURCE
   // address. Rows past M / N are clamped (their outputs are discarded).
   const int lr = lane >> 3, ls = lane & 7;
-  const T* asrc[GDA];
-  const T* wsrc[GDB];
+  const TE* asrc[GDA];
+  const TE* wsrc[GDB];
 #pragma unroll
   for (int i = 0; i < GDA; ++i) {
     const int r = (wid * GDA + i) * 8 + lr;
-    asrc[i] = A + (long)min(m0 + r, M - 1) * lda + (ls ^ (r & 7)) * 8;
+    asrc[i] = A + (long)min(m0 + r, M - 1) * lda + (ls ^ (r & 7)) * CE;
   }
 #pragma unroll
   for (int i = 0; i < GDB; ++i) {
     const int r = (wid * GDB + i) * 8 + lr;
-    wsrc[i] = W + (long)min(n0 + r, N - 1) * ldw + (ls ^ (r & 7)) * 8;
+    wsrc[i] = W + (long)min(n0 + r, N - 1) * ldw + (ls ^ (r & 7)) * CE;
+  }
+  // MX scale rows of this lane's fragments (row = fragment row l&15)
+  const int ksb = K / 32;
+  const uint8_t* sap[GFM];
+  const uint8_t* swp[GFN];
+  if constexpr (MX) {
+#pragma unroll
+    for (int i = 0; i < GFM; ++i)
+      sap[i] = P.sa + (long)bz * P.sa_bstride +
+               (long)min(m0 + wm * (BM / GWM) + i * 16 + (lane & 15), M - 1) * ksb + (lane >> 4);
+#pragma unroll
+    for (int j = 0; j < GFN; ++j)
+      swp[j] = P.sw + (long)min(n0 + wn * (BN / GWN) + j * 16 + (lane & 15), N - 1) * ksb +
+               (lane >> 4);
   }
 #define GLDS(kt, st)                                                                        \
   do {                                                                                      \
-    const int ko = (kt) * BK;                                                               \
+    const int ko = (kt) * BKE;                                                              \
     _Pragma("unroll") for (int i = 0; i < GDA; ++i) __builtin_amdgcn_global_load_lds(       \
         (const void __attribute__((address_space(1)))*)(asrc[i] + ko),                      \
-        (void __attribute__((address_space(3)))*)(&lds[st][((wid * GDA + i) * 8) * BK]), 16, \
+        (void __attribute__((address_space(3)))*)(&lds[st][((wid * GDA + i) * 8) * BKE]), 16, \
         0, 0);                                                                              \
     _Pragma("unroll") for (int i = 0; i < GDB; ++i) __builtin_amdgcn_global_load_lds(       \
         (const void __attribute__((address_space(1)))*)(wsrc[i] + ko),                      \
-        (void __attribute__((address_space(3)))*)(&lds[st][(BM + (wid * GDB + i) * 8) * BK]), \
+        (void __attribute__((address_space(3)))*)(&lds[st][(BM + (wid * GDB + i) * 8) * BKE]), \
         16, 0, 0);                                                                          \
   } while (0)
 
@@ -160,10 +189,17 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const T* __restrict__ A, long
   for (int i = 0; i < GFM; ++i)
 #pragma unroll
     for (int j = 0; j < GFN; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
-  const int nk = K / BK;
+  const int nk = K / BKE;
   GLDS(0, 0);
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
+    int sa_k[MX ? GFM : 1], sw_k[MX ? GFN : 1];
+    if constexpr (MX) {  // this tile's scales (issued before the wait: L2 hits)
+#pragma unroll
+      for (int i = 0; i < GFM; ++i) sa_k[i] = sap[i][kt * 4];
+#pragma unroll
+      for (int j = 0; j < GFN; ++j) sw_k[j] = swp[j][kt * 4];
+    }
     // tile kt has landed (this wave's DMA), then the barrier makes every
     // wave's part visible and orders all reads of the other stage (tile kt-1)
     // before it is refilled below
@@ -172,6 +208,33 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const T* __restrict__ A, long
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     if (kt + 1 < nk) GLDS(kt + 1, cur ^ 1);
+    if constexpr (MX) {
+      typedef int v8i __attribute__((ext_vector_type(8)));
+      v8i af[GFM], bf[GFN];
+      const int g = lane >> 4;
+#pragma unroll
+      for (int i = 0; i < GFM; ++i) {
+        const int row = wm * (BM / GWM) + i * 16 + (lane & 15);
+        const uint4 lo = *reinterpret_cast<const uint4*>(&lds[cur][row * BKE + ((g ^ (row & 7)) << 4)]);
+        const uint4 hi =
+            *reinterpret_cast<const uint4*>(&lds[cur][row * BKE + (((4 + g) ^ (row & 7)) << 4)]);
+        af[i] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+      }
+#pragma unroll
+      for (int j = 0; j < GFN; ++j) {
+        const int row = BM + wn * (BN / GWN) + j * 16 + (lane & 15);
+        const uint4 lo = *reinterpret_cast<const uint4*>(&lds[cur][row * BKE + ((g ^ (row & 7)) << 4)]);
+        const uint4 hi =
+            *reinterpret_cast<const uint4*>(&lds[cur][row * BKE + (((4 + g) ^ (row & 7)) << 4)]);
+        bf[j] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+      }
+#pragma unroll
+      for (int i = 0; i < GFM; ++i)
+#pragma unroll
+        for (int j = 0; j < GFN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+              af[i], bf[j], acc[i][j], 0, 0, 0, sa_k[i], 0, sw_k[j]);
+    } else
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       V8 af[GFM], bf[GFN];
@@ -179,12 +242,12 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const T* __restrict__ A, long
 #pragma unroll
       for (int i = 0; i < GFM; ++i) {
         const int row = wm * (BM / GWM) + i * 16 + (lane & 15);
-        af[i] = *reinterpret_cast<const V8*>(&lds[cur][row * BK + ((kc ^ (row & 7)) << 3)]);
+        af[i] = *reinterpret_cast<const V8*>(&lds[cur][row * BKE + ((kc ^ (row & 7)) << 3)]);
       }
 #pragma unroll
       for (int j = 0; j < GFN; ++j) {
         const int row = BM + wn * (BN / GWN) + j * 16 + (lane & 15);
-        bf[j] = *reinterpret_cast<const V8*>(&lds[cur][row * BK + ((kc ^ (row & 7)) << 3)]);
+        bf[j] = *reinterpret_cast<const V8*>(&lds[cur][row * BKE + ((kc ^ (row & 7)) << 3)]);
       }
 #pragma unroll
       for (int i = 0; i < GFM; ++i)
@@ -554,6 +617,27 @@ static void gemm_dispatch(const T* A, long lda, long a_bstride, const T* W, long
   dim3 g(((N + BN - 1) / BN) * ((M + BM - 1) / BM), batch);
   gemm_big<T, EPI, OUT16><<<g, 512, 0, st>>>(A, lda, a_bstride, W, ldw, M, N, K, P);
 }
+
+template <typename T>
+void gemm_mx(int epi, const uint8_t* A, long lda, long a_bstride, const uint8_t* W, long ldw,
+             int M, int N, int K, int batch, const EpiParams& P, hipStream_t st) {
+  if (K % 128) throw std::runtime_error("mwx: MX-fp8 gemm K must be a multiple of 128");
+  dim3 g(((N + BN - 1) / BN) * ((M + BM - 1) / BM), batch);
+#define MXL(E) gemm_big<T, E, false, true><<<g, 512, 0, st>>>(A, lda, a_bstride, W, ldw, M, N, K, P)
+  switch (epi) {
+    case EPI_ENC_QKV: MXL(EPI_ENC_QKV); break;
+    case EPI_GELU: MXL(EPI_GELU); break;
+    case EPI_RES: MXL(EPI_RES); break;
+    case EPI_CROSS_KV: MXL(EPI_CROSS_KV); break;
+    case EPI_F32: MXL(EPI_F32); break;
+    default: throw std::runtime_error("mwx: unsupported MX-fp8 epilogue");
+  }
+#undef MXL
+}
+template void gemm_mx<_Float16>(int, const uint8_t*, long, long, const uint8_t*, long, int, int,
+                                int, int, const EpiParams&, hipStream_t);
+template void gemm_mx<__bf16>(int, const uint8_t*, long, long, const uint8_t*, long, int, int,
+                              int, int, const EpiParams&, hipStream_t);
 
 template <typename T>
 void gemm(int epi, bool out_f16, const T* A, long lda, long a_bstride, const T* W, long ldw,

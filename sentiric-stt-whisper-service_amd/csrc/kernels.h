@@ -42,7 +42,21 @@ struct EpiParams {
   float kscale = 1.0f;
   float qscale = 1.0f;
   bool pack_out = false;  // EPI_GELU: write the output as decode-GEMM A tiles (pack_index, K = ldc)
+  // MX-fp8 GEMMs: E8M0 scales [rows][K/32] of A (per grid.z batch stride) and W
+  const uint8_t* sa = nullptr;
+  long sa_bstride = 0;
+  const uint8_t* sw = nullptr;
 };
+
+// The encoder GEMMs on MX-fp8 operands (e4m3 bytes + E8M0 scale per 32 k,
+// P.sa / P.sw): EPI_ENC_QKV, EPI_GELU (16-bit T output), EPI_RES, EPI_CROSS_KV.
+template <typename T>
+void gemm_mx(int epi, const uint8_t* A, long lda, long a_bstride, const uint8_t* W, long ldw,
+             int M, int N, int K, int batch, const EpiParams& P, hipStream_t st);
+// Rows of a 16-bit matrix [M][K] (row stride ld) -> MX-fp8: q [M][K] e4m3,
+// s [M][K/32] E8M0 (quant.cpp: mx_quantize_block semantics).
+template <typename T>
+void mx_quantize(const T* x, long ld, int M, int K, uint8_t* q, uint8_t* s, hipStream_t st);
 
 // Decode weights live in HBM as MFMA fragment tiles: for each 16-column strip
 // nt and 32-deep k-step kt, the 16x32 block is 1 KB contiguous in the order the

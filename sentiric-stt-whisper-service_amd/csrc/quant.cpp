@@ -211,4 +211,45 @@ void ggml_quantize(int type, const float* src, uint8_t* dst, int64_t n) {
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// MX-fp8 (OCP MX: 32 consecutive k share an E8M0 scale, elements e4m3fn) for
+// the fp8 compute mode's encoder / cross-K/V weights. Scale rule (no
+// clipping): X = 2^e, e the smallest integer with amax <= 448 * 2^e; codes are
+// e4m3 round-to-nearest-even of x / X (same rule as k_mx.hip).
+// ---------------------------------------------------------------------------
+static int mx_exp_host(float amax) {
+  if (!(amax > 0.0f)) return 0;
+  int e0;
+  const float m = frexpf(amax, &e0);
+  const int e = (e0 - 1) - 8 + (2.0f * m > 1.75f ? 1 : 0);
+  return std::max(-127, std::min(127, e));
+}
+
+static uint8_t e4m3_rne_host(float v) {
+  const uint8_t sgn = v < 0.0f ? 0x80 : 0;
+  const float a = fabsf(v);
+  if (a < 0.015625f) return sgn | (uint8_t)rintf(a * 512.0f);
+  int E;
+  const float m = frexpf(a, &E);
+  int q = (int)rintf(m * 16.0f);
+  int ex = E - 1;
+  if (q == 16) {
+    q = 8;
+    ++ex;
+  }
+  return sgn | (uint8_t)(((ex + 7) << 3) | (q - 8));
+}
+
+void mx_quantize_row(const float* x, int K, uint8_t* q, uint8_t* s) {
+  for (int b = 0; b < K / 32; ++b) {
+    float amax = 0.0f;
+    for (int j = 0; j < 32; ++j) amax = std::max(amax, fabsf(x[b * 32 + j]));
+    const int e = mx_exp_host(amax);
+    const float inv = ldexpf(1.0f, -e);
+    for (int j = 0; j < 32; ++j) q[b * 32 + j] = e4m3_rne_host(x[b * 32 + j] * inv);
+    s[b] = (uint8_t)(127 + e);
+  }
+}
+
 }  // namespace mwx

@@ -37,7 +37,12 @@ SAMPLING_BEAM_SEARCH = 1
 
 
 class ContextParams(C.Structure):
-    _fields_ = [("use_gpu", C.c_bool), ("flash_attn", C.c_bool), ("gpu_device", C.c_int)]
+    _fields_ = [("use_gpu", C.c_bool), ("flash_attn", C.c_bool), ("gpu_device", C.c_int),
+                ("compute", C.c_int)]
+
+
+COMPUTE_MODEL = 0
+COMPUTE_MXFP8 = 1  # encoder / cross-K/V GEMMs on MX-fp8 MFMA
 
 
 class TokenData(C.Structure):
@@ -243,10 +248,11 @@ class Segment:
 class Context:
     """mwx_context + a pool of mwx_state objects."""
 
-    def __init__(self, model_path: str, device: int = 0):
+    def __init__(self, model_path: str, device: int = 0, compute: int = COMPUTE_MODEL):
         L = lib()
         cp = L.mwx_context_default_params()
         cp.gpu_device = device
+        cp.compute = compute
         self.ctx = L.mwx_init_from_file_with_params(model_path.encode(), cp)
         if not self.ctx:
             raise RuntimeError(f"mwx_init_from_file_with_params failed for {model_path}")
@@ -346,6 +352,21 @@ class Context:
             raise RuntimeError(f"mwx_test_mel returned {r}")
         return out
 
+    def test_gemm_mx(self, a: np.ndarray, w: np.ndarray) -> np.ndarray:
+        """c = MX-fp8(bf16(a)) @ MX-fp8(bf16(w))^T on the block-scaled fp8 MFMA."""
+        a = np.ascontiguousarray(a, dtype=np.float32)
+        w = np.ascontiguousarray(w, dtype=np.float32)
+        M, K = a.shape
+        N = w.shape[0]
+        c = np.empty((M, N), np.float32)
+        fn = lib().mwx_test_gemm_mx
+        fn.restype = C.c_int
+        fn.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_float),
+                       C.POINTER(C.c_float), C.POINTER(C.c_float)]
+        if fn(self.ctx, M, N, K, fptr(a), fptr(w), fptr(c)) != 0:
+            raise RuntimeError("mwx_test_gemm_mx failed")
+        return c
+
     def test_encode(self, pcm: np.ndarray, seek: int = 0, cross: bool = True,
                     state_index: int = 0):
         pcm = np.ascontiguousarray(pcm, dtype=np.float32)
@@ -398,8 +419,8 @@ class Context:
         return self._hp
 
     @classmethod
-    def open(cls, model_path: str, device: int = 0) -> "Context":
-        c = cls(model_path, device)
+    def open(cls, model_path: str, device: int = 0, compute: int = COMPUTE_MODEL) -> "Context":
+        c = cls(model_path, device, compute)
         c._hp = read_hparams(model_path)
         return c
 

@@ -421,3 +421,74 @@ print(json.dumps(out))
         res.append(json.loads(r.stdout.strip().splitlines()[-1]))
     assert res[0] == res[1]
     assert all(len(t) > 0 for t in res[0])
+
+
+# ---------------------------------------------------------------- MX-fp8 compute mode
+def _bf16(x):
+    u = np.ascontiguousarray(x, np.float32).view(np.uint32).astype(np.uint64)
+    u = (u + 0x7FFF + ((u >> 16) & 1)) >> 16 << 16
+    return u.astype(np.uint32).view(np.float32)
+
+
+def test_mx_gemm_exact(micro):
+    """One block-scaled fp8 MFMA GEMM (device activation quantizer, host
+    weight quantizer, v_mfma_scale_f32_16x16x128_f8f6f4 operand / scale
+    layout) against float64 products of the same MX-rounded operands: only
+    f32 accumulation error remains. Shapes cover partial 256-row/column tiles."""
+    from test_quant_format import np_mx_round
+    ctx, _, _ = micro
+    rng = np.random.default_rng(5)
+    for M, N, K in ((300, 260, 256), (64, 512, 1280)):
+        a = rng.standard_normal((M, K)).astype(np.float32) * rng.uniform(0.01, 10, (M, 1)).astype(np.float32)
+        w = rng.standard_normal((N, K)).astype(np.float32) * 0.05
+        c = ctx.test_gemm_mx(a, w)
+        aq = np_mx_round(_bf16(a)).reshape(M, K).astype(np.float64)
+        wq = np_mx_round(_bf16(w)).reshape(N, K).astype(np.float64)
+        ref = aq @ wq.T
+        scale = np.abs(aq) @ np.abs(wq).T
+        err = np.abs(c - ref) / (scale + 1e-30)
+        # (observed <= 1.4e-5: the block-scaled MFMA's internal accumulation
+        # is not a plain f32 fma chain)
+        assert err.max() < 5e-5, (M, N, K, err.max())
+        assert err.mean() < 2e-6, (M, N, K, err.mean())
+def test_mxfp8_encoder_matches_mx_oracle(make_model):
+    """MWX_COMPUTE_MXFP8: encoder and cross-K/V GEMMs on block-scaled fp8 MFMA.
+    The oracle's ORC_MXFP8 mode applies the same MX rounding to the same
+    operands. fp8 re-rounding amplifies tiny differences: the oracle itself
+    moves by 0.016 mean abs when its mel input is perturbed by 1e-5 (0.0015 in
+    16-bit mode), so the bar is that noise level, and the device must be
+    clearly closer to the MX oracle than to the 16-bit one."""
+    path = make_model("micro", mwx.GGML_BF16)
+    pcm = pcm_clip(0)
+    with mwx.Context.open(path, compute=mwx.COMPUTE_MXFP8) as ctx:
+        enc, k, v = ctx.test_encode(pcm)
+    omx, o16 = orc.Oracle(path, mxfp8=True), orc.Oracle(path)
+    mel, _ = omx.mel(pcm)
+    ref = omx.encode(mel)
+    ref16 = o16.encode(mel)
+    k_ref, v_ref = omx.cross(ref)
+    d_mx = np.abs(enc - ref)
+    d_16 = np.abs(enc - ref16)
+    assert d_mx.mean() < 0.6 * d_16.mean(), (d_mx.mean(), d_16.mean())
+    assert d_mx.mean() < 0.03 and d_mx.max() < 0.5, (d_mx.mean(), d_mx.max())
+    k16, v16 = o16.cross(ref16)
+    for got, want, want16 in ((k, k_ref, k16), (v, v_ref, v16)):
+        assert np.abs(got - want).mean() < 0.6 * np.abs(got - want16).mean()
+
+
+def test_mxfp8_greedy_tokens_track_mx_oracle(make_model):
+    """fp8 mode end to end: the token stream agrees with the MX oracle's until
+    fp8 re-rounding noise (see above) first reorders two close logits."""
+    path = make_model("micro-rich", mwx.GGML_BF16)
+    o = orc.Oracle(path, mxfp8=True)
+    with mwx.Context.open(path, compute=mwx.COMPUTE_MXFP8) as ctx:
+        pcm = pcm_clip(0)
+        opt = orc.FullOptions.service_defaults()
+        opt.temperature_inc = 0.0
+        opt.language = "en"
+        segs = run_fresh(ctx, pcm, service_params(ctx, temperature_inc=0.0, language=b"en"))
+        _, osegs, _, windows = o.full(pcm, opt)
+        assert len(segs) > 3 and len(windows) > 1
+        ids = [t.id for sg in segs for t in sg.tokens]
+        oids = [t.id for sg in osegs for t in sg.tokens]
+        assert ids[:16] == oids[:16]

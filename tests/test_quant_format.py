@@ -126,3 +126,35 @@ def test_q8_0_blocks_match_ggml_reference_quantizer(make_model):
     assert np.abs(q.astype(int) - q_np.astype(int)).max() <= 1
     np.testing.assert_allclose(d.astype(np.float32).reshape(-1), d_np.astype(np.float32).reshape(-1),
                                rtol=2e-3)
+
+
+def np_mx_round(x):
+    """MX-fp8 rule of the engine's fp8 compute mode (independent numpy
+    restatement): per 32 k, X = 2^E with E the smallest integer such that
+    max|x| <= 448 * 2^E; elements rounded to e4m3fn (nearest even, subnormal
+    step 2^-9) in units of X."""
+    x = x.astype(np.float32).reshape(-1, 32)
+    amax = np.abs(x).max(axis=1)
+    E = np.zeros(len(x), np.int64)
+    nz = amax > 0
+    E[nz] = np.ceil(np.log2(amax[nz].astype(np.float64) / 448.0)).astype(np.int64)
+    X = np.ldexp(np.float32(1.0), E).astype(np.float32)[:, None]
+    v = x / X
+    a = np.abs(v)
+    e = np.floor(np.log2(np.where(a > 0, a, 1.0))).astype(np.int64)
+    step = np.where(e < -6, np.float32(2.0 ** -9), np.ldexp(np.float32(1.0), e - 3)).astype(np.float32)
+    q = (np.rint(a / step) * step * np.sign(v)).astype(np.float32)
+    return (q * X).reshape(-1)
+
+
+def test_mxfp8_weights_follow_the_mx_rule(make_model):
+    """Oracle MX-fp8 mode: encoder and cross-K/V weights are the MX rounding of
+    the file's 16-bit weights (numpy restatement); other weights untouched."""
+    path = make_model("micro", mwx.GGML_BF16)
+    plain, mx = orc.Oracle(path), orc.Oracle(path, mxfp8=True)
+    for name in ("encoder.blocks.0.attn.query.weight", "encoder.blocks.1.mlp.2.weight",
+                 "decoder.blocks.2.cross_attn.value.weight"):
+        np.testing.assert_array_equal(mx.tensor(name), np_mx_round(plain.tensor(name)))
+    for name in ("decoder.blocks.0.attn.query.weight", "decoder.token_embedding.weight",
+                 "encoder.conv1.weight"):
+        np.testing.assert_array_equal(mx.tensor(name), plain.tensor(name))
