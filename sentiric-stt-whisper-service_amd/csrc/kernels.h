@@ -46,6 +46,7 @@ struct EpiParams {
   const uint8_t* sa = nullptr;
   long sa_bstride = 0;
   const uint8_t* sw = nullptr;
+  bool xcd_remap = true;  // gemm_big: XCD-aware tile order
 };
 
 // The encoder GEMMs on MX-fp8 operands (e4m3 bytes + E8M0 scale per 32 k,

@@ -77,6 +77,33 @@ void* mwx_stt_new(const char* model_dir, const char* model_filename, int paralle
   }
 }
 
+// As mwx_stt_new, with dynamic request batching (Settings::max_batch /
+// batch_window_us).
+void* mwx_stt_new_batched(const char* model_dir, const char* model_filename,
+                          int parallel_requests, int queue_timeout_ms, int beam_size,
+                          const char* language, int vad_ms_min, int gpu_device, int max_batch,
+                          int batch_window_us) {
+  Settings s;
+  s.model_dir = model_dir;
+  s.model_filename = model_filename;
+  s.parallel_requests = parallel_requests;
+  s.request_queue_timeout_ms = queue_timeout_ms;
+  s.beam_size = beam_size;
+  s.language = language;
+  s.vad_ms_min_duration = vad_ms_min;
+  s.gpu_device = gpu_device;
+  s.max_batch = max_batch;
+  s.batch_window_us = batch_window_us;
+  try {
+    return new SttEngine(s);
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "SttEngine: %s\n", e.what());
+    return nullptr;
+  }
+}
+
+long mwx_stt_batches(void* eng) { return static_cast<SttEngine*>(eng)->batches_run(); }
+
 void mwx_stt_free(void* eng) { delete static_cast<SttEngine*>(eng); }
 
 // 0.. = JSON length written; -1 = error; -2 = EngineBusyException;

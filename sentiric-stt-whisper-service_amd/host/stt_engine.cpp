@@ -34,6 +34,20 @@ SttEngine::SttEngine(const Settings& settings) : settings_(settings) {
   ctx_ = mwx_init_from_file_with_params(path.c_str(), cp);
   if (!ctx_) throw std::runtime_error("Whisper model initialization failed");
   const int pool = std::max(1, settings_.parallel_requests);
+  if (settings_.max_batch > 1) {
+    // one batcher thread per pool slot, each with its own max_batch states
+    for (int i = 0; i < pool; ++i) {
+      std::vector<mwx_state*> sts;
+      for (int b = 0; b < settings_.max_batch; ++b) {
+        mwx_state* st = mwx_init_state(ctx_);
+        if (!st) throw std::runtime_error("Whisper state initialization failed");
+        sts.push_back(st);
+        all_states_.push_back(st);
+      }
+      batchers_.emplace_back(&SttEngine::batcher_loop, this, sts);
+    }
+    return;
+  }
   for (int i = 0; i < pool; ++i) {
     mwx_state* st = mwx_init_state(ctx_);
     if (!st) throw std::runtime_error("Whisper state initialization failed");
@@ -43,8 +57,129 @@ SttEngine::SttEngine(const Settings& settings) : settings_(settings) {
 }
 
 SttEngine::~SttEngine() {
+  {
+    std::lock_guard<std::mutex> lock(q_mutex_);
+    stop_ = true;
+  }
+  q_cv_.notify_all();
+  for (auto& t : batchers_) t.join();
   for (mwx_state* st : all_states_) mwx_free_state(st);
   if (ctx_) mwx_free(ctx_);
+}
+
+// Everything make_params reads from the request: equal keys -> identical
+// mwx_full_params, so those requests can share one mwx_full_batch.
+std::string SttEngine::options_key(const RequestOptions& o) const {
+  const int beam = o.beam_size >= 0 ? o.beam_size : settings_.beam_size;
+  const float temp = o.temperature >= 0.0f ? o.temperature : settings_.temperature;
+  const int best_of = o.best_of >= 0 ? o.best_of : settings_.best_of;
+  const std::string lang = o.language.empty() ? settings_.language : o.language;
+  char buf[96];
+  std::snprintf(buf, sizeof buf, "%d|%.9g|%d|%d|%d|", beam, temp, best_of, (int)o.translate,
+                (int)o.enable_diarization);
+  return std::string(buf) + lang + "|" + o.prompt;
+}
+
+std::vector<TranscriptionResult> SttEngine::transcribe_batched(const std::vector<float>& pcmf32,
+                                                               const RequestOptions& options,
+                                                               PerformanceMetrics* out_metrics) {
+  auto req = std::make_shared<Pending>();
+  req->pcm = &pcmf32;
+  req->options = options;
+  req->key = options_key(options);
+  req->t_enq = std::chrono::steady_clock::now();
+  std::unique_lock<std::mutex> lock(q_mutex_);
+  queue_.push_back(req);
+  q_cv_.notify_one();
+  // EngineBusyException when no batcher picks the request up in time
+  // (the state-pool queue timeout of src/stt_engine.cpp:63-85)
+  if (!done_cv_.wait_for(lock, std::chrono::milliseconds(settings_.request_queue_timeout_ms),
+                         [&] { return req->started; })) {
+    req->cancelled = true;
+    for (auto it = queue_.begin(); it != queue_.end(); ++it)
+      if (*it == req) {
+        queue_.erase(it);
+        break;
+      }
+    throw EngineBusyException("Server is busy (Queue timeout)");
+  }
+  done_cv_.wait(lock, [&] { return req->done; });
+  if (out_metrics) *out_metrics = {req->t_start_ms, req->t_proc_ms, req->token_count};
+  if (req->ret != 0) {
+    std::fprintf(stderr, "Whisper processing failed: %d\n", req->ret);
+    return {};
+  }
+  return std::move(req->results);
+}
+
+void SttEngine::batcher_loop(std::vector<mwx_state*> states) {
+  const int max_b = (int)states.size();
+  while (true) {
+    std::vector<std::shared_ptr<Pending>> batch;
+    {
+      std::unique_lock<std::mutex> lock(q_mutex_);
+      q_cv_.wait(lock, [&] { return stop_ || !queue_.empty(); });
+      if (stop_) return;
+      // gather: wait up to batch_window_us for more requests of this key
+      const auto deadline = queue_.front()->t_enq +
+                            std::chrono::microseconds(settings_.batch_window_us);
+      const std::string key = queue_.front()->key;
+      auto count = [&] {
+        int c = 0;
+        for (auto& r : queue_) c += r->key == key;
+        return c;
+      };
+      while (!stop_ && count() < max_b &&
+             q_cv_.wait_until(lock, deadline) != std::cv_status::timeout) {
+      }
+      if (stop_) return;
+      for (auto it = queue_.begin(); it != queue_.end() && (int)batch.size() < max_b;) {
+        if ((*it)->key == key) {
+          (*it)->started = true;
+          batch.push_back(*it);
+          it = queue_.erase(it);
+        } else {
+          ++it;
+        }
+      }
+    }
+    done_cv_.notify_all();
+    if (batch.empty()) continue;
+    const auto t0 = std::chrono::steady_clock::now();
+    std::string lang;
+    // the batch is aborted only when every request in it asks to abort
+    std::function<bool()> abort_fn = nullptr;
+    bool any_abort = false;
+    for (auto& r : batch) any_abort |= (bool)r->options.should_abort;
+    if (any_abort)
+      abort_fn = [&batch] {
+        for (auto& r : batch)
+          if (!r->options.should_abort || !r->options.should_abort()) return false;
+        return true;
+      };
+    const mwx_full_params p = make_params(batch[0]->options, lang, abort_fn);
+    std::vector<const float*> ptrs;
+    std::vector<int> lens;
+    for (auto& r : batch) {
+      ptrs.push_back(r->pcm->data());
+      lens.push_back((int)r->pcm->size());
+    }
+    const int ret = mwx_full_batch(ctx_, states.data(), p, ptrs.data(), lens.data(), (int)batch.size());
+    const auto t1 = std::chrono::steady_clock::now();
+    batches_run_++;
+    for (size_t b = 0; b < batch.size(); ++b) {
+      auto& r = *batch[b];
+      r.ret = ret;
+      r.t_start_ms = ms_between(r.t_enq, t0);
+      r.t_proc_ms = ms_between(t0, t1);
+      if (ret == 0) r.results = collect(states[b], lang, r.pcm->size(), &r.token_count);
+    }
+    {
+      std::lock_guard<std::mutex> lock(q_mutex_);
+      for (auto& r : batch) r->done = true;
+    }
+    done_cv_.notify_all();
+  }
 }
 
 mwx_state* SttEngine::acquire_state() {
@@ -174,6 +309,7 @@ std::vector<TranscriptionResult> SttEngine::transcribe(const std::vector<float>&
     if (out_metrics) *out_metrics = {0.0, 0.0, 0};
     return {};
   }
+  if (settings_.max_batch > 1) return transcribe_batched(pcmf32, options, out_metrics);
   StateGuard guard(*this);
   mwx_state* state = guard.get();
   const auto t_acq = std::chrono::steady_clock::now();

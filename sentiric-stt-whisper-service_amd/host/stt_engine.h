@@ -12,13 +12,18 @@
 // prosody and speaker clustering (their result fields keep neutral values).
 #pragma once
 
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdint>
+#include <deque>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <queue>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "mwx.h"
@@ -45,6 +50,14 @@ struct Settings {
   bool suppress_nst = true;
   int gpu_device = 0;
   int stream_buffer_samples = 8000;
+  // Engine extension (no reference counterpart): dynamic request batching.
+  // max_batch > 1: concurrent transcribe() calls with the same decoding
+  // options are gathered (up to max_batch, waiting at most batch_window_us
+  // for more) and run as one mwx_full_batch by one of parallel_requests
+  // batcher threads. max_batch = 1 keeps the reference's one-request-per-
+  // state path.
+  int max_batch = 1;
+  int batch_window_us = 2000;
 };
 
 struct TokenData {
@@ -116,7 +129,35 @@ class SttEngine {
   std::vector<std::vector<TranscriptionResult>> transcribe_batch(
       const std::vector<std::vector<float>>& clips, const RequestOptions& options);
 
+  // Batches run by the request batcher so far (max_batch > 1).
+  long batches_run() const { return batches_run_.load(); }
+
  private:
+  // ---- dynamic request batching (Settings::max_batch > 1) ----
+  struct Pending {
+    const std::vector<float>* pcm;
+    RequestOptions options;
+    std::string key;  // requests with equal keys share mwx_full_params
+    std::chrono::steady_clock::time_point t_enq;
+    bool started = false, done = false, cancelled = false;
+    int ret = 0;
+    double t_start_ms = 0.0, t_proc_ms = 0.0;
+    int token_count = 0;
+    std::vector<TranscriptionResult> results;
+  };
+  std::vector<TranscriptionResult> transcribe_batched(const std::vector<float>& pcmf32,
+                                                      const RequestOptions& options,
+                                                      PerformanceMetrics* out_metrics);
+  void batcher_loop(std::vector<mwx_state*> states);
+  std::string options_key(const RequestOptions& o) const;
+  std::deque<std::shared_ptr<Pending>> queue_;
+  std::mutex q_mutex_;
+  std::condition_variable q_cv_;     // batcher: new work / stop
+  std::condition_variable done_cv_;  // callers: started / done
+  std::vector<std::thread> batchers_;
+  bool stop_ = false;
+  std::atomic<long> batches_run_{0};
+
   mwx_state* acquire_state();
   void release_state(mwx_state* state);
   mwx_full_params make_params(const RequestOptions& options, std::string& target_lang,

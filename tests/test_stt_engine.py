@@ -28,6 +28,11 @@ def lib():
     L.mwx_stt_new.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_char_p,
                               C.c_int, C.c_int]
     L.mwx_stt_free.argtypes = [C.c_void_p]
+    L.mwx_stt_new_batched.restype = C.c_void_p
+    L.mwx_stt_new_batched.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_int,
+                                      C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int]
+    L.mwx_stt_batches.restype = C.c_long
+    L.mwx_stt_batches.argtypes = [C.c_void_p]
     L.mwx_stt_transcribe_pcm16.argtypes = [C.c_void_p, C.POINTER(C.c_int16), C.c_int, C.c_int,
                                            C.c_char_p, C.c_int, C.c_float, C.c_char_p, C.c_int,
                                            C.POINTER(C.c_double)]
@@ -60,7 +65,7 @@ def test_is_hallucination_matches_restatement():
 def test_library_exports():
     L = lib()
     for name in ("mwx_stt_is_hallucination", "mwx_stt_new", "mwx_stt_free",
-                 "mwx_stt_transcribe_pcm16"):
+                 "mwx_stt_transcribe_pcm16", "mwx_stt_new_batched", "mwx_stt_batches"):
         assert hasattr(L, name)
 
 
@@ -147,6 +152,46 @@ def test_engine_busy_when_pool_exhausted(tmp_path):
         assert -2 in codes and any(c >= 0 for c in codes), codes
     finally:
         L.mwx_stt_free(eng)
+
+
+@pytest.mark.gpu
+def test_dynamic_batching_equals_single_requests(tmp_path):
+    """Concurrent transcribe_pcm16 calls on an engine with max_batch 8 are
+    served as shared mwx_full_batch runs; every caller gets exactly the
+    result a one-request engine gives for its clip (fresh states on both
+    sides, so the fallback sampler's RNG streams match)."""
+    import mwx
+    path = str(tmp_path / "ggml-micro.bin")
+    mwx.write_synthetic_model(path, "micro-rich", mwx.GGML_F16, 0)
+    L = lib()
+    d = str(tmp_path).encode()
+    clips = [mwx.synth_pcm16(40 + k, n=(6 + 3 * k) * 16000) for k in range(8)]
+    singles = []
+    for pcm in clips:
+        eng = L.mwx_stt_new(d, b"ggml-micro.bin", 1, 5000, 1, b"en", 500, 0)
+        rc, res, _ = _transcribe(L, eng, pcm)
+        L.mwx_stt_free(eng)
+        assert rc >= 0
+        singles.append(res)
+    eng = L.mwx_stt_new_batched(d, b"ggml-micro.bin", 1, 20000, 1, b"en", 500, 0, 8, 200000)
+    assert eng
+    out = [None] * len(clips)
+
+    def run(i):
+        out[i] = _transcribe(L, eng, clips[i])
+
+    try:
+        ts = [threading.Thread(target=run, args=(i,)) for i in range(len(clips))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        batches = L.mwx_stt_batches(eng)
+    finally:
+        L.mwx_stt_free(eng)
+    assert all(o[0] >= 0 for o in out)
+    assert [o[1] for o in out] == singles
+    assert batches < len(clips), batches  # requests were actually batched
 
 
 def test_missing_model_raises_in_constructor(tmp_path):
