@@ -3,7 +3,7 @@ set -o pipefail
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
 TAG=${1:-fp8}
-timeout -k 10 600 python -u -m pytest tests -m gpu ${PYTEST_K} -x -q -rf --timeout 300 --timeout-method thread > gpurun_out/tests_$TAG.log 2>&1 || { echo "tests failed"; tail -40 gpurun_out/tests_$TAG.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests -m gpu ${PYTEST_K:+-k "$PYTEST_K"} -x -q -rf --timeout 300 --timeout-method thread > gpurun_out/tests_$TAG.log 2>&1 || { echo "tests failed"; tail -40 gpurun_out/tests_$TAG.log; exit 1; }
 tail -2 gpurun_out/tests_$TAG.log
 timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --fp8 > gpurun_out/bench_${TAG}.log 2>&1 || { echo "fp8 bench failed"; tail -20 gpurun_out/bench_${TAG}.log; exit 1; }
 tail -1 gpurun_out/bench_${TAG}.log | cut -c1-200

@@ -16,6 +16,8 @@
 //   non-flash path exactly: f32 scores of f16 q.k, scale, max, exp, double
 //   sum, multiply by (float)(1/sum), round P to f16, then P.V in f32. K and V
 //   rows are streamed with 8 lanes per 128-B row (fully coalesced).
+#include <cstdlib>
+
 #include "kcommon.h"
 #include "kernels.h"
 
@@ -224,6 +226,19 @@ __device__ __forceinline__ double block_sum_256d(double v, double* red) {
   return (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+// q.k over 8 f16 elements with v_dot2_f32_f16 (q, k exact f16 values; f32
+// accumulation, pairs in index order): 4 instructions instead of 8 multiplies
+// and 8 adds. Used by every decode attention kernel, so all of them score a
+// row identically.
+__device__ __forceinline__ float dot8(const h2* q, f16x8 k) {
+  float d = __builtin_amdgcn_fdot2(q[0], __builtin_shufflevector(k, k, 0, 1), 0.0f, false);
+  d = __builtin_amdgcn_fdot2(q[1], __builtin_shufflevector(k, k, 2, 3), d, false);
+  d = __builtin_amdgcn_fdot2(q[2], __builtin_shufflevector(k, k, 4, 5), d, false);
+  d = __builtin_amdgcn_fdot2(q[3], __builtin_shufflevector(k, k, 6, 7), d, false);
+  return d;
+}
+
 // sum over the 8 lanes of an aligned lane group (DPP: xor 1, xor 2 within a
 // quad, then the mirrored quad); every lane of the group gets the same value
 __device__ __forceinline__ float dpp_sum8(float d) {
@@ -332,13 +347,17 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
     }
   }
   __syncthreads();
-  float qv[8], nk[8], nv[8];
+  float nv[8];
+  h2 qh[4];
+  f16x8 nkh;
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    qv[e] = sq[c * 8 + e];
-    nk[e] = SELF ? snk[c * 8 + e] : 0.0f;
+    nkh[e] = SELF ? (_Float16)snk[c * 8 + e] : (_Float16)0.0f;
     nv[e] = SELF ? snv[c * 8 + e] : 0.0f;
   }
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    qh[e] = h2{(_Float16)sq[c * 8 + 2 * e], (_Float16)sq[c * 8 + 2 * e + 1]};
   // scores (q.k in f32 over the f16 rows)
   auto score_batch = [&](const f16x8* kk, int bidx) {
     __builtin_amdgcn_sched_barrier(0);  // keep exactly one batch of loads ahead
@@ -347,9 +366,7 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
       const int j = bidx * 256 + wid * 64 + u * 8 + kg;
       // (j >= n lanes also take the LDS row: finite, and their score is dropped)
       const bool isnew = SELF && min(j, n - 1) == jnew;
-      float d = 0.0f;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) d += qv[e] * (isnew ? nk[e] : (float)kk[u][e]);
+      float d = dot8(qh, isnew ? nkh : kk[u]);
       d = dpp_sum8(d);
       if (c == 0 && j < n) sc[j] = d * scale;
     }
@@ -387,15 +404,28 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
   float acc[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) acc[e] = 0.0f;
+  f16x8 nvh;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) nvh[e] = (_Float16)nv[e];
+  // P.V with v_dot2_f32_f16 over the lane's row pairs (u, u+1): acc[e] +=
+  // p_u*v_u[e] + p_u1*v_u1[e] (P is f16 exact, as ggml rounds it)
   auto pv_batch = [&](const f16x8* vv, int bidx) {
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int u = 0; u < UB; ++u) {
-      const int j = bidx * 256 + wid * 64 + u * 8 + kg;
-      const bool isnew = SELF && min(j, n - 1) == jnew;  // p = 0 past the end
-      const float p = j < n ? sc[min(j, n - 1)] : 0.0f;
+    for (int u = 0; u < UB; u += 2) {
+      h2 ph;
+      f16x8 r[2];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] += p * (isnew ? nv[e] : (float)vv[u][e]);
+      for (int t = 0; t < 2; ++t) {
+        const int j = bidx * 256 + wid * 64 + (u + t) * 8 + kg;
+        const bool isnew = SELF && min(j, n - 1) == jnew;
+        float p = sc[min(j, n - 1)];  // (unconditional read: no exec-masked ds_read)
+        if (j >= n) p = 0.0f;          // p = 0 past the end
+        ph[t] = (_Float16)p;
+        r[t] = isnew ? nvh : vv[u + t];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] = __builtin_amdgcn_fdot2(ph, h2{r[0][e], r[1][e]}, acc[e], false);
     }
   };
   if constexpr (SELF) {
@@ -437,7 +467,7 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
 // is exactly that of dec_attn_kernel<T, false>, so results do not depend on
 // the grouping.
 template <typename T, int NQ>
-__global__ __launch_bounds__(256, 2) void dec_xattn_kernel(
+__global__ __launch_bounds__(256) void dec_xattn_kernel(
     const float* __restrict__ P, int KS, int pcols, const float* __restrict__ bias,
     const _Float16* __restrict__ kbase, const _Float16* __restrict__ vbase,
     const int* __restrict__ kv_index, const int* __restrict__ active, int n, int cap, int R,
@@ -487,25 +517,21 @@ __global__ __launch_bounds__(256, 2) void dec_xattn_kernel(
   }
   LOADROWS(ka, K, 0, 0)
   __syncthreads();
-  float qv[NQ][8];
+  h2 qh[NQ][4];
 #pragma unroll
   for (int q = 0; q < NQ; ++q)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) qv[q][e] = sq[q][c * 8 + e];
+    for (int e = 0; e < 4; ++e)
+      qh[q][e] = h2{(_Float16)sq[q][c * 8 + 2 * e], (_Float16)sq[q][c * 8 + 2 * e + 1]};
   auto score_batch = [&](const f16x8* kk, int bidx, int half) {
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int uu = 0; uu < UH; ++uu) {
       const int u = half * UH + uu;
       const int j = bidx * 256 + wid * 64 + u * 8 + kg;
-      float kf[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) kf[e] = (float)kk[uu][e];
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
-        float d = 0.0f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) d += qv[q][e] * kf[e];
+        float d = dot8(qh[q], kk[uu]);
         d = dpp_sum8(d);
         if (c == 0 && j < n) sc[q][j] = d * scale;
       }
@@ -565,16 +591,19 @@ __global__ __launch_bounds__(256, 2) void dec_xattn_kernel(
   auto pv_batch = [&](const f16x8* vv, int bidx, int half) {
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int uu = 0; uu < UH; ++uu) {
-      const int j = bidx * 256 + wid * 64 + (half * UH + uu) * 8 + kg;
-      float vf[8];
+    for (int uu = 0; uu < UH; uu += 2) {  // row pairs (u, u+1) as in dec_attn_kernel
+      const int j0 = bidx * 256 + wid * 64 + (half * UH + uu) * 8 + kg, j1 = j0 + 8;
+      h2 vp[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) vf[e] = (float)vv[uu][e];
+      for (int e = 0; e < 8; ++e) vp[e] = h2{vv[uu][e], vv[uu + 1][e]};
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
-        const float p = j < n ? sc[q][min(j, n - 1)] : 0.0f;
+        float p0 = sc[q][min(j0, n - 1)], p1 = sc[q][min(j1, n - 1)];
+        if (j0 >= n) p0 = 0.0f;
+        if (j1 >= n) p1 = 0.0f;
+        const h2 ph = h2{(_Float16)p0, (_Float16)p1};
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc[q][e] += p * vf[e];
+        for (int e = 0; e < 8; ++e) acc[q][e] = __builtin_amdgcn_fdot2(ph, vp[e], acc[q][e], false);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
