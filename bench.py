@@ -117,6 +117,151 @@ def cpu_baseline(model_path, arch, threads, prompt_len, steps):
     }
 
 
+def prosody_segments(n_samp, seed):
+    """Whisper-like segmentation of one clip: consecutive 1-8 s segments."""
+    rng = np.random.default_rng(seed)
+    starts, lens, s = [], [], 0
+    while s < n_samp:
+        n = min(int(rng.integers(16000, 8 * 16000)), n_samp - s)
+        starts.append(s)
+        lens.append(n)
+        s += n
+    return starts, lens
+
+
+def prosody_bench(args):
+    """Segment prosody (k_prosody.hip through mwx_prosody_batch_device) over
+    the segments of --clips clips per GPU (default 256 x 30 s), PCM and
+    segment table resident in HBM; one launch per step, one workgroup per
+    segment. CPU baseline: the reference's own extract_prosody
+    (oracle/_ref) on a bounded sample of the same segments."""
+    import ctypes
+    import torch
+    import mwx
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    import shard
+    clips = args.clips if args.clips != 32 else 256
+    n_samp = int(args.clip_seconds * 16000)
+    ids = shard.clip_ids(rank, clips)
+    pcm = np.concatenate([mwx.pcm16_to_f32(mwx.synth_pcm16(k, n_samp)) for k in ids])
+    desc, frames = [], 0
+    for c, k in enumerate(ids):
+        st, ln = prosody_segments(n_samp, k)
+        for s0, n in zip(st, ln):
+            desc.append((c * n_samp + s0, n, frames))
+            frames += n // 160 if n >= 160 else 0
+    desc = np.array(desc, np.int64)
+    n_seg = len(desc)
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "mwx_bench_prosody_micro.bin")
+    if local == 0 and not os.path.exists(path):
+        tmp = path + f".tmp{os.getpid()}"
+        mwx.write_synthetic_model(tmp, "micro", mwx.GGML_F16, 0)
+        os.replace(tmp, path)
+    if dist is not None:
+        dist.barrier()
+    ctx = mwx.Context.open(path, device=local)
+    L = mwx.lib()
+    d_pcm = torch.from_numpy(pcm).to(f"cuda:{local}")
+    d_desc = torch.from_numpy(desc.reshape(-1)).to(f"cuda:{local}")
+    d_out = torch.empty(n_seg * ctypes.sizeof(mwx.Prosody), dtype=torch.uint8, device=f"cuda:{local}")
+    prm = L.mwx_prosody_default_params()
+    st0 = ctx.state(0)
+
+    def step():
+        rc = L.mwx_prosody_batch_device(ctx.ctx, st0, d_pcm.data_ptr(), d_desc.data_ptr(), n_seg,
+                                        frames, 16000, ctypes.byref(prm), d_out.data_ptr())
+        if rc != 0:
+            raise RuntimeError(f"mwx_prosody_batch_device rc={rc}")
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()  # the state's stream: mwx_perf_read below syncs it too
+    L.mwx_perf_read(st0, None, None)
+    L.mwx_perf_enable(st0, b"prosody")
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    tot_ms, nl = ctypes.c_double(), ctypes.c_int()
+    L.mwx_perf_read(st0, ctypes.byref(tot_ms), ctypes.byref(nl))  # synchronizes the stream
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    L.mwx_perf_enable(st0, None)
+    if dist is not None:
+        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    audio_s = world * clips * args.clip_seconds * args.steps
+    if rank == 0:
+        avg_s = tot_ms.value / 1e3 / max(1, nl.value)
+        work = 4 * int(desc[:, 1].sum())  # algorithmic: every sample read once
+        achieved = work / avg_s / 1e9
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = prosody_cpu_baseline(pcm, desc)
+        line = {
+            "metric": "segment_prosody_audio_seconds_per_second",
+            "value": round(audio_s / elapsed, 1),
+            "unit": "audio-sec/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (seeded 16 kHz PCM16 clips resident in HBM)",
+            "config": {"workload": f"extract_prosody over {n_seg} segments (1-8 s) of {clips} x "
+                                   f"{args.clip_seconds:g} s clips per GPU, one launch per step",
+                       "global_batch": world * n_seg, "seq_len": n_samp,
+                       "parallelism": f"dp{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None, "kernel": "prosody",
+                         "avg_launch_us": round(avg_s * 1e6, 2), "launches": nl.value,
+                         "work_per_launch": work,
+                         "work_desc": "4 B per PCM sample of every segment (read once)"},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def prosody_cpu_baseline(pcm, desc, budget_s=10.0):
+    """The reference's extract_prosody (oracle/_ref, compiled from its own
+    sources) — or, where that was not built, the oracle restatement — on one
+    core over the first segments until ~budget_s of CPU time."""
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    kind, fn = "port", None
+    ref = os.path.join(ROOT, "oracle", "_ref", "libref_prosody.so")
+    if os.path.exists(ref):
+        import make_prosody_golden as mpg
+        L = mpg.load_ref()
+        kind = "reference"
+        fn = lambda x: mpg.ref_prosody(L, x, 16000, (0.07, 170.0, 60.0, 500.0))  # noqa: E731
+    else:
+        import orc
+        fn = lambda x: orc.prosody(x)  # noqa: E731
+    done_s, t0, i = 0.0, time.perf_counter(), 0
+    while time.perf_counter() - t0 < budget_s and i < len(desc):
+        s0, n = int(desc[i, 0]), int(desc[i, 1])
+        fn(pcm[s0:s0 + n])
+        done_s += n / 16000.0
+        i += 1
+    el = time.perf_counter() - t0
+    return {"value": round(done_s / el, 1), "unit": "audio-sec/s", "cores": 1, "kind": kind,
+            "sample": f"first {i} segments ({done_s:.0f} s of audio), one thread"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -136,7 +281,11 @@ def main():
                     help="MX-fp8 compute for the encoder / cross-K/V GEMMs (C5)")
     ap.add_argument("--host-input", action="store_true",
                     help="PCM in host memory, uploaded inside each step (PCIe-inclusive rate)")
+    ap.add_argument("--prosody", action="store_true",
+                    help="segment-prosody leg (SURVEY.md §8 f4) instead of transcription")
     args = ap.parse_args()
+    if args.prosody:
+        return prosody_bench(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

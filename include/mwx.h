@@ -215,6 +215,60 @@ mwx_token_data mwx_full_get_token_data_from_state(struct mwx_state* state,
                                                   int i_segment, int i_token);
 int mwx_full_lang_id_from_state(struct mwx_state* state);
 
+/* --- segment prosody -----------------------------------------------------
+ * The reference's per-segment affect / speaker features
+ * (src/prosody_extractor.h:6-31 AffectiveTags, ProsodyOptions; computed by
+ * extract_prosody for every kept segment, src/stt_engine.cpp:313-337) on the
+ * GPU, bit-identical to the reference's CPU build. */
+typedef struct mwx_prosody_params { /* ProsodyOptions, same defaults */
+  float lpf_alpha;                  /* 0.07 */
+  float gender_threshold;           /* 170 Hz */
+  float min_pitch;                  /* 60 Hz */
+  float max_pitch;                  /* 500 Hz */
+} mwx_prosody_params;
+
+enum mwx_gender { MWX_GENDER_UNKNOWN = 0 /* "?" */, MWX_GENDER_M = 1, MWX_GENDER_F = 2 };
+enum mwx_emotion {
+  MWX_EMOTION_NEUTRAL = 0,
+  MWX_EMOTION_EXCITED = 1,
+  MWX_EMOTION_ANGRY = 2,
+  MWX_EMOTION_SAD = 3
+};
+
+typedef struct mwx_prosody { /* AffectiveTags */
+  float pitch_mean, pitch_std, energy_mean, energy_std, spectral_centroid,
+      zero_crossing_rate, arousal, valence;
+  float speaker_vec[8];
+  int gender;      /* enum mwx_gender (gender_proxy) */
+  int emotion;     /* enum mwx_emotion (emotion_proxy) */
+  int serial_runs; /* diagnostics: filter runs recomputed serially */
+  int reserved;
+} mwx_prosody;
+
+mwx_prosody_params mwx_prosody_default_params(void);
+
+/* Prosody of n_seg segments [seg_start[i], seg_start[i] + seg_len[i]) of one
+ * PCM buffer (host or device memory, n_pcm samples at sample_rate, 100 <=
+ * sample_rate <= 160000). A segment shorter than 160 samples gets the
+ * reference's empty-input result (extract_prosody(nullptr, 0, ...)). Runs on
+ * the state's stream; synchronous. 0 on success, <0 on bad arguments or a
+ * device error. */
+int mwx_prosody_batch(struct mwx_context* ctx, struct mwx_state* state, const float* pcm,
+                      int64_t n_pcm, const int64_t* seg_start, const int64_t* seg_len,
+                      int n_seg, int sample_rate, const mwx_prosody_params* params,
+                      mwx_prosody* out);
+
+/* As mwx_prosody_batch with every array in device memory (no host copies, no
+ * synchronization: the results are ready when the state's stream is). For
+ * throughput measurement over HBM-resident inputs. d_desc holds n_seg int64
+ * triples {start, len, frame_offset}: frame_offset = the sum of
+ * len / (sample_rate / 100) over the segments before it; total_frames = that
+ * sum over all n_seg. */
+int mwx_prosody_batch_device(struct mwx_context* ctx, struct mwx_state* state,
+                             const float* d_pcm, const int64_t* d_desc, int n_seg,
+                             int64_t total_frames, int sample_rate,
+                             const mwx_prosody_params* params, mwx_prosody* d_out);
+
 /* --- vocabulary / model ------------------------------------------------- */
 const char* mwx_token_to_str(struct mwx_context* ctx, mwx_token token);
 mwx_token mwx_token_eot(struct mwx_context* ctx);
@@ -245,7 +299,7 @@ void mwx_log_set(mwx_log_callback log_callback, void* user_data);
  * Times every launch of one kernel class with a pair of HIP events recorded on
  * the state's stream (the stream the kernels run on). Classes: "mel",
  * "enc_gemm", "enc_attn", "cross_gemm", "dec_gemm", "dec_attn_self",
- * "dec_attn_cross", "logits_gemm", "logits_proc". NULL disables.
+ * "dec_attn_cross", "logits_gemm", "logits_proc", "prosody". NULL disables.
  * mwx_perf_read synchronizes, returns the summed milliseconds and the launch
  * count since the last read, and resets them. */
 void mwx_perf_enable(struct mwx_state* state, const char* kernel_class);

@@ -79,6 +79,13 @@ def lib() -> C.CDLL:
     L.orc_full_n_windows.argtypes = [P]
     L.orc_full_window_tokens.restype = C.c_int
     L.orc_full_window_tokens.argtypes = [P, C.c_int, C.POINTER(C.c_int), C.c_int]
+    L.orc_prosody.restype = None
+    L.orc_prosody.argtypes = [fp, C.c_int64, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, P]
+    L.orc_clusterer_new.restype = P
+    L.orc_clusterer_new.argtypes = [C.c_float]
+    L.orc_clusterer_free.argtypes = [P]
+    L.orc_clusterer_assign.restype = C.c_int
+    L.orc_clusterer_assign.argtypes = [P, fp, C.c_int, C.c_char_p, C.c_int]
     _lib = L
     return L
 
@@ -290,3 +297,59 @@ class Oracle:
             windows.append(list(buf)[:n])
         L.orc_full_free(r)
         return rc.value, segs, lang, windows
+
+
+# ---------------------------------------------------------------------------
+# Segment prosody / speaker clustering (prosody_oracle.cpp; src/
+# prosody_extractor.cpp, src/speaker_cluster.cpp)
+# ---------------------------------------------------------------------------
+class ProsodyRec(C.Structure):
+    """mwx_prosody / AffectiveTags (gender 0 '?', 1 'M', 2 'F'; emotion 0
+    neutral, 1 excited, 2 angry, 3 sad)."""
+    _fields_ = [(n, C.c_float) for n in ("pitch_mean", "pitch_std", "energy_mean", "energy_std",
+                                         "spectral_centroid", "zero_crossing_rate", "arousal",
+                                         "valence")] + [
+        ("speaker_vec", C.c_float * 8), ("gender", C.c_int), ("emotion", C.c_int),
+        ("serial_runs", C.c_int), ("reserved", C.c_int)]
+
+
+PROSODY_FLOATS = ("pitch_mean", "pitch_std", "energy_mean", "energy_std", "spectral_centroid",
+                  "zero_crossing_rate", "arousal", "valence")
+
+
+def prosody_key(r) -> tuple:
+    """Everything the reference returns, as exact bit patterns (serial_runs,
+    a diagnostic, excluded)."""
+    f = [getattr(r, n) for n in PROSODY_FLOATS] + list(r.speaker_vec)
+    return tuple(np.array(f, np.float32).view(np.uint32).tolist()) + (r.gender, r.emotion)
+
+
+def prosody(pcm: Optional[np.ndarray], sample_rate: int = 16000, lpf_alpha: float = 0.07,
+            gender_threshold: float = 170.0, min_pitch: float = 60.0,
+            max_pitch: float = 500.0) -> ProsodyRec:
+    out = ProsodyRec()
+    if pcm is None:
+        lib().orc_prosody(None, 0, sample_rate, lpf_alpha, gender_threshold, min_pitch, max_pitch,
+                          C.byref(out))
+        return out
+    a = np.ascontiguousarray(pcm, np.float32)
+    lib().orc_prosody(_fp(a), len(a), sample_rate, lpf_alpha, gender_threshold, min_pitch,
+                      max_pitch, C.byref(out))
+    return out
+
+
+class Clusterer:
+    def __init__(self, threshold: float = 0.88):
+        self.h = lib().orc_clusterer_new(threshold)
+
+    def assign(self, vec) -> str:
+        a = np.ascontiguousarray(vec, np.float32)
+        buf = C.create_string_buffer(64)
+        lib().orc_clusterer_assign(self.h, _fp(a), len(a), buf, 64)
+        return buf.value.decode()
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_clusterer_free(self.h)
+            self.h = None
+

@@ -224,4 +224,25 @@ struct Draw {
 void sample_draws(const float* probs, const float* logprobs, int V, const double* u,
                   const int* ndraw, int KD, Draw* out, int* need, int R, hipStream_t st);
 
+// Segment prosody (k_prosody.hip): reference extract_prosody per segment.
+struct ProsodySeg {
+  long start;      // first sample in the clip
+  long len;        // samples
+  long frame_off;  // offset of the segment's frames in the scratch arrays
+};
+// same layout as mwx_prosody (include/mwx.h)
+struct ProsodyOut {
+  float pitch_mean, pitch_std, energy_mean, energy_std, spectral_centroid, zero_crossing_rate,
+      arousal, valence;
+  float speaker_vec[8];
+  int gender;   // 0 '?', 1 'M', 2 'F'
+  int emotion;  // 0 neutral, 1 excited, 2 angry, 3 sad
+  int serial_runs;
+  int pad;
+};
+// fstate: [sum frames] floats, feat: [sum frames] float4 (frames = len / frame)
+void prosody_launch(const float* pcm, const ProsodySeg* seg, int n_seg, float* fstate,
+                    float4* feat, ProsodyOut* out, int frame, int sample_rate, float alpha,
+                    float gender_thr, float min_pitch, float max_pitch, hipStream_t st);
+
 }  // namespace mwx

@@ -25,14 +25,29 @@ std::string hex(const std::string& s) {
 
 std::string to_json(const std::vector<TranscriptionResult>& rs) {
   std::string o = "[";
-  char buf[256];
+  char buf[1024];
   for (size_t i = 0; i < rs.size(); ++i) {
     const TranscriptionResult& r = rs[i];
     std::snprintf(buf, sizeof buf, "%s{\"prob\":%.9g,\"t0\":%lld,\"t1\":%lld,\"turn\":%d,\"n\":%d,",
                   i ? "," : "", r.prob, (long long)r.t0, (long long)r.t1, (int)r.speaker_turn_next,
                   r.token_count);
     o += buf;
-    o += "\"text\":\"" + hex(r.text) + "\",\"language\":\"" + hex(r.language) + "\",\"tokens\":[";
+    o += "\"text\":\"" + hex(r.text) + "\",\"language\":\"" + hex(r.language) + "\",";
+    const AffectiveTags& a = r.affective;
+    std::snprintf(buf, sizeof buf,
+                  "\"gender\":\"%s\",\"emotion\":\"%s\",\"speaker\":\"%s\",\"arousal\":%.9g,"
+                  "\"valence\":%.9g,\"pitch_mean\":%.9g,\"pitch_std\":%.9g,\"energy_mean\":%.9g,"
+                  "\"energy_std\":%.9g,\"spectral_centroid\":%.9g,\"zero_crossing_rate\":%.9g,",
+                  r.gender_proxy.c_str(), r.emotion_proxy.c_str(), r.speaker_id.c_str(), r.arousal,
+                  r.valence, a.pitch_mean, a.pitch_std, a.energy_mean, a.energy_std,
+                  a.spectral_centroid, a.zero_crossing_rate);
+    o += buf;
+    o += "\"speaker_vec\":[";
+    for (size_t j = 0; j < a.speaker_vec.size(); ++j) {
+      std::snprintf(buf, sizeof buf, "%s%.9g", j ? "," : "", a.speaker_vec[j]);
+      o += buf;
+    }
+    o += "],\"tokens\":[";
     for (size_t j = 0; j < r.tokens.size(); ++j) {
       const TokenData& t = r.tokens[j];
       std::snprintf(buf, sizeof buf, "%s{\"p\":%.9g,\"t0\":%lld,\"t1\":%lld,\"text\":\"", j ? "," : "",
@@ -100,6 +115,15 @@ void* mwx_stt_new_batched(const char* model_dir, const char* model_filename,
     std::fprintf(stderr, "SttEngine: %s\n", e.what());
     return nullptr;
   }
+}
+
+// SpeakerClusterer over n 8-D vectors in order: writes the ids, one per line.
+int mwx_stt_cluster_ids(const float* vecs, int n, float threshold, char* out, int cap) {
+  SpeakerClusterer c(threshold);
+  std::string o;
+  for (int i = 0; i < n; ++i)
+    o += c.assign_or_add(std::vector<float>(vecs + 8 * i, vecs + 8 * i + 8)) + "\n";
+  return emit(o, out, cap);
 }
 
 long mwx_stt_batches(void* eng) { return static_cast<SttEngine*>(eng)->batches_run(); }

@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 
 #include "text_filters.h"
@@ -23,7 +24,63 @@ double ms_between(std::chrono::steady_clock::time_point a, std::chrono::steady_c
 
 constexpr float kMinAvgTokenProb = 0.40f;  // src/stt_engine.cpp:264
 
+float cosine_sim(const std::vector<float>& a, const std::vector<float>& b) {
+  float dot = 0.0f, na = 0.0f, nb = 0.0f;  // one pass, in index order
+  for (size_t i = 0; i < a.size(); ++i) {
+    dot += a[i] * b[i];
+    na += a[i] * a[i];
+    nb += b[i] * b[i];
+  }
+  if (na == 0.0f || nb == 0.0f) return 0.0f;
+  return dot / (std::sqrt(na) * std::sqrt(nb));
+}
+
+AffectiveTags to_tags(const mwx_prosody& p) {
+  static const char* kGender[] = {"?", "M", "F"};
+  static const char* kEmotion[] = {"neutral", "excited", "angry", "sad"};
+  AffectiveTags t;
+  t.gender_proxy = kGender[p.gender];
+  t.emotion_proxy = kEmotion[p.emotion];
+  t.arousal = p.arousal;
+  t.valence = p.valence;
+  t.pitch_mean = p.pitch_mean;
+  t.pitch_std = p.pitch_std;
+  t.energy_mean = p.energy_mean;
+  t.energy_std = p.energy_std;
+  t.spectral_centroid = p.spectral_centroid;
+  t.zero_crossing_rate = p.zero_crossing_rate;
+  t.speaker_vec.assign(p.speaker_vec, p.speaker_vec + 8);
+  return t;
+}
+
 }  // namespace
+
+std::string SpeakerClusterer::assign_or_add(const std::vector<float>& vec) {
+  const Cluster* best = nullptr;
+  float best_sim = 0.0f;
+  for (const auto& kv : clusters_) {
+    const float sim = cosine_sim(vec, kv.second.centroid);
+    if (sim > best_sim) {
+      best_sim = sim;
+      best = &kv.second;
+    }
+  }
+  if (best && best_sim >= threshold_) {
+    Cluster& c = clusters_[best->id];
+    const size_t n = c.count;
+    for (size_t i = 0; i < c.centroid.size(); ++i)
+      c.centroid[i] = (c.centroid[i] * n + vec[i]) / (n + 1);
+    c.count = n + 1;
+    return c.id;
+  }
+  Cluster fresh;
+  fresh.id = "spk_" + std::to_string(next_id_++);
+  fresh.centroid = vec;
+  fresh.count = 1;
+  const std::string id = fresh.id;
+  clusters_[id] = std::move(fresh);
+  return id;
+}
 
 SttEngine::SttEngine(const Settings& settings) : settings_(settings) {
   const std::string path = settings_.model_dir + "/" + settings_.model_filename;
@@ -172,7 +229,15 @@ void SttEngine::batcher_loop(std::vector<mwx_state*> states) {
       r.ret = ret;
       r.t_start_ms = ms_between(r.t_enq, t0);
       r.t_proc_ms = ms_between(t0, t1);
-      if (ret == 0) r.results = collect(states[b], lang, r.pcm->size(), &r.token_count);
+      if (ret == 0) {
+        try {
+          r.results = collect(states[b], lang, r.pcm->data(), r.pcm->size(),
+                              r.options.prosody_opts, &r.token_count);
+        } catch (const std::exception& e) {
+          std::fprintf(stderr, "SttEngine: %s\n", e.what());
+          r.ret = -100;
+        }
+      }
     }
     {
       std::lock_guard<std::mutex> lock(q_mutex_);
@@ -245,8 +310,11 @@ mwx_full_params SttEngine::make_params(const RequestOptions& options, std::strin
 
 // Segment / token extraction and post-filters of src/stt_engine.cpp:258-337.
 std::vector<TranscriptionResult> SttEngine::collect(mwx_state* state, const std::string& lang,
-                                                    size_t pcm_size, int* token_count) const {
+                                                    const float* pcm, size_t pcm_size,
+                                                    const ProsodyOptions& popts,
+                                                    int* token_count) const {
   std::vector<TranscriptionResult> results;
+  std::vector<int64_t> seg_start, seg_len;
   const int eot = mwx_token_eot(ctx_);
   const int n_seg = mwx_full_n_segments_from_state(state);
   for (int i = 0; i < n_seg; ++i) {
@@ -271,13 +339,13 @@ std::vector<TranscriptionResult> SttEngine::collect(mwx_state* state, const std:
     if (token_count) *token_count += valid;
     const float avg = valid > 0 ? static_cast<float>(total_p / valid) : 0.0f;
     if (avg < kMinAvgTokenProb && valid > 0) continue;
-    // segment sample range (src/stt_engine.cpp:313-321): consumed by the
-    // prosody stage, which is out of scope; kept for the bounds behaviour
+    // segment sample range (src/stt_engine.cpp:313-321)
     int64_t s0 = static_cast<int64_t>((static_cast<double>(t0) / 100.0) * 16000.0);
     int64_t s1 = static_cast<int64_t>((static_cast<double>(t1) / 100.0) * 16000.0);
     s0 = std::max<int64_t>(0, std::min<int64_t>(s0, (int64_t)pcm_size));
     s1 = std::max<int64_t>(s0, std::min<int64_t>(s1, (int64_t)pcm_size));
-    (void)s1;
+    seg_start.push_back(s0);
+    seg_len.push_back(s1 - s0);
     TranscriptionResult r;
     r.text = text;
     r.language = lang;
@@ -287,10 +355,31 @@ std::vector<TranscriptionResult> SttEngine::collect(mwx_state* state, const std:
     r.speaker_turn_next = turn;
     r.tokens = std::move(tokens);
     r.token_count = valid;
-    r.gender_proxy = "unknown";
-    r.emotion_proxy = "neutral";
-    r.speaker_id = "?";
     results.push_back(std::move(r));
+  }
+  // prosody of every kept segment in one GPU launch, then speaker clustering
+  // in segment order (src/stt_engine.cpp:323-337); segments shorter than 160
+  // samples get the empty-input tags and speaker "?"
+  std::vector<mwx_prosody> pros(results.size());
+  if (!results.empty()) {
+    mwx_prosody_params pp;
+    pp.lpf_alpha = popts.lpf_alpha;
+    pp.gender_threshold = popts.gender_threshold;
+    pp.min_pitch = popts.min_pitch;
+    pp.max_pitch = popts.max_pitch;
+    const int rc = mwx_prosody_batch(ctx_, state, pcm, (int64_t)pcm_size, seg_start.data(),
+                                     seg_len.data(), (int)results.size(), 16000, &pp, pros.data());
+    if (rc != 0) throw std::runtime_error("mwx_prosody_batch failed");
+  }
+  SpeakerClusterer clusterer(settings_.cluster_threshold);
+  for (size_t i = 0; i < results.size(); ++i) {
+    TranscriptionResult& r = results[i];
+    r.affective = to_tags(pros[i]);
+    r.gender_proxy = r.affective.gender_proxy;
+    r.emotion_proxy = r.affective.emotion_proxy;
+    r.arousal = r.affective.arousal;
+    r.valence = r.affective.valence;
+    r.speaker_id = seg_len[i] < 160 ? "?" : clusterer.assign_or_add(r.affective.speaker_vec);
   }
   return results;
 }
@@ -326,7 +415,8 @@ std::vector<TranscriptionResult> SttEngine::transcribe(const std::vector<float>&
                  ret);
     return {};
   }
-  return collect(state, lang, pcm_size, out_metrics ? &out_metrics->token_count : nullptr);
+  return collect(state, lang, pcmf32.data(), pcm_size, options.prosody_opts,
+                 out_metrics ? &out_metrics->token_count : nullptr);
 }
 
 std::vector<std::vector<TranscriptionResult>> SttEngine::transcribe_batch(
@@ -354,7 +444,9 @@ std::vector<std::vector<TranscriptionResult>> SttEngine::transcribe_batch(
   if (ret == 0) {
     const size_t min_samples = static_cast<size_t>((settings_.vad_ms_min_duration * 16000) / 1000);
     for (size_t b = 0; b < clips.size(); ++b)
-      if (clips[b].size() >= min_samples) out[b] = collect(states[b], lang, clips[b].size(), nullptr);
+      if (clips[b].size() >= min_samples)
+        out[b] = collect(states[b], lang, clips[b].data(), clips[b].size(), options.prosody_opts,
+                         nullptr);
   }
   for (mwx_state* s : states) mwx_free_state(s);
   return out;

@@ -7,9 +7,11 @@
 // (:204-212), the whisper_full parameter mapping (:214-243), the too-short
 // audio gate (:153-167), and the result post-filters (:261-311: hallucination
 // phrases, tokens with id >= eot skipped, average token p < 0.40 drops the
-// segment). Out of scope: VAD, resampling (non-16 kHz input is
-// passed through, as the reference does when libsamplerate fails, :141),
-// prosody and speaker clustering (their result fields keep neutral values).
+// segment), per-segment prosody (src/stt_engine.cpp:313-337: computed on the
+// GPU by mwx_prosody_batch, bit-identical to src/prosody_extractor.cpp) and
+// speaker clustering (src/speaker_cluster.cpp, restated below). Out of scope
+// (SURVEY.md §8): VAD and resampling (non-16 kHz input is passed through, as
+// the reference does when libsamplerate fails, :141).
 #pragma once
 
 #include <atomic>
@@ -24,6 +26,7 @@
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "mwx.h"
@@ -50,6 +53,7 @@ struct Settings {
   bool suppress_nst = true;
   int gpu_device = 0;
   int stream_buffer_samples = 8000;
+  float cluster_threshold = 0.88f;  // src/config.h:71
   // Engine extension (no reference counterpart): dynamic request batching.
   // max_batch > 1: concurrent transcribe() calls with the same decoding
   // options are gathered (up to max_batch, waiting at most batch_window_us
@@ -67,6 +71,50 @@ struct TokenData {
   int64_t t1;
 };
 
+// src/prosody_extractor.h:6-27
+struct AffectiveTags {
+  std::string gender_proxy;   // "M" / "F" / "?"
+  std::string emotion_proxy;  // "excited" | "neutral" | "sad" | "angry"
+  float arousal = 0.0f;
+  float valence = 0.0f;
+  float pitch_mean = 0.0f;
+  float pitch_std = 0.0f;
+  float energy_mean = 0.0f;
+  float energy_std = 0.0f;
+  float spectral_centroid = 0.0f;
+  float zero_crossing_rate = 0.0f;
+  std::vector<float> speaker_vec;  // 8-D
+};
+
+struct ProsodyOptions {
+  float lpf_alpha = 0.07f;
+  float gender_threshold = 170.0f;
+  float min_pitch = 60.0f;
+  float max_pitch = 500.0f;
+};
+
+// Online speaker clustering of segment speaker vectors (the reference's
+// SpeakerClusterer, src/speaker_cluster.h:45-66 / .cpp:5-40): each vector
+// joins the cluster of highest cosine similarity if that is >= threshold
+// (running-mean centroid), else opens "spk_<n>". Clusters live in an
+// std::unordered_map keyed by id, scanned in the map's order with ties kept
+// by the first — the same container as the reference, hence the same order.
+class SpeakerClusterer {
+ public:
+  explicit SpeakerClusterer(float threshold = 0.88f) : threshold_(threshold) {}
+  std::string assign_or_add(const std::vector<float>& vec);
+
+ private:
+  struct Cluster {
+    std::string id;
+    std::vector<float> centroid;
+    size_t count = 0;
+  };
+  float threshold_;
+  std::unordered_map<std::string, Cluster> clusters_;
+  int next_id_ = 0;
+};
+
 struct RequestOptions {
   std::string language;
   std::string prompt;
@@ -75,6 +123,7 @@ struct RequestOptions {
   float temperature = -1.0f;
   int beam_size = -1;
   int best_of = -1;
+  ProsodyOptions prosody_opts;
   std::function<bool()> should_abort = nullptr;
 };
 
@@ -91,6 +140,7 @@ struct TranscriptionResult {
   std::string emotion_proxy;
   float arousal = 0.0f;
   float valence = 0.0f;
+  AffectiveTags affective;
   std::string speaker_id;
 };
 
@@ -163,7 +213,8 @@ class SttEngine {
   mwx_full_params make_params(const RequestOptions& options, std::string& target_lang,
                               std::function<bool()>& abort_fn) const;
   std::vector<TranscriptionResult> collect(mwx_state* state, const std::string& lang,
-                                           size_t pcm_size, int* token_count) const;
+                                           const float* pcm, size_t pcm_size,
+                                           const ProsodyOptions& popts, int* token_count) const;
 
   Settings settings_;
   mwx_context* ctx_ = nullptr;

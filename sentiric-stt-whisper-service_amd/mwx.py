@@ -87,6 +87,30 @@ class FullParams(C.Structure):
     ]
 
 
+class ProsodyParams(C.Structure):
+    """mwx_prosody_params = the reference's ProsodyOptions
+    (src/prosody_extractor.h:21-27)."""
+    _fields_ = [("lpf_alpha", C.c_float), ("gender_threshold", C.c_float),
+                ("min_pitch", C.c_float), ("max_pitch", C.c_float)]
+
+
+class Prosody(C.Structure):
+    """mwx_prosody = AffectiveTags (src/prosody_extractor.h:6-18)."""
+    _fields_ = [(n, C.c_float) for n in ("pitch_mean", "pitch_std", "energy_mean", "energy_std",
+                                         "spectral_centroid", "zero_crossing_rate", "arousal",
+                                         "valence")] + [
+        ("speaker_vec", C.c_float * 8), ("gender", C.c_int), ("emotion", C.c_int),
+        ("serial_runs", C.c_int), ("reserved", C.c_int)]
+
+    @property
+    def gender_proxy(self) -> str:
+        return ("?", "M", "F")[self.gender]
+
+    @property
+    def emotion_proxy(self) -> str:
+        return ("neutral", "excited", "angry", "sad")[self.emotion]
+
+
 _lib = None
 
 
@@ -165,6 +189,15 @@ def lib() -> C.CDLL:
     L.mwx_test_decode.argtypes = [P, P, C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_float)]
     L.mwx_test_decode_last.restype = C.c_int
     L.mwx_test_decode_last.argtypes = [P, P, C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_float)]
+    L.mwx_prosody_default_params.restype = ProsodyParams
+    L.mwx_prosody_default_params.argtypes = []
+    i64p = C.POINTER(C.c_int64)
+    L.mwx_prosody_batch.restype = C.c_int
+    L.mwx_prosody_batch.argtypes = [P, P, fpp, C.c_int64, i64p, i64p, C.c_int, C.c_int,
+                                    C.POINTER(ProsodyParams), C.POINTER(Prosody)]
+    L.mwx_prosody_batch_device.restype = C.c_int
+    L.mwx_prosody_batch_device.argtypes = [P, P, C.c_void_p, C.c_void_p, C.c_int, C.c_int64,
+                                           C.c_int, C.POINTER(ProsodyParams), C.c_void_p]
     _lib = L
     return L
 
@@ -351,6 +384,27 @@ class Context:
         if r != n_len:
             raise RuntimeError(f"mwx_test_mel returned {r}")
         return out
+
+    def prosody_batch(self, pcm: np.ndarray, starts, lens, sample_rate: int = 16000,
+                      params: Optional[ProsodyParams] = None, state_index: int = 0):
+        """mwx_prosody_batch: prosody of segments [starts[i], starts[i] + lens[i])
+        of pcm (a numpy f32 array or a DevicePCM)."""
+        st = np.ascontiguousarray(starts, np.int64)
+        ln = np.ascontiguousarray(lens, np.int64)
+        out = (Prosody * max(1, len(st)))()
+        if isinstance(pcm, DevicePCM):
+            ptr, n = pcm.ptr, pcm.n
+        else:
+            a = np.ascontiguousarray(pcm, np.float32)
+            ptr, n = fptr(a), len(a)
+        p = params if params is not None else lib().mwx_prosody_default_params()
+        rc = lib().mwx_prosody_batch(self.ctx, self.state(state_index), ptr, n,
+                                     st.ctypes.data_as(C.POINTER(C.c_int64)),
+                                     ln.ctypes.data_as(C.POINTER(C.c_int64)), len(st),
+                                     sample_rate, C.byref(p), out)
+        if rc != 0:
+            raise RuntimeError(f"mwx_prosody_batch failed ({rc})")
+        return list(out)[:len(st)]
 
     def test_gemm_mx(self, a: np.ndarray, w: np.ndarray) -> np.ndarray:
         """c = MX-fp8(bf16(a)) @ MX-fp8(bf16(w))^T on the block-scaled fp8 MFMA."""

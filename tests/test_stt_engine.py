@@ -65,7 +65,8 @@ def test_is_hallucination_matches_restatement():
 def test_library_exports():
     L = lib()
     for name in ("mwx_stt_is_hallucination", "mwx_stt_new", "mwx_stt_free",
-                 "mwx_stt_transcribe_pcm16", "mwx_stt_new_batched", "mwx_stt_batches"):
+                 "mwx_stt_transcribe_pcm16", "mwx_stt_new_batched", "mwx_stt_batches",
+                 "mwx_stt_cluster_ids"):
         assert hasattr(L, name)
 
 
@@ -79,6 +80,26 @@ def _transcribe(L, eng, pcm16, lang=b"en", beam=1, temp=-1.0):
     if r < 0:
         return r, None, list(m)
     return r, json.loads(buf.value.decode()), list(m)
+
+
+def check_prosody(res, pcm):
+    """Segment affect fields and speaker ids (src/stt_engine.cpp:313-337):
+    bit-exact against the oracle's prosody of each segment's sample range and
+    its clusterer run over the kept segments in order."""
+    import orc
+    clus = orc.Clusterer(0.88)
+    for g in res:
+        s0 = max(0, min(int((g["t0"] / 100.0) * 16000.0), len(pcm)))
+        s1 = max(s0, min(int((g["t1"] / 100.0) * 16000.0), len(pcm)))
+        w = orc.prosody(pcm[s0:s1] if s1 - s0 >= 160 else None)
+        assert g["gender"] == ("?", "M", "F")[w.gender]
+        assert g["emotion"] == ("neutral", "excited", "angry", "sad")[w.emotion]
+        for n in orc.PROSODY_FLOATS:
+            assert np.float32(g[n]) == np.float32(getattr(w, n)), n
+        assert np.array_equal(np.array(g["speaker_vec"], np.float32),
+                              np.array(list(w.speaker_vec), np.float32))
+        want_spk = clus.assign(np.array(list(w.speaker_vec), np.float32)) if s1 - s0 >= 160 else "?"
+        assert g["speaker"] == want_spk
 
 
 @pytest.mark.gpu
@@ -118,6 +139,7 @@ def test_transcribe_pcm16_matches_oracle(tmp_path):
                     assert (gt["t0"], gt["t1"]) == (wt[2], wt[3])
                 assert abs(g["prob"] - w["prob"]) < 5e-3
                 assert bytes.fromhex(g["language"]) == b"en"
+            check_prosody(res, mwx.pcm16_to_f32(pcm16))
             assert metrics[2] >= sum(len(w["tokens"]) for w in want)
         # too-short audio gate (src/stt_engine.cpp:153-167): < 500 ms -> no results
         eng = L.mwx_stt_new(str(tmp_path).encode(), b"ggml-micro.bin", 1, 5000, 1, b"auto", 500, 0)
