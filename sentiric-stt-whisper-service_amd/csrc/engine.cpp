@@ -130,7 +130,7 @@ struct State {
   DBuf energy;
   DBuf aq, as;  // MX-fp8 activations (codes [rows][K], scales [rows][K/32])
   DBuf ibuf;  // small int arrays (slot maps)
-  DBuf pro_pcm, pro_desc, pro_fs, pro_ft, pro_out;  // segment prosody
+  DBuf pro_pcm, pro_desc, pro_fs, pro_ft, pro_fc, pro_out;  // segment prosody
   // decoder workspace (row-batched)
   DBuf xd, hd, qd, od, ffd, logits, kself, vself, stepin, ctl, tokout, probs, logprobs, smask;
   DBuf pqkv, pres, pq;  // split-K partial slabs of the decode GEMMs

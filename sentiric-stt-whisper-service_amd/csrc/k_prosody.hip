@@ -10,16 +10,19 @@
 // order-dependent in float and are restated so the GPU can run them wide
 // without changing a bit:
 //  * the one-pole low-pass y += a * (x - y) runs across the whole segment.
-//    Each thread takes a run of frames, warms the filter up over the W samples
-//    before its run from a guessed state, and records the state it reaches at
-//    each of its frame starts. The filter is a contraction, so the guessed and
-//    true trajectories meet exactly (same float) within the warm-up; whether
-//    they met is CHECKED — thread t's state at its first frame must equal
-//    thread t-1's exact end state, bit for bit — and a run that fails the
-//    check is recomputed serially from the exact state. The serial pass is
-//    therefore the fallback, never an approximation.
+//    Each thread takes a run of >= 2 frames, warms the filter up over the W
+//    samples before its run from a guessed state, and computes its frames'
+//    features on its own trajectory. The filter is a contraction, so the
+//    guessed and true trajectories meet exactly (same float) within the
+//    warm-up; whether they met is CHECKED — thread t's state at its first
+//    frame must equal thread t-1's exact end state, bit for bit — and a run
+//    that fails the check is recomputed serially from the exact state (up to
+//    the frame where it meets its own trajectory). The serial pass is the
+//    fallback, never an approximation.
 //  * per-frame sums (energy, spectral centroid, crossings) are sequential
-//    over the frame's samples, one thread per frame — as the reference.
+//    over the frame's samples, inside the run that owns the frame — as the
+//    reference. Each lane streams its own samples through registers, 32 per
+//    block, the next block in flight.
 //  * segment means / deviations accumulate over frames in frame order: one
 //    wave per statistic, a wave-uniform chain fed 64 frames at a time by
 //    v_readlane (coalesced loads, the adds stay in the reference's order).
@@ -69,32 +72,123 @@ __device__ __forceinline__ float sqrt_rn(float x) {
 
 __device__ __forceinline__ float lpf_step(float y, float x, float a) { return y + a * (x - y); }
 
-// Streams p[0..n) through registers in blocks of 32 (eight 16-byte loads in
-// flight per lane, each lane on its own run of samples) and calls fn on every
-// sample in order: a lane's 128-byte lines are consumed whole from registers
-// instead of being re-fetched sample by sample through L1.
+// Streams p[0..n) through registers in blocks of SB samples (each lane on
+// its own run of samples, 16-byte loads) and calls fn on every sample in
+// order. Double-buffered: block i+1 is in flight while block i is consumed,
+// so a lane's serial chain does not wait a full memory latency per block.
+constexpr int SB = 32;
+
+__device__ __forceinline__ void load_blk(const float* __restrict__ p, float (&v)[SB]) {
+#pragma unroll
+  for (int q = 0; q < SB; q += 4) {
+    float4 t;
+    __builtin_memcpy(&t, p + q, 16);
+    v[q] = t.x;
+    v[q + 1] = t.y;
+    v[q + 2] = t.z;
+    v[q + 3] = t.w;
+  }
+}
+
 template <class Fn>
 __device__ __forceinline__ void stream(const float* __restrict__ p, long n, Fn&& fn) {
+  const long nb = n / SB;
+  float a[SB], b[SB];
+  if (nb > 0) load_blk(p, a);
   long i = 0;
-  for (; i + 32 <= n; i += 32) {
-    float v[32];
+  for (; i + 2 <= nb; i += 2) {
+    load_blk(p + (i + 1) * SB, b);
 #pragma unroll
-    for (int q = 0; q < 32; q += 4) {
-      float4 t;
-      __builtin_memcpy(&t, p + i + q, 16);
-      v[q] = t.x;
-      v[q + 1] = t.y;
-      v[q + 2] = t.z;
-      v[q + 3] = t.w;
-    }
+    for (int q = 0; q < SB; ++q) fn(a[q]);
+    if (i + 2 < nb) load_blk(p + (i + 2) * SB, a);
 #pragma unroll
-    for (int q = 0; q < 32; ++q) fn(v[q]);
+    for (int q = 0; q < SB; ++q) fn(b[q]);
   }
-  for (; i < n; ++i) fn(p[i]);
+  if (i < nb) {
+#pragma unroll
+    for (int q = 0; q < SB; ++q) fn(a[q]);
+  }
+  long j = nb * SB;
+  for (; j + 4 <= n; j += 4) {
+    float4 t;
+    __builtin_memcpy(&t, p + j, 16);
+    fn(t.x);
+    fn(t.y);
+    fn(t.z);
+    fn(t.w);
+  }
+  for (; j < n; ++j) fn(p[j]);
 }
 
 __device__ __forceinline__ float readlane_f(float v, int lane) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+// Calls fn(lane 0's v), fn(lane 1's v), ... fn(lane m-1's v) in order on
+// every lane (a wave-uniform sequential chain); a full block of 64 is
+// unrolled so the lane reads are constant-indexed and issue ahead of the adds.
+template <class Fn>
+__device__ __forceinline__ void chain(float v, int m, Fn&& fn) {
+  if (m == 64) {
+#pragma unroll
+    for (int i = 0; i < 64; ++i) fn(readlane_f(v, i));
+  } else {
+    for (int i = 0; i < m; ++i) fn(readlane_f(v, i));
+  }
+}
+
+// Everything the reference computes inside its frame loop for one frame
+// (src/prosody_extractor.cpp:64-127) given the low-pass state y on entry;
+// y leaves as the state after the frame. Raw-sample sums first (they set the
+// hysteresis threshold), then the low-passed pass re-reads the frame (now in
+// cache). Writes {rms, zcr, centroid, f0 or -1} and the packed word
+// cycles | voiced << 16 | silent << 17.
+__device__ __forceinline__ void frame_features(const float* __restrict__ xf, int F, float& y,
+                                               float alpha, float duration, float min_pitch,
+                                               float max_pitch, float4* ftf, int* fcf) {
+  float prev = xf[0];
+  float r0 = prev * prev, power = 0.0f, weighted = 0.0f, kf = 0.0f;
+  unsigned any = __float_as_uint(prev);
+  stream(xf + 1, F - 1, [&](float v) {
+    r0 += v * v;
+    kf += 1.0f;  // exact: k < 2^24
+    const float d = fabsf(v - prev);
+    weighted += d * kf;
+    power += d;
+    prev = v;
+    any |= __float_as_uint(v);
+  });
+  const float rms = sqrt_rn(__fdiv_rn(r0, (float)F));
+  const float clip = fmax_ref(0.002f, rms * 0.15f);
+  // low-passed crossings and the hysteresis cycle counter: `pos` = the last
+  // sample beyond +-clip was above +clip; a later one below -clip is a cycle
+  // (the reference's is_positive / initialized pair: before any sample
+  // leaves the band nothing counts, and pos starts false)
+  y = lpf_step(y, xf[0], alpha);
+  bool yneg = !(y >= 0.0f);
+  bool pos = false;
+  int cycles = 0, zc = 0;
+  stream(xf + 1, F - 1, [&](float v) {
+    y = lpf_step(y, v, alpha);
+    const bool neg = !(y >= 0.0f);
+    zc += neg != yneg;
+    yneg = neg;
+    const bool up = y > clip, dn = y < -clip;
+    cycles += pos & dn;
+    pos = up | (pos & !dn);
+  });
+  float f0v = -1.0f;
+  int voiced = 0;
+  if (rms > 0.015f && cycles > 0) {
+    const float e = __fdiv_rn((float)cycles, duration);
+    if (e >= min_pitch && e <= max_pitch) {
+      f0v = e;
+      voiced = 1;
+    }
+  }
+  *ftf = make_float4(rms, __fdiv_rn((float)zc, (float)F),
+                     power > 0.0f ? __fdiv_rn(weighted, power) : 0.0f, f0v);
+  *fcf = (voiced ? cycles : 0) | voiced << 16 | (any == 0) << 17;
 }
 
 }  // namespace
@@ -104,7 +198,8 @@ __device__ __forceinline__ float readlane_f(float v, int lane) {
 __global__ __launch_bounds__(PT) void prosody_kernel(const float* __restrict__ pcm,
                                                      const ProsodySeg* __restrict__ seg,
                                                      float* __restrict__ fstate,
-                                                     float4* __restrict__ feat, ProsodyOut* out,
+                                                     float4* __restrict__ feat,
+                                                     int* __restrict__ fcyc, ProsodyOut* out,
                                                      int F, int sample_rate, float alpha,
                                                      float gender_thr, float min_pitch,
                                                      float max_pitch, int warm) {
@@ -112,6 +207,7 @@ __global__ __launch_bounds__(PT) void prosody_kernel(const float* __restrict__ p
   __shared__ int s_hist[PMAX_HALF];
   __shared__ float s_stat[8];
   __shared__ int s_cnt[2];
+  __shared__ int s_first;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const ProsodySeg sg = seg[blockIdx.x];
   ProsodyOut& o = out[blockIdx.x];
@@ -128,38 +224,47 @@ __global__ __launch_bounds__(PT) void prosody_kernel(const float* __restrict__ p
   const long nfr = (long)((unsigned)n / (unsigned)F);  // frames i + F <= n (n < 2^31: host-checked)
   float* fs = fstate + sg.frame_off;
   float4* ft = feat + sg.frame_off;
-  // phase-1 silence flags live in the feature slots until phase 2 fills them
-  int* zf = reinterpret_cast<int*>(ft);
+  int* fc = fcyc + sg.frame_off;
 
-  // ---- 1. low-pass states at every frame start (speculative, checked) ----
-  const long fpt = (nfr + PT - 1) / PT;
+  // ---- 1+2. one streaming pass: low-pass runs + per-frame features ----
+  // Run t owns frames [f0, f1) (at least 2 frames per run so the warm-up is
+  // amortized), warms its filter up over the `warm` samples before them from
+  // a guessed state, and computes those frames' features on its own
+  // trajectory. Runs whose start state misses the exact one are recomputed
+  // serially below.
+  const float duration = __fdiv_rn((float)F, (float)sample_rate);
+  long fpt = (nfr + PT - 1) / PT;
+  if (fpt < 2) fpt = 2;
   const long f0 = (long)t * fpt, f1 = f0 + fpt < nfr ? f0 + fpt : nfr;
   float y_end = 0.0f, y_spec = 0.0f;
   if (f0 < f1) {
     const long j0 = f0 * F;
     long w0 = j0 - warm;
     if (w0 < 0) w0 = 0;
-    float y = t == 0 ? 0.0f : x[w0];  // thread 0 starts from the true state
+    float y = t == 0 ? 0.0f : x[w0];  // run 0 starts from the true state
     stream(x + w0, j0 - w0, [&](float v) { y = lpf_step(y, v, alpha); });
     y_spec = y;
     for (long f = f0; f < f1; ++f) {
       fs[f] = y;
-      unsigned any = 0;
-      stream(x + f * F, F, [&](float v) {
-        any |= __float_as_uint(v);
-        y = lpf_step(y, v, alpha);
-      });
-      zf[f] = any == 0;  // digital-silence frame (all +0.0)
+      frame_features(x + f * F, F, y, alpha, duration, min_pitch, max_pitch, ft + f, fc + f);
     }
     y_end = y;
   }
   s_spec[t] = y_spec;
   s_end[t] = y_end;
+  if (t == 0) s_first = PT;
+  for (int i = t; i < PMAX_HALF; i += PT) s_hist[i] = 0;
   __syncthreads();
+  // every run checks its start against its neighbour's end in parallel; the
+  // serial pass starts at the first run that missed (none, usually)
+  const bool miss = t > 0 && f0 < f1 && __float_as_uint(y_spec) != __float_as_uint(s_end[t - 1]);
+  if (miss) atomicMin(&s_first, t);
+  const bool any_miss = __syncthreads_or(miss);
   int redo = 0;
-  if (t == 0) {
-    float prev = s_end[0];
-    for (int u = 1; u < PT; ++u) {
+  if (t == 0 && any_miss) {
+    const int u0 = s_first;
+    float prev = s_end[u0 - 1];
+    for (int u = u0; u < PT; ++u) {
       const long g0 = (long)u * fpt, g1 = g0 + fpt < nfr ? g0 + fpt : nfr;
       if (g0 >= g1) break;
       if (__float_as_uint(s_spec[u]) == __float_as_uint(prev)) {
@@ -181,132 +286,84 @@ __global__ __launch_bounds__(PT) void prosody_kernel(const float* __restrict__ p
           break;
         }
         fs[f] = y;
-        if (zf[f] && __float_as_uint(lpf_step(y, 0.0f, alpha)) == __float_as_uint(y)) continue;
-        const float* xf = x + f * F;
-        for (int k = 0; k < F; ++k) y = lpf_step(y, xf[k], alpha);
+        if (((fc[f] >> 17) & 1) &&
+            __float_as_uint(lpf_step(y, 0.0f, alpha)) == __float_as_uint(y)) {
+          // silent frame at a fixed point (|y| tiny): the filter output is
+          // the constant y, so no crossings and no cycles; rms and centroid 0
+          ft[f] = make_float4(0.0f, 0.0f, 0.0f, -1.0f);
+          fc[f] = 1 << 17;
+          continue;
+        }
+        frame_features(x + f * F, F, y, alpha, duration, min_pitch, max_pitch, ft + f, fc + f);
       }
       prev = met ? s_end[u] : y;
     }
   }
-  for (int i = t; i < PMAX_HALF; i += PT) s_hist[i] = 0;
   __syncthreads();
-
-  // ---- 2. per-frame features (src/prosody_extractor.cpp:63-128) ----
-  const float duration = __fdiv_rn((float)F, (float)sample_rate);
   for (long f = t; f < nfr; f += PT) {
-    const float* xf = x + f * F;
-    // energy and spectral-centroid sums (raw samples), in sample order
-    float r0 = 0.0f, power = 0.0f, weighted = 0.0f, prev = 0.0f;
-    int k = 0;
-    stream(xf, F, [&](float v) {
-      r0 += v * v;
-      if (k > 0) {
-        const float d = fabsf(v - prev);
-        weighted += d * (float)k;
-        power += d;
-      }
-      prev = v;
-      ++k;
-    });
-    const float rms = sqrt_rn(__fdiv_rn(r0, (float)F));
-    const float clip = fmax_ref(0.002f, rms * 0.15f);
-    // low-passed crossings and the hysteresis cycle counter (state 0: not
-    // yet armed, 1: positive, 2: negative; a 1 -> 2 move is one cycle)
-    float y = fs[f], yp = 0.0f;
-    int cycles = 0, zc = 0, sm = 0;
-    k = 0;
-    stream(xf, F, [&](float v) {
-      y = lpf_step(y, v, alpha);
-      if (k > 0) {
-        zc += (y >= 0.0f) != (yp >= 0.0f);
-        const bool up = y > clip, dn = y < -clip;
-        cycles += (sm == 1) & dn;
-        sm = up ? 1 : (dn ? 2 : sm);
-      }
-      yp = y;
-      ++k;
-    });
-    float f0v = -1.0f;
-    if (rms > 0.015f && cycles > 0) {
-      const float e = __fdiv_rn((float)cycles, duration);
-      if (e >= min_pitch && e <= max_pitch) {
-        f0v = e;
-        atomicAdd(&s_hist[cycles], 1);
-      }
-    }
-    ft[f] = make_float4(rms, __fdiv_rn((float)zc, (float)F),
-                        power > 0.0f ? __fdiv_rn(weighted, power) : 0.0f, f0v);
+    const int w = fc[f];
+    if (w & (1 << 16)) atomicAdd(&s_hist[w & 0xFFFF], 1);
   }
   __syncthreads();
 
-  // ---- 3. segment statistics, each in frame order (one wave per chain) ----
+  // ---- 3. segment statistics, each in frame order (src/prosody_extractor.cpp:9-18,
+  // 130-135): one wave per chain, 64 frames per coalesced load
   if (wave == 0) {  // f0: mean and deviation over the voiced frames
-    float s = 0.0f;
+    float sf = 0.0f;
     int cnt = 0;
     for (long b = 0; b < nfr; b += 64) {
       const float v = b + lane < nfr ? ft[b + lane].w : -1.0f;
-      const int m = (int)(nfr - b < 64 ? nfr - b : 64);
-      for (int i = 0; i < m; ++i) {
-        const float e = readlane_f(v, i);
+      chain(v, (int)(nfr - b < 64 ? nfr - b : 64), [&](float e) {
         if (e >= 0.0f) {
-          s += e;
+          sf += e;
           ++cnt;
         }
-      }
+      });
     }
-    float acc = 0.0f, mean = 0.0f;
+    float af = 0.0f;
     if (cnt > 0) {
-      mean = __fdiv_rn(s, (float)cnt);
+      const float mf = __fdiv_rn(sf, (float)cnt);
       for (long b = 0; b < nfr; b += 64) {
         const float v = b + lane < nfr ? ft[b + lane].w : -1.0f;
-        const int m = (int)(nfr - b < 64 ? nfr - b : 64);
-        for (int i = 0; i < m; ++i) {
-          const float e = readlane_f(v, i);
-          if (e >= 0.0f) acc += (e - mean) * (e - mean);
-        }
+        chain(v, (int)(nfr - b < 64 ? nfr - b : 64), [&](float e) {
+          if (e >= 0.0f) af += (e - mf) * (e - mf);
+        });
       }
     }
     if (lane == 0) {
-      s_stat[0] = cnt > 0 ? sqrt_rn(__fdiv_rn(acc, (float)cnt)) : 0.0f;  // pitch_std
+      s_stat[0] = cnt > 0 ? sqrt_rn(__fdiv_rn(af, (float)cnt)) : 0.0f;  // pitch_std
       s_cnt[0] = cnt;
     }
   } else if (wave == 1) {  // energy: mean, deviation, onsets
-    float s = 0.0f, last = 0.0f;
+    float sr = 0.0f, last = 0.0f;
     int peaks = 0;
     for (long b = 0; b < nfr; b += 64) {
       const float v = b + lane < nfr ? ft[b + lane].x : 0.0f;
-      const int m = (int)(nfr - b < 64 ? nfr - b : 64);
-      for (int i = 0; i < m; ++i) {
-        const float r = readlane_f(v, i);
-        s += r;
+      chain(v, (int)(nfr - b < 64 ? nfr - b : 64), [&](float r) {
+        sr += r;
         if (r > 0.05f && last <= 0.05f) ++peaks;
         last = r;
-      }
+      });
     }
-    const float mean = __fdiv_rn(s, (float)nfr);
-    float acc = 0.0f;
+    const float mr = __fdiv_rn(sr, (float)nfr);
+    float ar = 0.0f;
     for (long b = 0; b < nfr; b += 64) {
       const float v = b + lane < nfr ? ft[b + lane].x : 0.0f;
-      const int m = (int)(nfr - b < 64 ? nfr - b : 64);
-      for (int i = 0; i < m; ++i) {
-        const float r = readlane_f(v, i);
-        acc += (r - mean) * (r - mean);
-      }
+      chain(v, (int)(nfr - b < 64 ? nfr - b : 64), [&](float r) { ar += (r - mr) * (r - mr); });
     }
     if (lane == 0) {
-      s_stat[1] = mean;
-      s_stat[2] = sqrt_rn(__fdiv_rn(acc, (float)nfr));
+      s_stat[1] = mr;
+      s_stat[2] = sqrt_rn(__fdiv_rn(ar, (float)nfr));
       s_cnt[1] = peaks;
     }
   } else {  // waves 2 / 3: spectral centroid / zero-crossing-rate means
-    float s = 0.0f;
+    float sm = 0.0f;
     for (long b = 0; b < nfr; b += 64) {
       const float4 q = b + lane < nfr ? ft[b + lane] : make_float4(0, 0, 0, 0);
       const float v = wave == 2 ? q.z : q.y;
-      const int m = (int)(nfr - b < 64 ? nfr - b : 64);
-      for (int i = 0; i < m; ++i) s += readlane_f(v, i);
+      chain(v, (int)(nfr - b < 64 ? nfr - b : 64), [&](float e) { sm += e; });
     }
-    if (lane == 0) s_stat[wave + 1] = nfr > 0 ? __fdiv_rn(s, (float)nfr) : 0.0f;
+    if (lane == 0) s_stat[wave + 1] = nfr > 0 ? __fdiv_rn(sm, (float)nfr) : 0.0f;
   }
   __syncthreads();
   if (t != 0) return;
@@ -316,15 +373,21 @@ __global__ __launch_bounds__(PT) void prosody_kernel(const float* __restrict__ p
   const int nf0 = s_cnt[0];
   float pitch = 0.0f;  // vector_median: the (n/2)-th smallest f0
   if (nf0 > 0) {
-    const int k = nf0 / 2;
-    int cum = 0;
-    for (int c = 0; c < PMAX_HALF; ++c) {
-      cum += s_hist[c];
-      if (cum > k) {
-        pitch = __fdiv_rn((float)c, duration);
+    // cycles < F / 2: scan those bins, eight LDS reads in flight at a time
+    const int k = nf0 / 2, nb = F / 2 + 1;
+    int cum = 0, c = 0;
+    for (; c < nb; c += 8) {
+      int h[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) h[q] = c + q < PMAX_HALF ? s_hist[c + q] : 0;
+      int q = 0;
+      for (; q < 8 && cum + h[q] <= k; ++q) cum += h[q];
+      if (q < 8) {
+        c += q;
         break;
       }
     }
+    pitch = __fdiv_rn((float)c, duration);
   }
   r.pitch_std = s_stat[0];
   if (nfr > 0) {
@@ -391,18 +454,19 @@ __global__ __launch_bounds__(PT) void prosody_kernel(const float* __restrict__ p
 }
 
 void prosody_launch(const float* pcm, const ProsodySeg* seg, int n_seg, float* fstate,
-                    float4* feat, ProsodyOut* out, int frame, int sample_rate, float alpha,
+                    float4* feat, int* fcyc, ProsodyOut* out, int frame, int sample_rate, float alpha,
                     float gender_thr, float min_pitch, float max_pitch, hipStream_t st) {
   if (n_seg <= 0) return;
-  // warm-up: |1 - alpha|^W below e^-40 (~2^-58), then 64 steps for the two
-  // trajectories to settle on the same float (0.07 -> 615 samples); other
-  // alphas just take the checked serial pass more often
-  int warm = 640;
+  // warm-up: |1 - alpha|^W below e^-20 (~2^-29, past the float resolution
+  // of the state relative to the signal), then 64 steps for the two
+  // trajectories to settle on the same float (0.07 -> 352 samples); a run
+  // whose trajectories have not met takes the checked serial pass
+  int warm = 352;
   if (alpha > 0.0f && alpha < 1.0f) {
-    const float w = 40.0f / -log1pf(-alpha);
-    warm = w > 4096.0f ? 4096 : (int)w + 64;
+    const float w = 20.0f / -log1pf(-alpha);
+    warm = w > 4096.0f ? 4096 : ((int)w + 64 + 31) & ~31;
   }
-  prosody_kernel<<<n_seg, PT, 0, st>>>(pcm, seg, fstate, feat, out, frame, sample_rate, alpha,
+  prosody_kernel<<<n_seg, PT, 0, st>>>(pcm, seg, fstate, feat, fcyc, out, frame, sample_rate, alpha,
                                         gender_thr, min_pitch, max_pitch, warm);
 }
 

@@ -240,9 +240,10 @@ struct ProsodyOut {
   int serial_runs;
   int pad;
 };
-// fstate: [sum frames] floats, feat: [sum frames] float4 (frames = len / frame)
+// fstate: [sum frames] floats, feat: [sum frames] float4, fcyc: [sum frames]
+// ints (frames = len / frame)
 void prosody_launch(const float* pcm, const ProsodySeg* seg, int n_seg, float* fstate,
-                    float4* feat, ProsodyOut* out, int frame, int sample_rate, float alpha,
+                    float4* feat, int* fcyc, ProsodyOut* out, int frame, int sample_rate, float alpha,
                     float gender_thr, float min_pitch, float max_pitch, hipStream_t st);
 
 }  // namespace mwx
