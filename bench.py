@@ -281,6 +281,8 @@ def main():
                     help="MX-fp8 compute for the encoder / cross-K/V GEMMs (C5)")
     ap.add_argument("--host-input", action="store_true",
                     help="PCM in host memory, uploaded inside each step (PCIe-inclusive rate)")
+    ap.add_argument("--pcm16", action="store_true",
+                    help="with --host-input: upload int16 PCM, converted on the device")
     ap.add_argument("--prosody", action="store_true",
                     help="segment-prosody leg (SURVEY.md §8 f4) instead of transcription")
     args = ap.parse_args()
@@ -330,7 +332,10 @@ def main():
 
     # inputs resident in HBM before the timed region (the PCIe-inclusive rate,
     # host buffers uploaded inside the step, is --host-input)
-    if args.host_input:
+    if args.host_input and args.pcm16:
+        p16s = [mwx.synth_pcm16(k, n_samp) for k in shard.clip_ids(rank, args.clips)]
+        run_batch = lambda: ctx.full_batch_pcm16(p16s, p)  # noqa: E731
+    elif args.host_input:
         run_batch = lambda: ctx.full_batch(pcms, p)  # noqa: E731
     else:
         dev = [ctx.upload(x) for x in pcms]
@@ -424,7 +429,8 @@ def main():
             "vs_baseline": None,
             "dtype": (f"mxfp8 encoder/cross GEMMs + {args.wtype}" if args.fp8 else args.wtype),
             "data": ("synthetic (seeded 16 kHz PCM16 clips, "
-                     + ("host memory, uploaded per step" if args.host_input else "resident in HBM")
+                     + (("host int16, uploaded and converted per step" if args.pcm16 else
+                         "host memory, uploaded per step") if args.host_input else "resident in HBM")
                      + "; seeded weights in the ggml .bin layout)"),
             "config": {
                 "workload": (f"whisper-{args.arch} {args.wtype}: {args.clips} x {args.clip_seconds:g} s "

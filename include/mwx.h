@@ -191,6 +191,13 @@ int mwx_full_batch(struct mwx_context* ctx, struct mwx_state* const* states,
                    const float* const* samples, const int* n_samples,
                    int n_clips);
 
+/* As mwx_full_batch with 16-bit PCM (host or device memory), converted on
+ * the device exactly as SttEngine::transcribe_pcm16 converts it (x / 32768,
+ * src/stt_engine.cpp:123): half the bytes over PCIe. */
+int mwx_full_batch_pcm16(struct mwx_context* ctx, struct mwx_state* const* states,
+                         struct mwx_full_params params, const int16_t* const* samples,
+                         const int* n_samples, int n_clips);
+
 /* Device input buffers on the context's GPU (for mwx_full_batch over
  * HBM-resident PCM): allocate n floats, upload n floats from host memory
  * (synchronous), free. NULL / <0 on failure. */
@@ -315,6 +322,13 @@ int mwx_perf_read(struct mwx_state* state, double* total_ms, int* launches);
  * Returns 0 on success. */
 int mwx_write_synthetic_model(const char* path, const char* arch, int wtype,
                               uint64_t seed);
+
+/* Quantizes a whisper ggml .bin (f32 / f16 / bf16) into a ggml block type
+ * (q4_0 = 2, q4_1 = 3, q5_0 = 6, q5_1 = 7, q8_0 = 8) with the rules of
+ * whisper.cpp's `quantize` tool: 2-D tensors except the positional
+ * embeddings are quantized, everything else is copied; ftype becomes
+ * 2000 + ftype. Returns 0 on success. */
+int mwx_model_quantize(const char* in_path, const char* out_path, int type);
 
 #ifdef __cplusplus
 }

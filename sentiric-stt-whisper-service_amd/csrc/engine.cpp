@@ -127,7 +127,7 @@ struct State {
   hipEvent_t ev_in = nullptr, ev_done[MWX_MAX_GROUPS] = {};
   // encoder workspace (clip-batched)
   DBuf pcm, mel, melmax, melT, h1p, x, h, q, k, vt, o, ff, enc, cross_k, cross_v;
-  DBuf energy;
+  DBuf energy, pcm16;
   DBuf aq, as;  // MX-fp8 activations (codes [rows][K], scales [rows][K/32])
   DBuf ibuf;  // small int arrays (slot maps)
   DBuf pro_pcm, pro_desc, pro_fs, pro_ft, pro_fc, pro_out;  // segment prosody
@@ -511,7 +511,8 @@ struct TsState {
 
 struct ClipRun {
   State* st = nullptr;
-  const float* pcm = nullptr;
+  const void* pcm = nullptr;
+  size_t pcm_off = 0;  // element offset in the device PCM staging
   int n = 0;
   int n_len = 0, n_len_org = 0, n_fft_frames = 0;
   size_t mel_off = 0;  // element offset of this clip's mel

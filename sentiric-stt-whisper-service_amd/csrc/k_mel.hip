@@ -193,6 +193,25 @@ void launch_mel_window(const float* mel, long mel_clip_stride, const int* clip_o
   mel_window_kernel<<<g, 256, 0, st>>>(mel, mel_clip_stride, clip_of_slot, seek_of_slot,
                                        n_len_of_slot, n_mels, T, cpad, melT);
 }
+// pcm16 -> f32 as SttEngine::transcribe_pcm16 converts (x / 32768, exact)
+__global__ void pcm16_to_f32_kernel(const int16_t* __restrict__ in, long n, float* __restrict__ out) {
+  const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i + 4 <= n) {
+    const short4 v = *reinterpret_cast<const short4*>(in + i);
+    *reinterpret_cast<float4*>(out + i) =
+        make_float4((float)v.x / 32768.0f, (float)v.y / 32768.0f, (float)v.z / 32768.0f,
+                    (float)v.w / 32768.0f);
+  } else {
+    for (long j = i; j < n; ++j) out[j] = (float)in[j] / 32768.0f;
+  }
+}
+
+void launch_pcm16_to_f32(const int16_t* in, long n, float* out, hipStream_t st) {
+  if (n <= 0) return;
+  const long th = (n + 3) / 4;
+  pcm16_to_f32_kernel<<<(unsigned)((th + 255) / 256), 256, 0, st>>>(in, n, out);
+}
+
 void launch_signal_energy(const float* x, int n, float* out, hipStream_t st) {
   signal_energy_kernel<<<(n + 255) / 256, 256, 0, st>>>(x, n, out);
 }

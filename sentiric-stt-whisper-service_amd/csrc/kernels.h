@@ -101,6 +101,8 @@ void launch_mel_window(const float* mel, long mel_clip_stride, const int* clip_o
                        const int* seek_of_slot, const int* n_len_of_slot, int n_mels, int T,
                        int cpad, _Float16* melT, int n_slots, hipStream_t st);
 void launch_signal_energy(const float* x, int n, float* out, hipStream_t st);
+// pcm16 / 32768 -> f32 (in and out 8- / 16-byte aligned)
+void launch_pcm16_to_f32(const int16_t* in, long n, float* out, hipStream_t st);
 
 // LayerNorm of x rows into y. With P != nullptr, x is first completed from
 // the KS split-K partial slabs P[KS][M][N]: x = (sum P + pbias) + x.

@@ -668,6 +668,106 @@ extern "C" int mwx_write_synthetic_model(const char* path, const char* arch,
   return w.f ? 0 : -4;
 }
 
+// ---------------------------------------------------------------------------
+// model quantizer: whisper.cpp's `quantize` tool (examples/quantize +
+// examples/common-ggml.cpp ggml_common_quantize_0 at v1.8.2) — every 2-D
+// tensor except the positional embeddings (and conv biases, which are not
+// 2-D in ggml's sense for the rule below) is rewritten as `type` blocks from
+// its f32 (or f16 / bf16 widened) values; everything else is copied
+// unchanged; hparams.ftype becomes GGML_QNT_VERSION * 1000 + ftype. Streams
+// one tensor at a time.
+// ---------------------------------------------------------------------------
+extern "C" int mwx_model_quantize(const char* in_path, const char* out_path, int type) {
+  using namespace mwx;
+  if (!in_path || !out_path || !ggml_type_is_quant(type)) return -1;
+  std::ifstream fi(in_path, std::ios::binary);
+  if (!fi) return -2;
+  std::ofstream fo(out_path, std::ios::binary | std::ios::trunc);
+  if (!fo) return -3;
+  auto copy = [&](size_t n) {
+    std::vector<char> b(n);
+    fi.read(b.data(), (std::streamsize)n);
+    fo.write(b.data(), (std::streamsize)n);
+    return (bool)fi;
+  };
+  uint32_t magic = 0;
+  int32_t hp[11];
+  if (!rd(fi, magic) || magic != 0x67676d6cu) return -4;
+  for (int32_t& v : hp)
+    if (!rd(fi, v)) return -4;
+  if (hp[10] % 1000 != 1 && hp[10] % 1000 != 0 && hp[10] % 1000 != 24) {
+    MWX_LOG_ERROR("mwx_model_quantize: input must be f32 / f16 / bf16 (ftype %d)\n", hp[10]);
+    return -5;
+  }
+  hp[10] = ggml_ftype_of(type);
+  fo.write(reinterpret_cast<const char*>(&magic), 4);
+  fo.write(reinterpret_cast<const char*>(hp), sizeof hp);
+  int32_t n_mel = 0, n_fft = 0;
+  if (!rd(fi, n_mel) || !rd(fi, n_fft) || n_mel <= 0 || n_fft <= 0) return -4;
+  fo.write(reinterpret_cast<const char*>(&n_mel), 4);
+  fo.write(reinterpret_cast<const char*>(&n_fft), 4);
+  if (!copy((size_t)n_mel * n_fft * 4)) return -4;
+  int32_t n_vocab = 0;
+  if (!rd(fi, n_vocab) || n_vocab < 0) return -4;
+  fo.write(reinterpret_cast<const char*>(&n_vocab), 4);
+  for (int i = 0; i < n_vocab; ++i) {
+    uint32_t len = 0;
+    if (!rd(fi, len)) return -4;
+    fo.write(reinterpret_cast<const char*>(&len), 4);
+    if (len && !copy(len)) return -4;
+  }
+  std::vector<uint8_t> data, qout;
+  std::vector<float> f32;
+  while (true) {
+    int32_t nd = 0, nl = 0, tt = 0;
+    fi.read(reinterpret_cast<char*>(&nd), 4);
+    if (fi.eof()) break;
+    if (!rd(fi, nl) || !rd(fi, tt) || nd < 1 || nd > 4 || nl <= 0 || nl > 256) return -4;
+    int32_t ne[4] = {1, 1, 1, 1};
+    for (int i = 0; i < nd; ++i)
+      if (!rd(fi, ne[i])) return -4;
+    std::string name(nl, '\0');
+    fi.read(&name[0], nl);
+    int64_t n = 1;
+    for (int i = 0; i < nd; ++i) n *= ne[i];
+    const size_t bytes = ggml_tensor_bytes(tt, ne[0], n);
+    if (bytes == 0) return -6;
+    data.resize(bytes);
+    fi.read(reinterpret_cast<char*>(data.data()), (std::streamsize)bytes);
+    if (!fi) return -4;
+    const bool skip = name == "encoder.positional_embedding" ||
+                      name == "decoder.positional_embedding" ||
+                      name == "encoder.conv1.bias" || name == "encoder.conv2.bias";
+    const bool quant = nd == 2 && !skip && ne[0] % 32 == 0 &&
+                       (tt == GGML_F32 || tt == GGML_F16 || tt == GGML_BF16);
+    const int32_t ot = quant ? type : tt;
+    fo.write(reinterpret_cast<const char*>(&nd), 4);
+    fo.write(reinterpret_cast<const char*>(&nl), 4);
+    fo.write(reinterpret_cast<const char*>(&ot), 4);
+    fo.write(reinterpret_cast<const char*>(ne), 4 * nd);
+    fo.write(name.data(), nl);
+    if (!quant) {
+      fo.write(reinterpret_cast<const char*>(data.data()), (std::streamsize)bytes);
+      continue;
+    }
+    f32.resize((size_t)n);
+    for (int64_t i = 0; i < n; ++i) {
+      if (tt == GGML_F32) {
+        memcpy(&f32[i], &data[4 * i], 4);
+      } else {
+        uint16_t h;
+        memcpy(&h, &data[2 * i], 2);
+        f32[i] = tt == GGML_F16 ? f16_to_f32(h) : bf16_to_f32(h);
+      }
+    }
+    qout.resize(ggml_tensor_bytes(type, ne[0], n));
+    ggml_quantize(type, f32.data(), qout.data(), n);
+    fo.write(reinterpret_cast<const char*>(qout.data()), (std::streamsize)qout.size());
+  }
+  fo.close();
+  return fo ? 0 : -7;
+}
+
 extern "C" void mwx_log_set(mwx_log_callback cb, void* user_data) {
   mwx::g_log_cb = cb;
   mwx::g_log_user = user_data;

@@ -141,6 +141,9 @@ def lib() -> C.CDLL:
     L.mwx_device_upload.argtypes = [P, fpp, fpp, C.c_size_t]
     L.mwx_device_buffer_free.restype = None
     L.mwx_device_buffer_free.argtypes = [P, fpp]
+    L.mwx_full_batch_pcm16.restype = C.c_int
+    L.mwx_full_batch_pcm16.argtypes = [P, C.POINTER(P), FullParams, C.POINTER(C.c_void_p),
+                                       C.POINTER(C.c_int), C.c_int]
     L.mwx_full_batch.restype = C.c_int
     L.mwx_full_batch.argtypes = [P, C.POINTER(P), FullParams, C.POINTER(C.POINTER(C.c_float)),
                                  C.POINTER(C.c_int), C.c_int]
@@ -172,6 +175,8 @@ def lib() -> C.CDLL:
         f = getattr(L, f"mwx_{n}")
         f.restype = C.c_int
         f.argtypes = [P]
+    L.mwx_model_quantize.restype = C.c_int
+    L.mwx_model_quantize.argtypes = [C.c_char_p, C.c_char_p, C.c_int]
     L.mwx_write_synthetic_model.restype = C.c_int
     L.mwx_write_synthetic_model.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_uint64]
     L.mwx_perf_enable.restype = None
@@ -228,6 +233,13 @@ def write_synthetic_model(path: str, arch: str, wtype: int = GGML_F16, seed: int
     rc = lib().mwx_write_synthetic_model(path.encode(), arch.encode(), wtype, seed)
     if rc != 0:
         raise RuntimeError(f"mwx_write_synthetic_model failed ({rc})")
+
+
+def quantize_model(in_path: str, out_path: str, qtype: int) -> None:
+    """mwx_model_quantize: whisper.cpp `quantize` tool rules."""
+    rc = lib().mwx_model_quantize(in_path.encode(), out_path.encode(), qtype)
+    if rc != 0:
+        raise RuntimeError(f"mwx_model_quantize failed ({rc})")
 
 
 def synth_pcm16(k: int, n: int = 480000, sr: int = 16000) -> np.ndarray:
@@ -325,6 +337,16 @@ class Context:
 
     def full_batch(self, pcms: Sequence[np.ndarray], params: FullParams) -> int:
         return self.full_batch_states(pcms, params, range(len(pcms)))
+
+    def full_batch_pcm16(self, pcms: Sequence[np.ndarray], params: FullParams) -> int:
+        """mwx_full_batch_pcm16: int16 PCM converted on the device."""
+        n = len(pcms)
+        arrs = [np.ascontiguousarray(p, dtype=np.int16) for p in pcms]
+        states = (C.c_void_p * n)(*[self.state(i) for i in range(n)])
+        ptrs = (C.c_void_p * n)(*[a.ctypes.data for a in arrs])
+        lens = (C.c_int * n)(*[len(a) for a in arrs])
+        self._keep = arrs
+        return lib().mwx_full_batch_pcm16(self.ctx, states, params, ptrs, lens, n)
 
     def full_batch_states(self, pcms: Sequence[np.ndarray], params: FullParams,
                           state_indices: Sequence[int]) -> int:

@@ -207,6 +207,21 @@ def test_device_resident_input_equals_host_input(micro):
     assert dev == host and all(len(t) > 0 for t in host)
 
 
+def test_pcm16_input_equals_f32_input(micro):
+    """mwx_full_batch_pcm16 (int16 PCM converted on the device, x / 32768)
+    gives the transcripts of mwx_full_batch over the host-converted f32 PCM;
+    clip lengths not a multiple of 4 exercise the staging offsets."""
+    ctx, o, _ = micro
+    p = service_params(ctx, temperature_inc=0.0, language=b"en")
+    p16 = [mwx.synth_pcm16(40 + k, n=int(16000 * (5.0 + 2.5 * k)) + k) for k in range(3)]
+    def toks():
+        return [[(t.id, t.p) for s in ctx.segments(i) for t in s.tokens] for i in range(3)]
+    assert ctx.full_batch([mwx.pcm16_to_f32(x) for x in p16], p) == 0
+    want = toks()
+    assert ctx.full_batch_pcm16(p16, p) == 0
+    assert toks() == want and all(len(t) > 0 for t in want)
+
+
 def test_bench_fixed_steps_long_form(micro):
     """Benchmark workload on a long clip: every 30-s window decodes the fixed
     step count, then the clip advances by a whole window (oracle: same rule)."""

@@ -158,3 +158,53 @@ def test_mxfp8_weights_follow_the_mx_rule(make_model):
     for name in ("decoder.blocks.0.attn.query.weight", "decoder.token_embedding.weight",
                  "encoder.conv1.weight"):
         np.testing.assert_array_equal(mx.tensor(name), plain.tensor(name))
+
+
+def np_quantize_q8_0_exact(x):
+    """quantize_row_q8_0_ref bit for bit: d = amax / 127 (f32), id = 1/d,
+    q = roundf(x * id) (half away from zero), d stored as f16."""
+    x = x.astype(np.float32).reshape(-1, 32)
+    amax = np.abs(x).max(axis=1, keepdims=True)
+    d = (amax / np.float32(127.0)).astype(np.float32)
+    idv = np.where(d != 0, np.float32(1.0) / np.where(d != 0, d, np.float32(1)), 0).astype(np.float32)
+    v = (x * idv).astype(np.float32)
+    q = np.sign(v) * np.floor(np.abs(v) + np.float32(0.5))
+    return d.astype(np.float16), q.astype(np.int8)
+
+
+@pytest.mark.parametrize("tt", QTYPES, ids=["q4_0", "q4_1", "q5_0", "q5_1", "q8_0"])
+def test_model_quantize_tool(make_model, tmp_path, tt):
+    """mwx_model_quantize (whisper.cpp `quantize` rules) on an f16 file: 2-D
+    weights become `tt` blocks of the f16 values, positional embeddings / conv
+    biases / 1-D tensors / 3-D conv kernels are copied byte for byte, ftype
+    2000 + ftype; q8_0 blocks equal quantize_row_q8_0_ref exactly."""
+    src = make_model("micro", mwx.GGML_F16)
+    dst = str(tmp_path / "q.bin")
+    mwx.quantize_model(src, dst, tt)
+    hp_s, ts_s = read_tensors(src)
+    hp_d, ts_d = read_tensors(dst)
+    assert hp_d[:10] == hp_s[:10] and hp_d[10] == 2000 + FTYPE[tt]
+    assert list(ts_d) == list(ts_s)
+    for name, (t, ne, raw) in ts_s.items():
+        td, ned, rawd = ts_d[name]
+        assert ned == ne
+        if len(ne) == 2 and name not in ("encoder.positional_embedding",
+                                         "decoder.positional_embedding",
+                                         "encoder.conv1.bias", "encoder.conv2.bias"):
+            assert td == tt, name
+            n = int(np.prod(ne))
+            x = np.frombuffer(raw, np.float16).astype(np.float32)
+            got = np_dequant(tt, rawd, n)
+            xb = x.reshape(-1, 32)
+            step = (xb.max(axis=1) - xb.min(axis=1)) / {2: 15, 3: 15, 6: 31, 7: 31, 8: 254}[tt]
+            assert np.all(np.abs(got.reshape(-1, 32) - xb).max(axis=1) <= step * 1.01 + 1e-6), name
+            if tt == mwx.GGML_Q8_0:
+                d, q = np_quantize_q8_0_exact(x)
+                b = np.frombuffer(rawd, np.uint8).reshape(-1, 34)
+                np.testing.assert_array_equal(b[:, 2:].view(np.int8), q)
+                np.testing.assert_array_equal(b[:, 0:2].copy().view(np.float16), d)
+        else:
+            assert (td, rawd) == (t, raw), name
+    # the oracle (and so the engine's loader, same reader rules) accepts it
+    o = orc.Oracle(dst)
+    assert o.tensor("decoder.blocks.0.mlp.0.weight").shape[0] > 0
