@@ -43,6 +43,15 @@ int mwx_test_decode_last(struct mwx_context* ctx, struct mwx_state* state, const
 int mwx_test_gemm_mx(struct mwx_context* ctx, int M, int N, int K, const float* a,
                      const float* w, float* c);
 
+/* std::discrete_distribution draws on the device (k_misc.hip sample_draws):
+ * probs / logprobs [R][V], u [R][KD] (generate_canonical<double, 53> values),
+ * ndraw [R] (<= KD <= 16); ids [R][KD] out. exact != 0 runs only the
+ * sequential-order kernel. reps > 1 repeats the launch and returns the mean
+ * microseconds per launch in *us (HIP events). Returns 0 or <0. */
+int mwx_test_sample_draws(struct mwx_context* ctx, const float* probs, const float* logprobs,
+                          int R, int V, const double* u, const int* ndraw, int KD, int exact,
+                          int reps, int* ids, double* us);
+
 #ifdef __cplusplus
 }
 #endif

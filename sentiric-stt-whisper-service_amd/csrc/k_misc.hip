@@ -655,15 +655,28 @@ __global__ __launch_bounds__(64) void sample_draws_exact_kernel(const float* __r
 }
 
 // Fast path: the same draws from a parallel evaluation. S = sum p_i (any
-// order), q_i = p_i / S, cumulative values by per-thread chunks + a block scan.
+// order), q_i = p_i * (1 / S); each of the 16 waves owns a contiguous 1/16 of the row
+// and walks it in tiles of 512 (8 consecutive elements per lane, coalesced
+// loads), cumulative values = wave base + lane scan + in-lane order.
 // Sequential rounding (the exact kernel) and this evaluation differ by at most
-// ~2.4e-11 in any cumulative value (n * 2^-53 for each running sum, plus the
+// ~1e-11 in any cumulative value (V * 2^-53 for the running sums, plus the
 // relative difference of the two S through q), so when u lies more than
 // DR_MARGIN from the cumulative values on both sides of the crossing the
 // exact kernel would pick the same index. Rows with a draw inside the margin
-// are flagged and redone by sample_draws_exact_kernel.
+// — or not claimed by exactly one element, as rounding can leave a gap or an
+// overlap at lane / tile / wave boundaries — are flagged and redone by
+// sample_draws_exact_kernel.
 constexpr double DR_MARGIN = 2e-10;
-constexpr int DR_T = 256;
+constexpr int DR_T = 1024;  // 16 waves per row: each walks ~1/16 of the vocabulary
+
+__device__ __forceinline__ double wave_incl_scan_d(double x, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double t = __shfl_up(x, o, 64);
+    if (lane >= o) x += t;
+  }
+  return x;
+}
 
 __global__ __launch_bounds__(DR_T) void sample_draws_kernel(const float* __restrict__ probs,
                                                             const float* __restrict__ logprobs,
@@ -672,51 +685,90 @@ __global__ __launch_bounds__(DR_T) void sample_draws_kernel(const float* __restr
                                                             Draw* __restrict__ out,
                                                             int* __restrict__ need) {
   __shared__ double red[DR_T / 64];
-  __shared__ double scan[DR_T];
   __shared__ int ids[16];
+  __shared__ int claims[16];
   __shared__ int bad;
   const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int nd = ndraw[row];
   if (nd <= 0) return;
   const float* P = probs + (long)row * V;
-  if (tid < 16) ids[tid] = -1;
+  if (tid < 16) {
+    ids[tid] = -1;
+    claims[tid] = 0;
+  }
   if (tid == 0) bad = 0;
+  // wave regions: contiguous, multiples of 8 elements (V is even: 8-byte loads)
+  constexpr int NW = DR_T / 64;
+  const int RW = ((V + NW - 1) / NW + 7) & ~7;
+  const int r0 = min(V, wid * RW), r1 = min(V, r0 + RW);
+  auto ld2 = [&](int i) {
+    return i + 1 < r1 ? *reinterpret_cast<const float2*>(P + i)
+                      : make_float2(i < r1 ? P[i] : 0.0f, 0.0f);
+  };
   double s = 0.0;
-  for (int i = tid; i < V; i += DR_T) s += (double)P[i];
+  for (int i0 = r0 + 2 * lane; i0 < r1; i0 += 8 * 128) {
+    float2 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = ld2(i0 + k * 128);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += (double)v[k].x + (double)v[k].y;
+  }
   s = wave_sum_d(s);
   if (lane == 0) red[wid] = s;
   __syncthreads();
-  const double S = (red[0] + red[1]) + (red[2] + red[3]);
-  const int CH = (V + DR_T - 1) / DR_T;
-  const int a = min(V, tid * CH), b = min(V, a + CH);
-  double loc = 0.0;
-  for (int i = a; i < b; ++i) loc += (double)P[i] / S;
-  // inclusive scan of the chunk totals (Hillis-Steele over DR_T threads)
-  scan[tid] = loc;
-  __syncthreads();
-  for (int o = 1; o < DR_T; o <<= 1) {
-    const double v = tid >= o ? scan[tid - o] : 0.0;
-    __syncthreads();
-    scan[tid] += v;
-    __syncthreads();
-  }
-  const double base = scan[tid] - loc;  // cumulative value before element a
-  // the thread whose chunk holds the crossing of u finds its index
-  for (int d = 0; d < nd; ++d) {
-    const double ud = u[(long)row * KD + d];
-    if (a >= b || !(ud > base - DR_MARGIN)) continue;       // crossing before this chunk
-    if (b < V && scan[tid] + DR_MARGIN < ud) continue;     // ... or after it
-    double prev = base, c = base;
-    for (int i = a; i < b; ++i) {
-      c = i == V - 1 ? 1.0 : c + (double)P[i] / S;  // cp[V-1] = 1.0
-      if (c >= ud) {
-        if (i == a && !(ud > base)) break;  // crossing in an earlier chunk
-        ids[d] = i;
-        if (!(ud - prev > DR_MARGIN && c - ud > DR_MARGIN)) bad = 1;
-        break;
-      }
-      prev = c;
+  double S = 0.0;
+  for (int w = 0; w < NW; ++w) S += red[w];
+  const double iS = 1.0 / S;
+  double carry = 0.0;
+  for (int w = 0; w < wid; ++w) carry += red[w] * iS;
+  double ud[16];
+#pragma unroll
+  for (int d = 0; d < 16; ++d) ud[d] = d < nd ? u[(long)row * KD + d] : 2.0;
+  // tiles double-buffered: the next tile's loads are in flight during the
+  // scan of this one
+  float2 nx[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) nx[k] = ld2(r0 + 8 * lane + 2 * k);
+  for (int t0 = r0; t0 < r1; t0 += 512) {
+    const int e0 = t0 + 8 * lane;
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[2 * k] = nx[k].x;
+      v[2 * k + 1] = nx[k].y;
     }
+    if (t0 + 512 < r1) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) nx[k] = ld2(e0 + 512 + 2 * k);
+    }
+    double loc = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) loc += (double)v[k] * iS;
+    const double inc = wave_incl_scan_d(loc, lane);
+    const double before = carry + (inc - loc), after = carry + inc;
+    const double total = __shfl(inc, 63, 64);
+#pragma unroll
+    for (int d = 0; d < 16; ++d) {
+      if (d >= nd) break;
+      // a draw crosses this tile only if carry < u <= carry + total (+ margin)
+      if (!(ud[d] > carry - DR_MARGIN) || ud[d] > carry + total + DR_MARGIN) continue;
+      if (!(ud[d] > before && ud[d] <= after) && !(e0 + 8 > V - 1 && e0 <= V - 1 && ud[d] > before))
+        continue;
+      double prev = before, c = before;
+      for (int k = 0; k < 8; ++k) {
+        const int i = e0 + k;
+        if (i >= r1) break;
+        c = i == V - 1 ? 1.0 : c + (double)v[k] * iS;  // cp[V-1] = 1.0
+        if (c >= ud[d]) {
+          ids[d] = i;
+          atomicAdd(&claims[d], 1);
+          if (!(ud[d] - prev > DR_MARGIN && c - ud[d] > DR_MARGIN)) bad = 1;
+          break;
+        }
+        prev = c;
+      }
+    }
+    carry += total;
   }
   __syncthreads();
   if (tid < nd) {
@@ -727,15 +779,17 @@ __global__ __launch_bounds__(DR_T) void sample_draws_kernel(const float* __restr
     r.plog = logprobs[(long)row * V + r.id];
     r.pad = 0;
     out[(long)row * KD + tid] = r;
-    if (id < 0) bad = 1;  // (cannot happen: cp[V-1] = 1 > u) -> exact path
+    if (id < 0 || claims[tid] != 1) bad = 1;  // unclaimed / doubly claimed -> exact path
   }
   __syncthreads();
   if (tid == 0) need[row] = bad;
 }
 
 void sample_draws(const float* probs, const float* logprobs, int V, const double* u,
-                  const int* ndraw, int KD, Draw* out, int* need, int R, hipStream_t st) {
-  static const bool exact_only = getenv("MWX_DRAW_EXACT") != nullptr;
+                  const int* ndraw, int KD, Draw* out, int* need, int R, hipStream_t st,
+                  int force_exact) {
+  static const bool env_exact = getenv("MWX_DRAW_EXACT") != nullptr;
+  const bool exact_only = force_exact < 0 ? env_exact : force_exact != 0;
   if (!exact_only)
     sample_draws_kernel<<<R, DR_T, 0, st>>>(probs, logprobs, V, u, ndraw, KD, out, need);
   sample_draws_exact_kernel<<<R, 64, 0, st>>>(probs, logprobs, V, u, ndraw, KD, out,

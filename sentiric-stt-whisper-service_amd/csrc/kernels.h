@@ -223,8 +223,10 @@ struct Draw {
 // need: [R] scratch (rows whose fast-path draw lies within the rounding
 // margin and is redone by the sequential libstdc++-order kernel).
 // MWX_DRAW_EXACT=1 runs the sequential kernel for every row.
+// force_exact: -1 = MWX_DRAW_EXACT env, 0 = fast path + fallback, 1 = exact only.
 void sample_draws(const float* probs, const float* logprobs, int V, const double* u,
-                  const int* ndraw, int KD, Draw* out, int* need, int R, hipStream_t st);
+                  const int* ndraw, int KD, Draw* out, int* need, int R, hipStream_t st,
+                  int force_exact = -1);
 
 // Segment prosody (k_prosody.hip): reference extract_prosody per segment.
 struct ProsodySeg {

@@ -194,6 +194,10 @@ def lib() -> C.CDLL:
     L.mwx_test_decode.argtypes = [P, P, C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_float)]
     L.mwx_test_decode_last.restype = C.c_int
     L.mwx_test_decode_last.argtypes = [P, P, C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_float)]
+    L.mwx_test_sample_draws.restype = C.c_int
+    L.mwx_test_sample_draws.argtypes = [P, fpp, fpp, C.c_int, C.c_int, C.POINTER(C.c_double),
+                                        C.POINTER(C.c_int), C.c_int, C.c_int, C.c_int,
+                                        C.POINTER(C.c_int), C.POINTER(C.c_double)]
     L.mwx_prosody_default_params.restype = ProsodyParams
     L.mwx_prosody_default_params.argtypes = []
     i64p = C.POINTER(C.c_int64)
@@ -427,6 +431,26 @@ class Context:
         if rc != 0:
             raise RuntimeError(f"mwx_prosody_batch failed ({rc})")
         return list(out)[:len(st)]
+
+    def test_sample_draws(self, probs: np.ndarray, logprobs: np.ndarray, u: np.ndarray,
+                          ndraw: np.ndarray, exact: bool = False, reps: int = 1):
+        """mwx_test_sample_draws: ids [R][KD] and mean us per launch."""
+        pr = np.ascontiguousarray(probs, np.float32)
+        lp = np.ascontiguousarray(logprobs, np.float32)
+        uu = np.ascontiguousarray(u, np.float64)
+        nd = np.ascontiguousarray(ndraw, np.int32)
+        R, V = pr.shape
+        KD = uu.shape[1]
+        ids = np.zeros((R, KD), np.int32)
+        us = C.c_double()
+        rc = lib().mwx_test_sample_draws(self.ctx, fptr(pr), fptr(lp), R, V,
+                                         uu.ctypes.data_as(C.POINTER(C.c_double)),
+                                         nd.ctypes.data_as(C.POINTER(C.c_int)), KD, int(exact),
+                                         reps, ids.ctypes.data_as(C.POINTER(C.c_int)),
+                                         C.byref(us))
+        if rc != 0:
+            raise RuntimeError(f"mwx_test_sample_draws failed ({rc})")
+        return ids, us.value
 
     def test_gemm_mx(self, a: np.ndarray, w: np.ndarray) -> np.ndarray:
         """c = MX-fp8(bf16(a)) @ MX-fp8(bf16(w))^T on the block-scaled fp8 MFMA."""
