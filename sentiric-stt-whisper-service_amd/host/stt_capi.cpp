@@ -6,6 +6,7 @@
 #include <string>
 
 #include "stt_engine.h"
+#include "stt_stream.h"
 #include "text_filters.h"
 
 using namespace mwx_host;
@@ -124,6 +125,77 @@ int mwx_stt_cluster_ids(const float* vecs, int n, float threshold, char* out, in
   for (int i = 0; i < n; ++i)
     o += c.assign_or_add(std::vector<float>(vecs + 8 * i, vecs + 8 * i + 8)) + "\n";
   return emit(o, out, cap);
+}
+
+// As mwx_stt_new_batched, with Settings::stream_buffer_samples.
+void* mwx_stt_new_ex(const char* model_dir, const char* model_filename, int parallel_requests,
+                     int queue_timeout_ms, int beam_size, const char* language, int vad_ms_min,
+                     int gpu_device, int max_batch, int batch_window_us,
+                     int stream_buffer_samples) {
+  Settings s;
+  s.model_dir = model_dir;
+  s.model_filename = model_filename;
+  s.parallel_requests = parallel_requests;
+  s.request_queue_timeout_ms = queue_timeout_ms;
+  s.beam_size = beam_size;
+  s.language = language;
+  s.vad_ms_min_duration = vad_ms_min;
+  s.gpu_device = gpu_device;
+  s.max_batch = max_batch;
+  s.batch_window_us = batch_window_us;
+  s.stream_buffer_samples = stream_buffer_samples;
+  try {
+    return new SttEngine(s);
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "SttEngine: %s\n", e.what());
+    return nullptr;
+  }
+}
+
+// StreamSession over an engine: feed one chunk (len 0 = end of speech);
+// returns the events as JSON (strings hex-encoded) like mwx_stt_transcribe_pcm16.
+void* mwx_stt_stream_new(void* eng) { return new StreamSession(*static_cast<SttEngine*>(eng)); }
+void mwx_stt_stream_free(void* s) { delete static_cast<StreamSession*>(s); }
+
+int mwx_stt_stream_feed(void* s, const uint8_t* data, int len, char* out, int cap) {
+  try {
+    const auto evs = static_cast<StreamSession*>(s)->feed(data, len > 0 ? (size_t)len : 0);
+    std::string o = "[";
+    char buf[512];
+    for (size_t i = 0; i < evs.size(); ++i) {
+      const StreamEvent& e = evs[i];
+      std::snprintf(buf, sizeof buf,
+                    "%s{\"final\":%d,\"arousal\":%.9g,\"valence\":%.9g,\"pitch_mean\":%.9g,"
+                    "\"pitch_std\":%.9g,\"energy_mean\":%.9g,\"energy_std\":%.9g,"
+                    "\"spectral_centroid\":%.9g,\"zero_crossing_rate\":%.9g,",
+                    i ? "," : "", (int)e.is_final, e.arousal, e.valence, e.pitch_mean, e.pitch_std,
+                    e.energy_mean, e.energy_std, e.spectral_centroid, e.zero_crossing_rate);
+      o += buf;
+      o += "\"text\":\"" + hex(e.transcription) + "\",\"gender\":\"" + e.gender_proxy +
+           "\",\"emotion\":\"" + e.emotion_proxy + "\",\"speaker\":\"" + e.speaker_id +
+           "\",\"speaker_vec\":[";
+      for (size_t j = 0; j < e.speaker_vec.size(); ++j) {
+        std::snprintf(buf, sizeof buf, "%s%.9g", j ? "," : "", e.speaker_vec[j]);
+        o += buf;
+      }
+      o += "],\"words\":[";
+      for (size_t j = 0; j < e.words.size(); ++j) {
+        const StreamWord& w = e.words[j];
+        std::snprintf(buf, sizeof buf, "%s{\"start\":%.9g,\"end\":%.9g,\"p\":%.9g,\"word\":\"",
+                      j ? "," : "", w.start, w.end, w.probability);
+        o += buf;
+        o += hex(w.word) + "\"}";
+      }
+      o += "]}";
+    }
+    o += "]";
+    const int r = emit(o, out, cap);
+    return r < -1 ? r - 2 : r;
+  } catch (const EngineBusyException&) {
+    return -2;
+  } catch (...) {
+    return -1;
+  }
 }
 
 long mwx_stt_batches(void* eng) { return static_cast<SttEngine*>(eng)->batches_run(); }
