@@ -53,6 +53,13 @@ def kernel_model(arch, kclass, clips, rows, launches, prompt_len, steps):
         # it), plus q in / o out per row
         b = clips * L * d * 2 * 2 + rows * d * 2 * 2
         return "hbm", b, f"{clips:g} clips x K+V 1500x{d} f16 + {rows:g} rows x q/o per launch"
+    if kclass == "dec_attn_self":
+        # every row reads its history K and V (f16, 64 per head) for one
+        # layer: positions 1..(prompt_len + steps - 1) averaged over the steps,
+        # plus the QKV slab reads and the o write
+        n_avg = (prompt_len + (prompt_len + steps - 1)) / 2.0
+        b = rows * (n_avg * d * 2 * 2 + 3 * d * 4 * 2 + d * 2)
+        return "hbm", b, f"{rows:g} rows x mean {n_avg:.0f} positions x K+V {d} f16 per launch"
     if kclass == "enc_gemm":
         conv = 2 * T * d * 3 * n_mels + 2 * L * d * 3 * d
         layer = 2 * L * d * (3 * d + d + 4 * d + 4 * d)
