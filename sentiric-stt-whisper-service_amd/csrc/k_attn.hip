@@ -461,180 +461,6 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
   }
 }
 
-// Decoder self-attention, one WAVE per (row, head), four heads per
-// workgroup: the row's new K/V come from the split-K QKV slabs (written to the
-// cache and used from registers), every key of the head is scored by the same
-// wave, and the softmax and the P.V reduction are wave reductions — no
-// workgroup barrier anywhere (the per-(row, head) work is a few dozen keys, so
-// the barriers of a 256-thread workgroup per head were most of its time).
-// Scores, softmax and P.V use the arithmetic of dec_attn_kernel (dot8 +
-// dpp_sum8, f32 exp, double sum, (float)(1/sum), P rounded to f16, fdot2 row
-// pairs), with the keys of a lane group accumulated in one wave instead of
-// four.
-constexpr int SELF_MAX_KEYS = 448;  // n_text_ctx
-
-template <typename T>
-__global__ __launch_bounds__(256) void dec_self_kernel(
-    const float* __restrict__ P, int KS, int pcols, const float* __restrict__ bias, float qscale,
-    float kscale, _Float16* __restrict__ kbase, _Float16* __restrict__ vbase,
-    const int* __restrict__ kv_index, const int* __restrict__ pos, const int* __restrict__ active,
-    int cap, T* __restrict__ o, int H, float scale, const int* __restrict__ kvmap,
-    const int* __restrict__ own_from, int map_row0, int nq, int R) {
-  __shared__ float sc_all[4][SELF_MAX_KEYS];
-  __shared__ float nq_all[4][3][64];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int HG = (H + 3) / 4;  // head groups per row
-  int row = blockIdx.y, hg = blockIdx.x;
-  if (nq > 1) {
-    // nq rows per clip (beam / best-of decoders): the nq workgroups of one
-    // (clip, head group) land on one XCD (same id % 8 within a window of
-    // 8 * nq ids), so the history rows they share are read from HBM once
-    const int L = blockIdx.x, W = 8 * nq;
-    const int q = (L % W) / 8, g = (L / W) * 8 + L % 8;
-    if (g >= (R / nq) * HG) return;
-    row = (g / HG) * nq + q;
-    hg = g % HG;
-  }
-  const int h = hg * 4 + wid;
-  if (h >= H || !active[row]) return;
-  float* sc = sc_all[wid];
-  const int kg = lane >> 3, c = lane & 7;
-  const int p_row = pos[row], n = p_row + 1;
-  const int slot = kv_index ? kv_index[row] : row;
-  const int D = H * 64;
-  _Float16* K = kbase + (((long)slot * H + h) * cap) * 64;
-  _Float16* V = vbase + (((long)slot * H + h) * cap) * 64;
-  const int own0 = own_from ? own_from[row] : 0;
-  const int* mrow = kvmap ? kvmap + (long)row * cap : nullptr;
-  const long rstride = (long)H * cap * 64;
-  const int jmax = max(n - 2, 0);  // the new row (n - 1) comes from registers
-  const int nb = (n + 63) / 64;
-  f16x8 ka[8], kb[8];
-#define SROWS(buf, base, bidx)                                        \
-  _Pragma("unroll") for (int u = 0; u < 8; ++u) {                     \
-    const int j = min((bidx) * 64 + u * 8 + kg, jmax);                \
-    const _Float16* src = base + (long)j * 64 + c * 8;                \
-    if (j < own0) src += ((long)mrow[j] - map_row0 - slot) * rstride; \
-    buf[u] = *reinterpret_cast<const f16x8*>(src);                    \
-  }
-  // q, k, v element `lane` of this head from the slabs (loads first, then
-  // the first key batch, then the reduction)
-  const long pstride = (long)R * pcols;
-  float pk[3][8];
-#pragma unroll
-  for (int part = 0; part < 3; ++part) {
-    const float* pp = P + (long)row * pcols + part * D + h * 64 + lane;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) pk[part][k] = pp[min(k, KS - 1) * pstride];
-  }
-  SROWS(ka, K, 0)
-  float qk[3];
-#pragma unroll
-  for (int part = 0; part < 3; ++part) {
-    float acc = pk[part][0];
-#pragma unroll
-    for (int k = 1; k < 8; ++k) acc += k < KS ? pk[part][k] : 0.0f;
-    qk[part] = acc;
-  }
-  const int col = h * 64 + lane;
-  const float qv = (float)(_Float16)((qk[0] + bias[col]) * qscale);
-  const _Float16 kvh = (_Float16)(qk[1] * kscale);
-  const _Float16 vvh = (_Float16)(qk[2] + bias[2 * D + col]);
-  K[(long)p_row * 64 + lane] = kvh;
-  V[(long)p_row * 64 + lane] = vvh;
-  nq_all[wid][0][lane] = qv;
-  nq_all[wid][1][lane] = (float)kvh;
-  nq_all[wid][2][lane] = (float)vvh;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  h2 qh[4];
-  f16x8 nkh, nvh;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    nkh[e] = (_Float16)nq_all[wid][1][c * 8 + e];
-    nvh[e] = (_Float16)nq_all[wid][2][c * 8 + e];
-  }
-#pragma unroll
-  for (int e = 0; e < 4; ++e)
-    qh[e] = h2{(_Float16)nq_all[wid][0][c * 8 + 2 * e], (_Float16)nq_all[wid][0][c * 8 + 2 * e + 1]};
-  auto score_batch = [&](const f16x8* kk, int bidx) {
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int j = bidx * 64 + u * 8 + kg;
-      const bool isnew = min(j, n - 1) == p_row;
-      float d = dot8(qh, isnew ? nkh : kk[u]);
-      d = dpp_sum8(d);
-      if (c == 0 && j < n) sc[j] = d * scale;
-    }
-  };
-  for (int b = 0; b < nb; b += 2) {  // (odd nb: one clamped batch extra)
-    SROWS(kb, K, b + 1)
-    score_batch(ka, b);
-    SROWS(ka, K, b + 2)
-    score_batch(kb, b + 1);
-  }
-  SROWS(ka, V, 0)
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  float mx = -INFINITY;
-  for (int j = lane; j < n; j += 64) mx = fmaxf(mx, sc[j]);
-  mx = wave_max(mx);
-  double sum = 0.0;
-  for (int j = lane; j < n; j += 64) {
-    const float e = expf(sc[j] - mx);
-    sc[j] = e;
-    sum += (double)e;
-  }
-  sum = wave_sum_d(sum);
-  const float inv = (float)(1.0 / sum);
-  for (int j = lane; j < n; j += 64) sc[j] = (float)(_Float16)(sc[j] * inv);
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  float acc[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) acc[e] = 0.0f;
-  auto pv_batch = [&](const f16x8* vv, int bidx) {
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int u = 0; u < 8; u += 2) {
-      h2 ph;
-      f16x8 r[2];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int j = bidx * 64 + (u + t) * 8 + kg;
-        const bool isnew = min(j, n - 1) == p_row;
-        float p = sc[min(j, n - 1)];
-        if (j >= n) p = 0.0f;
-        ph[t] = (_Float16)p;
-        r[t] = isnew ? nvh : vv[u + t];
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] = __builtin_amdgcn_fdot2(ph, h2{r[0][e], r[1][e]}, acc[e], false);
-    }
-  };
-  for (int b = 0; b < nb; b += 2) {
-    SROWS(kb, V, b + 1)
-    pv_batch(ka, b);
-    SROWS(ka, V, b + 2)
-    pv_batch(kb, b + 1);
-  }
-#undef SROWS
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    acc[e] += __shfl_xor(acc[e], 8, 64);
-    acc[e] += __shfl_xor(acc[e], 16, 64);
-    acc[e] += __shfl_xor(acc[e], 32, 64);
-  }
-  if (kg == 0) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) o[pack_index(row, h * 64 + c * 8 + e, D)] = to_t<T>(acc[e]);
-  }
-}
-
 // Cross-attention of NQ rows that share one clip's cross K/V (the decoders
 // of a beam search / best-of group: rows g*NQ .. g*NQ+NQ-1): one workgroup per
 // (group, head) streams the clip's K and V once for all NQ queries instead of
@@ -855,21 +681,11 @@ void dec_attention(const float* P, int KS, int pcols, const float* bias, float q
     nq = 1;
   }
   // (cross rows per lane group per batch: 8 measured best; 12 -1.2%, 16 -5%)
-  if (fixed_len == 0) {
-    static const bool old_self = getenv("MWX_SELF_ATTN_WG") != nullptr;
-    if (!old_self) {
-      const int HG = (H + 3) / 4;
-      dim3 gs(HG, R);
-      if (nq > 1) gs = dim3(((R / nq) * HG + 7) / 8 * 8 * nq, 1);
-      dec_self_kernel<T><<<gs, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale, kbase, vbase,
-                                             kv_index, pos, active, kv_len_cap, o, H, scale, kvmap,
-                                             own_from, map_row0, nq, R);
-      return;
-    }
+  if (fixed_len == 0)
     dec_attn_kernel<T, true><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale, kbase, vbase,
                                                 kv_index, pos, active, fixed_len, kv_len_cap, o,
                                                 H, scale, kvmap, own_from, map_row0, nq, R);
-  } else
+  else
     dec_attn_kernel<T, false><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale, kbase,
                                                  vbase, kv_index, pos, active, fixed_len,
                                                  kv_len_cap, o, H, scale, nullptr, nullptr, 0, nq,
