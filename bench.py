@@ -70,8 +70,9 @@ def kernel_model(arch, kclass, clips, rows, launches, prompt_len, steps):
     if kclass == "enc_attn":
         return "mfma", clips * H * 4 * L * L * 64, "QK^T + PV FLOPs per layer launch"
     if kclass == "dec_gemm":
-        w = Ld * 2 * (3 * d * d + d * d + d * d + d * d + 8 * d * d)
-        return "hbm", w * (prompt_len + steps) / max(1, launches), "decoder weight bytes per launch"
+        # six weight GEMMs per layer and decode step
+        w = 2 * (3 * d * d + d * d + d * d + d * d + 8 * d * d)
+        return "hbm", w / 6, "decoder weight bytes per launch (mean of the 6 GEMMs of a layer)"
     if kclass == "logits_gemm":
         return "hbm", V * d * 2 + rows * V * 4, "tied embedding bf16 + f32 logits"
     raise ValueError(kclass)
@@ -388,11 +389,11 @@ def main():
         launches = max(1, nl.value)
         avg_s = tot_ms.value / 1e3 / launches
         # decode kernels run per row group (MWX_DECODE_GROUPS chains on their
-        # own streams): rows per launch from the launch count of the timed steps
-        n_dec_steps = (prompt_len + args.decode_steps - 1) * n_windows
+        # own streams, default 1); the engine times every 8th decode step's
+        # launches (MWX_PERF_PERIOD), all inside the timed region
         rows = args.clips * max(1, args.beam)
         if args.perf_class.startswith("dec_attn"):
-            rows = rows * ARCH[args.arch][4] * n_dec_steps * args.steps / launches
+            rows = rows / max(1, int(os.environ.get("MWX_DECODE_GROUPS", "1")))
         clips_per_launch = args.clips * (rows / (args.clips * max(1, args.beam)))
         bound, work, desc = kernel_model(args.arch, args.perf_class, clips_per_launch, rows,
                                          launches // max(1, args.steps), prompt_len,

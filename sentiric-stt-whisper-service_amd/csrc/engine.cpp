@@ -155,6 +155,7 @@ struct State {
   std::vector<hipEvent_t> perf_ev, perf_gev;
   size_t perf_used = 0, perf_gused = 0;
   bool capturing = false;
+  bool capture_perf = true;  // false while capturing the uninstrumented step graph
   double perf_acc_ms = 0.0;
   long perf_acc_n = 0;
 };
@@ -176,7 +177,9 @@ struct PerfScope {
   hipEvent_t stop = nullptr;
   hipStream_t stream;
   PerfScope(State& s, const char* cls, hipStream_t strm = nullptr)
-      : S(s), on(!s.perf_class.empty() && s.perf_class == cls), stream(strm ? strm : s.stream) {
+      : S(s),
+        on(!s.perf_class.empty() && s.perf_class == cls && (!s.capturing || s.capture_perf)),
+        stream(strm ? strm : s.stream) {
     if (!on) return;
     std::vector<hipEvent_t>& ev = S.capturing ? S.perf_gev : S.perf_ev;
     size_t& used = S.capturing ? S.perf_gused : S.perf_used;

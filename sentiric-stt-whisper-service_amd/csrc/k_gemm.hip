@@ -109,6 +109,9 @@ __device__ __forceinline__ typename Elt<T>::v8 ld8(const T* p) {
 // PFLOP/s vs 0.37-0.63 for a 128x128 register-staged tile.
 // ---------------------------------------------------------------------------
 constexpr int BM = 256, BN = 256, BK = 64;
+#ifndef GEMM_PRIO
+#define GEMM_PRIO 1
+#endif
 constexpr int GWM = 2, GWN = 4;                  // wave grid
 constexpr int GFM = BM / GWM / 16, GFN = BN / GWN / 16;  // 8 x 4 fragments per wave
 constexpr int GDA = BM / 8 / 8, GDB = BN / 8 / 8;  // DMA instructions per wave per tile
@@ -259,10 +262,12 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
         const int row = BM + wn * (BN / GWN) + j * 16 + (lane & 15);
         bf[j] = *reinterpret_cast<const V8*>(&lds[cur][row * BKE + ((kc ^ (row & 7)) << 3)]);
       }
+      if (GEMM_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < GFM; ++i)
 #pragma unroll
         for (int j = 0; j < GFN; ++j) acc[i][j] = Elt<T>::mfma(af[i], bf[j], acc[i][j]);
+      if (GEMM_PRIO) __builtin_amdgcn_s_setprio(0);
     }
     // this wave's reads of `cur` have returned before its next barrier
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
