@@ -131,6 +131,20 @@ struct State {
   DBuf aq, as;  // MX-fp8 activations (codes [rows][K], scales [rows][K/32])
   DBuf ibuf;  // small int arrays (slot maps)
   DBuf pro_pcm, pro_desc, pro_fs, pro_ft, pro_fc, pro_out;  // segment prosody
+  // pinned host staging of the per-step decode control / result records
+  // (DMA straight from / to page-locked memory: no runtime bounce buffer)
+  void* pin = nullptr;
+  size_t pin_n = 0;
+  void* pinned(size_t bytes) {
+    if (bytes > pin_n) {
+      if (pin) (void)hipHostFree(pin);
+      pin = nullptr;
+      pin_n = 0;
+      HIPC(hipHostMalloc(&pin, bytes, hipHostMallocDefault));
+      pin_n = bytes;
+    }
+    return pin;
+  }
   // decoder workspace (row-batched)
   DBuf xd, hd, qd, od, ffd, logits, kself, vself, stepin, ctl, tokout, probs, logprobs, smask;
   DBuf pqkv, pres, pq;  // split-K partial slabs of the decode GEMMs
