@@ -114,7 +114,13 @@ constexpr int BM = 256, BN = 256, BK = 64;
 #endif
 constexpr int GWM = 2, GWN = 4;                  // wave grid
 constexpr int GFM = BM / GWM / 16, GFN = BN / GWN / 16;  // 8 x 4 fragments per wave
-constexpr int GDA = BM / 8 / 8, GDB = BN / 8 / 8;  // DMA instructions per wave per tile
+#ifndef GEMM_STAGES
+// 16-bit operands: LDS ring of 2 x 64-deep tiles (default) or 4 x 32-deep
+// tiles (three in flight); measured on the encoder shapes 817 vs 734 TF/s:
+// the 32-deep tile's extra barrier and fragment-read restart per 32 k cost
+// more than the deeper ring recovers
+#define GEMM_STAGES 2
+#endif
 
 // MX = true: A and W are MX-fp8 (e4m3 bytes, one E8M0 scale per 32 k of a row:
 // P.sa [M][K/32], P.sw [N][K/32]); a K tile is 128 deep (the same 128 B per
@@ -132,12 +138,21 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
   using V8 = typename Elt<T>::v8;
   using TE = typename std::conditional<MX, uint8_t, T>::type;  // operand element
   constexpr int CE = 16 / sizeof(TE);                          // elements per 16-B chunk
-  constexpr int BKE = 8 * CE;                                   // K-tile depth (128 B / row)
+  // ring: NSTG stages of (BM + BN) rows x RBY bytes (128 KB in total): 16-bit
+  // operands 2 x 64-deep (or GEMM_STAGES = 4: 4 x 32-deep), MX-fp8 2 x 128-deep
+  constexpr int NSTG = MX ? 2 : GEMM_STAGES;
+  constexpr int RBY = MX ? 128 : (GEMM_STAGES == 4 ? 64 : 128);  // bytes per row per tile
+  constexpr int CPR = RBY / 16;                                  // 16-B chunks per row
+  constexpr int RPI = 64 / CPR;                                  // rows per 1-KB DMA instruction
+  constexpr int BKE = CPR * CE;                                  // K-tile depth (elements)
+  constexpr int GDA = BM / RPI / 8, GDB = BN / RPI / 8;          // DMA instructions per wave per tile
+  // chunk swizzle: 16 consecutive rows read one chunk column conflict-free
+  auto swz = [](int row) { return CPR == 8 ? (row & 7) : ((row >> 2) & 3); };
   const TE* A = reinterpret_cast<const TE*>(Av);
   const TE* W = reinterpret_cast<const TE*>(Wv);
   // one __shared__ array only (a second one can make hipcc drain the LDS DMA
   // before every ds_read): [stage][A rows 0..255 | W rows 0..255][128 B]
-  __shared__ __attribute__((aligned(16))) TE lds[2][(BM + BN) * BKE];
+  __shared__ __attribute__((aligned(16))) TE lds[NSTG][(BM + BN) * BKE];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / GWN, wn = wid % GWN;
   const int nbn = (N + BN - 1) / BN;
@@ -157,18 +172,18 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
   // image linearly in lane order; the XOR swizzle (16-B chunk slot =
   // kc ^ (row & 7), conflict-free fragment reads) is applied on the SOURCE
   // address. Rows past M / N are clamped (their outputs are discarded).
-  const int lr = lane >> 3, ls = lane & 7;
+  const int lr = lane / CPR, ls = lane % CPR;
   const TE* asrc[GDA];
   const TE* wsrc[GDB];
 #pragma unroll
   for (int i = 0; i < GDA; ++i) {
-    const int r = (wid * GDA + i) * 8 + lr;
-    asrc[i] = A + (long)min(m0 + r, M - 1) * lda + (ls ^ (r & 7)) * CE;
+    const int r = (wid * GDA + i) * RPI + lr;
+    asrc[i] = A + (long)min(m0 + r, M - 1) * lda + (ls ^ swz(r)) * CE;
   }
 #pragma unroll
   for (int i = 0; i < GDB; ++i) {
-    const int r = (wid * GDB + i) * 8 + lr;
-    wsrc[i] = W + (long)min(n0 + r, N - 1) * ldw + (ls ^ (r & 7)) * CE;
+    const int r = (wid * GDB + i) * RPI + lr;
+    wsrc[i] = W + (long)min(n0 + r, N - 1) * ldw + (ls ^ swz(r)) * CE;
   }
   // MX scale rows of this lane's fragments (row = fragment row l&15)
   const int ksb = K / 32;
@@ -189,11 +204,11 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
     const int ko = (kt) * BKE;                                                              \
     _Pragma("unroll") for (int i = 0; i < GDA; ++i) __builtin_amdgcn_global_load_lds(       \
         (const void __attribute__((address_space(1)))*)(asrc[i] + ko),                      \
-        (void __attribute__((address_space(3)))*)(&lds[st][((wid * GDA + i) * 8) * BKE]), 16, \
+        (void __attribute__((address_space(3)))*)(&lds[st][((wid * GDA + i) * RPI) * BKE]), 16, \
         0, 0);                                                                              \
     _Pragma("unroll") for (int i = 0; i < GDB; ++i) __builtin_amdgcn_global_load_lds(       \
         (const void __attribute__((address_space(1)))*)(wsrc[i] + ko),                      \
-        (void __attribute__((address_space(3)))*)(&lds[st][(BM + (wid * GDB + i) * 8) * BKE]), \
+        (void __attribute__((address_space(3)))*)(&lds[st][(BM + (wid * GDB + i) * RPI) * BKE]), \
         16, 0, 0);                                                                          \
   } while (0)
 
@@ -203,9 +218,11 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
 #pragma unroll
     for (int j = 0; j < GFN; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
   const int nk = K / BKE;
-  GLDS(0, 0);
+#pragma unroll
+  for (int t = 0; t < NSTG - 1; ++t)
+    if (t < nk) GLDS(t, t);
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
+    const int cur = kt % NSTG;
     int sa_k[MX ? GFM : 1], sw_k[MX ? GFN : 1];
     if constexpr (MX) {  // this tile's scales (issued before the wait: L2 hits)
 #pragma unroll
@@ -216,11 +233,24 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
     // tile kt has landed (this wave's DMA), then the barrier makes every
     // wave's part visible and orders all reads of the other stage (tile kt-1)
     // before it is refilled below
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // (tiles issued after kt may stay in flight: counted wait)
+    {
+      const int after = min(NSTG - 2, nk - 1 - kt);
+      if constexpr (NSTG == 4) {
+        if (after >= 2)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (BM / 16 / 8 + BN / 16 / 8)) : "memory");
+        else if (after == 1)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BM / 16 / 8 + BN / 16 / 8) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (kt + 1 < nk) GLDS(kt + 1, cur ^ 1);
+    if (kt + NSTG - 1 < nk) GLDS(kt + NSTG - 1, (kt + NSTG - 1) % NSTG);
     if constexpr (MX) {
       typedef int v8i __attribute__((ext_vector_type(8)));
       v8i af[GFM], bf[GFN];
@@ -249,18 +279,18 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
               af[i], bf[j], acc[i][j], 0, 0, 0, sa_k[i], 0, sw_k[j]);
     } else
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < CPR / 4; ++s) {
       V8 af[GFM], bf[GFN];
       const int kc = s * 4 + (lane >> 4);
 #pragma unroll
       for (int i = 0; i < GFM; ++i) {
         const int row = wm * (BM / GWM) + i * 16 + (lane & 15);
-        af[i] = *reinterpret_cast<const V8*>(&lds[cur][row * BKE + ((kc ^ (row & 7)) << 3)]);
+        af[i] = *reinterpret_cast<const V8*>(&lds[cur][row * BKE + ((kc ^ swz(row)) << 3)]);
       }
 #pragma unroll
       for (int j = 0; j < GFN; ++j) {
         const int row = BM + wn * (BN / GWN) + j * 16 + (lane & 15);
-        bf[j] = *reinterpret_cast<const V8*>(&lds[cur][row * BKE + ((kc ^ (row & 7)) << 3)]);
+        bf[j] = *reinterpret_cast<const V8*>(&lds[cur][row * BKE + ((kc ^ swz(row)) << 3)]);
       }
       if (GEMM_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
