@@ -365,7 +365,10 @@ def main():
     L = mwx.lib()
     st0 = ctx.state(0)  # workspace / stream owner of the batch
     L.mwx_perf_read(st0, None, None)
-    L.mwx_perf_enable(st0, args.perf_class.encode())
+    # the dominant kernel's class, plus the encoder GEMMs (MFMA fraction,
+    # SURVEY.md §8 d asks for both bounds), timed in the same steps
+    classes = [args.perf_class] + (["enc_gemm"] if args.perf_class != "enc_gemm" else [])
+    L.mwx_perf_enable(st0, ",".join(classes).encode())
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -375,10 +378,13 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     import ctypes
-    tot_ms = ctypes.c_double()
-    nl = ctypes.c_int()
-    L.mwx_perf_read(st0, ctypes.byref(tot_ms), ctypes.byref(nl))
+    timed = {}
+    for cls in classes:
+        tms, nlc = ctypes.c_double(), ctypes.c_int()
+        L.mwx_perf_read_class(st0, cls.encode(), ctypes.byref(tms), ctypes.byref(nlc))
+        timed[cls] = (tms.value, nlc.value)
     L.mwx_perf_enable(st0, None)
+    tot_ms, nl = ctypes.c_double(timed[args.perf_class][0]), ctypes.c_int(timed[args.perf_class][1])
     if dist is not None:
         e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
@@ -417,6 +423,18 @@ def main():
                     "traffic": traffic}
         roof.update({"kernel": args.perf_class, "avg_launch_us": round(avg_s * 1e6, 2),
                      "launches": nl.value, "work_per_launch": work, "work_desc": desc})
+        roof_enc = None
+        if "enc_gemm" in timed and args.perf_class != "enc_gemm" and timed["enc_gemm"][1] > 0:
+            ems, en = timed["enc_gemm"]
+            _, ework, edesc = kernel_model(args.arch, "enc_gemm", args.clips, rows,
+                                           en // max(1, args.steps), prompt_len, args.decode_steps)
+            eavg = ems / 1e3 / en
+            epeak = 2 * MFMA_PEAK_TFLOPS if args.fp8 else MFMA_PEAK_TFLOPS
+            each = ework / eavg / 1e12
+            roof_enc = {"bound": "mfma", "achieved": round(each, 1), "peak": epeak,
+                        "unit": "TFLOP/s", "frac": round(each / epeak, 4), "kernel": "enc_gemm",
+                        "avg_launch_us": round(eavg * 1e6, 2), "launches": en,
+                        "work_per_launch": ework, "work_desc": edesc}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
@@ -453,6 +471,7 @@ def main():
             "rtf": round(elapsed / audio_s * world, 6),
             "x_realtime_per_gpu": round(value / world, 1),
             "roofline": roof,
+            "roofline_encoder": roof_enc,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

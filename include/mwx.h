@@ -311,6 +311,11 @@ void mwx_log_set(mwx_log_callback log_callback, void* user_data);
  * count since the last read, and resets them. */
 void mwx_perf_enable(struct mwx_state* state, const char* kernel_class);
 int mwx_perf_read(struct mwx_state* state, double* total_ms, int* launches);
+/* Several classes may be enabled at once as a comma-separated list;
+ * mwx_perf_read reads the first, mwx_perf_read_class any of them. Launches
+ * inside the decode-step graph are timed on every 8th step (MWX_PERF_PERIOD). */
+int mwx_perf_read_class(struct mwx_state* state, const char* kernel_class, double* total_ms,
+                        int* launches);
 
 /* --- model tooling --------------------------------------------------------
  * Writes a model in the ggml .bin layout read by whisper.cpp and by

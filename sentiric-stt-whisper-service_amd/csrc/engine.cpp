@@ -165,22 +165,34 @@ struct State {
   // perf: event pairs around launches of one kernel class. Eager launches
   // use perf_ev; launches captured into a decode-step graph use perf_gev (the
   // graph re-records them on every replay; harvested after each replay).
-  std::string perf_class;
+  // Several classes may be enabled at once (comma-separated): every pair is
+  // tagged with its class and accumulated per class.
+  std::string perf_class;                 // the enabled list ("" = off)
+  std::vector<std::string> perf_classes;  // parsed
   std::vector<hipEvent_t> perf_ev, perf_gev;
+  std::vector<int> perf_tag, perf_gtag;   // class of each event pair
   size_t perf_used = 0, perf_gused = 0;
   bool capturing = false;
   bool capture_perf = true;  // false while capturing the uninstrumented step graph
-  double perf_acc_ms = 0.0;
-  long perf_acc_n = 0;
+  std::vector<double> perf_acc_ms;
+  std::vector<long> perf_acc_n;
 };
 
-static void harvest_events(std::vector<hipEvent_t>& ev, size_t used, State& S) {
+static void harvest_events(std::vector<hipEvent_t>& ev, const std::vector<int>& tag, size_t used,
+                           State& S) {
   for (size_t i = 0; i + 1 < used; i += 2) {
     float ms = 0.0f;
     HIPC(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
-    S.perf_acc_ms += ms;
-    S.perf_acc_n += 1;
+    const int c = tag[i / 2];
+    S.perf_acc_ms[c] += ms;
+    S.perf_acc_n[c] += 1;
   }
+}
+
+static int perf_class_index(const State& S, const char* cls) {
+  for (size_t i = 0; i < S.perf_classes.size(); ++i)
+    if (S.perf_classes[i] == cls) return (int)i;
+  return -1;
 }
 
 // Records a start/stop HIP event pair around a launch when `cls` is the
@@ -191,17 +203,21 @@ struct PerfScope {
   hipEvent_t stop = nullptr;
   hipStream_t stream;
   PerfScope(State& s, const char* cls, hipStream_t strm = nullptr)
-      : S(s),
-        on(!s.perf_class.empty() && s.perf_class == cls && (!s.capturing || s.capture_perf)),
-        stream(strm ? strm : s.stream) {
-    if (!on) return;
+      : S(s), on(false), stream(strm ? strm : s.stream) {
+    if (s.perf_class.empty() || (s.capturing && !s.capture_perf)) return;
+    const int ci = perf_class_index(s, cls);
+    if (ci < 0) return;
+    on = true;
     std::vector<hipEvent_t>& ev = S.capturing ? S.perf_gev : S.perf_ev;
+    std::vector<int>& tag = S.capturing ? S.perf_gtag : S.perf_tag;
     size_t& used = S.capturing ? S.perf_gused : S.perf_used;
     while (ev.size() < used + 2) {
       hipEvent_t e;
       HIPC(hipEventCreate(&e));
       ev.push_back(e);
     }
+    if (tag.size() < used / 2 + 1) tag.resize(used / 2 + 1);
+    tag[used / 2] = ci;
     record(ev[used]);
     stop = ev[used + 1];
     used += 2;

@@ -183,6 +183,8 @@ def lib() -> C.CDLL:
     L.mwx_perf_enable.argtypes = [P, C.c_char_p]
     L.mwx_perf_read.restype = C.c_int
     L.mwx_perf_read.argtypes = [P, C.POINTER(C.c_double), C.POINTER(C.c_int)]
+    L.mwx_perf_read_class.restype = C.c_int
+    L.mwx_perf_read_class.argtypes = [P, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_int)]
     L.mwx_tokenize.restype = C.c_int
     L.mwx_tokenize.argtypes = [P, C.c_char_p, C.POINTER(C.c_int32), C.c_int]
     L.mwx_test_mel.restype = C.c_int
