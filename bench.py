@@ -42,7 +42,7 @@ ARCH = {  # n_mels, d, heads, enc layers, dec layers, vocab
 }
 
 
-def kernel_model(arch, kclass, clips, rows, launches, prompt_len, steps):
+def kernel_model(arch, kclass, clips, rows, launches, prompt_len, steps, windows=1):
     """Algorithmic work of one launch of `kclass`, averaged over the launches of
     one step: (bound, per-launch bytes or flops, description)."""
     n_mels, d, H, Le, Ld, V = ARCH[arch]
@@ -63,7 +63,7 @@ def kernel_model(arch, kclass, clips, rows, launches, prompt_len, steps):
     if kclass == "enc_gemm":
         conv = 2 * T * d * 3 * n_mels + 2 * L * d * 3 * d
         layer = 2 * L * d * (3 * d + d + 4 * d + 4 * d)
-        flops = clips * (conv + Le * layer)
+        flops = clips * windows * (conv + Le * layer)  # every 30-s window is encoded
         return "mfma", flops / max(1, launches), "conv1/conv2/QKV/out/FC1/FC2 FLOPs per launch"
     if kclass == "cross_gemm":
         return "mfma", 2 * clips * L * d * 2 * d * Ld, "all-layer cross K/V GEMM"
@@ -403,7 +403,7 @@ def main():
         clips_per_launch = args.clips * (rows / (args.clips * max(1, args.beam)))
         bound, work, desc = kernel_model(args.arch, args.perf_class, clips_per_launch, rows,
                                          launches // max(1, args.steps), prompt_len,
-                                         args.decode_steps)
+                                         args.decode_steps, n_windows)
         traffic = None
         tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(tf):
@@ -427,7 +427,8 @@ def main():
         if "enc_gemm" in timed and args.perf_class != "enc_gemm" and timed["enc_gemm"][1] > 0:
             ems, en = timed["enc_gemm"]
             _, ework, edesc = kernel_model(args.arch, "enc_gemm", args.clips, rows,
-                                           en // max(1, args.steps), prompt_len, args.decode_steps)
+                                           en // max(1, args.steps), prompt_len, args.decode_steps,
+                                           n_windows)
             eavg = ems / 1e3 / en
             epeak = 2 * MFMA_PEAK_TFLOPS if args.fp8 else MFMA_PEAK_TFLOPS
             each = ework / eavg / 1e12
