@@ -277,27 +277,35 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
         for (int j = 0; j < GFN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
               af[i], bf[j], acc[i][j], 0, 0, 0, sa_k[i], 0, sw_k[j]);
-    } else
+    } else {
+      // both 32-deep sub-steps' fragments are read up front: the MFMAs of
+      // sub-step 0 wait only for their own 12 reads (counted lgkmcnt) while
+      // sub-step 1's are in flight
+      constexpr int NSUB = CPR / 4;
+      V8 af[NSUB][GFM], bf[NSUB][GFN];
 #pragma unroll
-    for (int s = 0; s < CPR / 4; ++s) {
-      V8 af[GFM], bf[GFN];
-      const int kc = s * 4 + (lane >> 4);
+      for (int s = 0; s < NSUB; ++s) {
+        const int kc = s * 4 + (lane >> 4);
 #pragma unroll
-      for (int i = 0; i < GFM; ++i) {
-        const int row = wm * (BM / GWM) + i * 16 + (lane & 15);
-        af[i] = *reinterpret_cast<const V8*>(&lds[cur][row * BKE + ((kc ^ swz(row)) << 3)]);
+        for (int i = 0; i < GFM; ++i) {
+          const int row = wm * (BM / GWM) + i * 16 + (lane & 15);
+          af[s][i] = *reinterpret_cast<const V8*>(&lds[cur][row * BKE + ((kc ^ swz(row)) << 3)]);
+        }
+#pragma unroll
+        for (int j = 0; j < GFN; ++j) {
+          const int row = BM + wn * (BN / GWN) + j * 16 + (lane & 15);
+          bf[s][j] = *reinterpret_cast<const V8*>(&lds[cur][row * BKE + ((kc ^ swz(row)) << 3)]);
+        }
       }
 #pragma unroll
-      for (int j = 0; j < GFN; ++j) {
-        const int row = BM + wn * (BN / GWN) + j * 16 + (lane & 15);
-        bf[j] = *reinterpret_cast<const V8*>(&lds[cur][row * BKE + ((kc ^ swz(row)) << 3)]);
+      for (int s = 0; s < NSUB; ++s) {
+        if (GEMM_PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < GFM; ++i)
+#pragma unroll
+          for (int j = 0; j < GFN; ++j) acc[i][j] = Elt<T>::mfma(af[s][i], bf[s][j], acc[i][j]);
+        if (GEMM_PRIO) __builtin_amdgcn_s_setprio(0);
       }
-      if (GEMM_PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < GFM; ++i)
-#pragma unroll
-        for (int j = 0; j < GFN; ++j) acc[i][j] = Elt<T>::mfma(af[i], bf[j], acc[i][j]);
-      if (GEMM_PRIO) __builtin_amdgcn_s_setprio(0);
     }
     // this wave's reads of `cur` have returned before its next barrier
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
