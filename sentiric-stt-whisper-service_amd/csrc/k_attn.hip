@@ -302,12 +302,12 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
   const int* mrow = SELF && kvmap ? kvmap + (long)row * cap : nullptr;
   const long rstride = (long)H * cap * 64;
   // rows per 8-lane group per batch (cross: UBX, tunable), BR rows per batch
-  constexpr int UB = SELF ? 8 : UBX, BR = 32 * UB;
+  constexpr int UB = UBX, BR = 32 * UB;
   const int nb = (n + BR - 1) / BR;
   // rows past the end are clamped to the last OLD row (self: the new row is
   // being written by this workgroup and is taken from LDS instead)
   const int jmax = SELF ? max(n - 2, 0) : n - 1;
-  const bool wave_busy = wid * (8 * UB) < n;  // self: waves past the last row idle (n <= 256)
+  const bool wave_busy = wid * (8 * UB) < n;  // self: waves past the last row idle (n <= 32 UB)
   f16x8 ka[UB], kb2[UB];
 #define LOADROWS(buf, base, bidx)                                                  \
   _Pragma("unroll") for (int u = 0; u < UB; ++u) {                               \
@@ -315,6 +315,29 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
     const _Float16* src = base + (long)j * 64 + c * 8;                            \
     if (SELF && j < own0)                                                         \
       src += ((long)mrow[j] - map_row0 - slot) * rstride;                         \
+    buf[u] = *reinterpret_cast<const f16x8*>(src);                                \
+  }
+  // self (beam search): the history rows of batch 0 are resolved through the
+  // position map once, before anything else is loaded, and the row deltas are
+  // kept in registers for both the K and the V loads of that batch (the map
+  // read is one round trip ahead of K only, none ahead of V)
+  int mdel[SELF ? UB : 1];
+  if constexpr (SELF) {
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int j = min(wid * (8 * UB) + u * 8 + kg, jmax);
+      mdel[u] = (mrow && j < own0) ? mrow[j] - map_row0 - slot : 0;
+    }
+  }
+#define LOADROWS0(buf, base)                                                      \
+  _Pragma("unroll") for (int u = 0; u < UB; ++u) {                               \
+    const int j = min(wid * (8 * UB) + u * 8 + kg, jmax);                        \
+    const _Float16* src = base + (long)j * 64 + c * 8;                            \
+    if (SELF) {                                                                   \
+      int md = mdel[SELF ? u : 0];                                                \
+      asm volatile("" : "+v"(md)); /* no hoisted 64-bit V addresses */            \
+      src += (long)md * rstride;                                                  \
+    }                                                                             \
     buf[u] = *reinterpret_cast<const f16x8*>(src);                                \
   }
   // reduce the projections of this head from the split-K slabs (KS <= 8):
@@ -330,7 +353,7 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
 #pragma unroll
     for (int k = 0; k < 8; ++k) pk[k] = pp[min(k, KS - 1) * pstride];
   }
-  LOADROWS(ka, K, 0)
+  LOADROWS0(ka, K)
   if (red) {
     float acc = pk[0];
 #pragma unroll
@@ -373,8 +396,9 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
     }
   };
   if constexpr (SELF) {
-    // <= 2 batches (n <= 448): latency-bound, one batch per trip (loading V
-    // batch 0 together with K batch 0 measured 10% slower: occupancy 4 -> 3)
+    // <= 4 batches of 128 rows at UB = 4 (n <= 448): latency-bound, one batch
+    // per trip (loading V batch 0 together with K batch 0 measured 10% slower
+    // at UB = 8: occupancy 4 -> 3)
     for (int b = 0; wave_busy && b < nb; ++b) {
       if (b > 0) LOADROWS(ka, K, b)
       score_batch(ka, b);
@@ -387,7 +411,7 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
       score_batch(kb2, b + 1);
     }
   }
-  LOADROWS(ka, V, 0)
+  LOADROWS0(ka, V)
   __syncthreads();
   float mx = -INFINITY;
   for (int j = tid; j < n; j += 256) mx = fmaxf(mx, sc[j]);
@@ -443,6 +467,7 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
     }
   }
 #undef LOADROWS
+#undef LOADROWS0
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     acc[e] += __shfl_xor(acc[e], 8, 64);
@@ -681,7 +706,15 @@ void dec_attention(const float* P, int KS, int pcols, const float* bias, float q
     nq = 1;
   }
   // (cross rows per lane group per batch: 8 measured best; 12 -1.2%, 16 -5%)
-  if (fixed_len == 0)
+  // (self rows per lane group per batch: 4 -- 66 VGPRs, 7 waves/SIMD: beam 5
+  // 659 -> 687 audio-s/s; 8 with MWX_SELF_UB=8 for A/B)
+  static const bool self_ub4 = !(getenv("MWX_SELF_UB") && atoi(getenv("MWX_SELF_UB")) == 8);
+  if (fixed_len == 0 && self_ub4)
+    dec_attn_kernel<T, true, 4><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale, kbase,
+                                                   vbase, kv_index, pos, active, fixed_len,
+                                                   kv_len_cap, o, H, scale, kvmap, own_from,
+                                                   map_row0, nq, R);
+  else if (fixed_len == 0)
     dec_attn_kernel<T, true><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale, kbase, vbase,
                                                 kv_index, pos, active, fixed_len, kv_len_cap, o,
                                                 H, scale, kvmap, own_from, map_row0, nq, R);
