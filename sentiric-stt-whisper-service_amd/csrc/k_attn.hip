@@ -284,13 +284,18 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
     row = (g / H) * nq + q;
     h = g % H;
   }
-  if (!active[row]) return;
+  // the row's control words are fetched together (one round trip), then the
+  // inactive-row exit
+  const int act_r = active[row];
+  const int p_row = SELF ? pos[row] : 0;
+  const int slot = kv_index ? kv_index[row] : row;
+  const int own0 = SELF && own_from ? own_from[row] : 0;
+  asm volatile("" ::"s"(act_r), "s"(p_row), "s"(slot), "s"(own0));
+  if (!act_r) return;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int kg = lane >> 3, c = lane & 7;
-  const int p_row = SELF ? pos[row] : 0;
   const int n = SELF ? p_row + 1 : fixed_len;
   const int jnew = SELF ? p_row : -1;
-  const int slot = kv_index ? kv_index[row] : row;
   const int D = H * 64;
   _Float16* K = kbase + (((long)slot * H + h) * cap) * 64;
   _Float16* V = vbase + (((long)slot * H + h) * cap) * 64;
@@ -298,7 +303,6 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
   // other rows' histories; kvmap[row][j] names the row (numbered from
   // -map_row0 relative to kbase) whose cache holds position j (histories are
   // never overwritten, so no KV is copied)
-  const int own0 = SELF && own_from ? own_from[row] : 0;
   const int* mrow = SELF && kvmap ? kvmap + (long)row * cap : nullptr;
   const long rstride = (long)H * cap * 64;
   // rows per 8-lane group per batch (cross: UBX, tunable), BR rows per batch
@@ -508,13 +512,16 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
   const int kg = lane >> 3, c = lane & 7;
   bool act[NQ];
   bool any = false;
+  // the group's control words and its K/V slot are fetched together (one
+  // round trip), then the all-inactive exit
+  const int slot = kv_index ? kv_index[row0] : row0;
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
-    act[q] = row0 + q < R && active[row0 + q];
+    act[q] = row0 + q < R && active[min(row0 + q, R - 1)];
     any |= act[q];
   }
+  asm volatile("" ::"s"(slot));
   if (!any) return;
-  const int slot = kv_index ? kv_index[row0] : row0;
   const int D = H * 64;
   const _Float16* K = kbase + (((long)slot * H + h) * cap) * 64;
   const _Float16* V = vbase + (((long)slot * H + h) * cap) * 64;

@@ -125,23 +125,17 @@ __global__ __launch_bounds__(256) void ln_dec_kernel(float* __restrict__ x,
                                                      const float* __restrict__ pbias) {
   __shared__ double red[2][4];
   const int row = blockIdx.x;
-  if (active && !active[row]) return;
+  // the row, its split-K slabs and the activity flag are all requested before
+  // the inactive-row exit waits on the flag (one round trip, not two)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const bool own = tid * 8 < N;
   const int i0 = own ? tid * 8 : 0;
   float* xr = x + (long)row * N + i0;
-  float v[8];
-  {
-    const f32x4 a = *reinterpret_cast<const f32x4*>(xr);
-    const f32x4 c = *reinterpret_cast<const f32x4*>(xr + 4);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      v[e] = a[e];
-      v[4 + e] = c[e];
-    }
-  }
+  const f32x4 xa = *reinterpret_cast<const f32x4*>(xr);
+  const f32x4 xc = *reinterpret_cast<const f32x4*>(xr + 4);
+  f32x4 pk[8][2];
+  f32x4 pb0, pb1;
   if (P) {
-    f32x4 pk[8][2];
     const float* pp = P + (long)row * N + i0;
 #pragma unroll
     for (int k = 0; k < 8; ++k)
@@ -149,8 +143,22 @@ __global__ __launch_bounds__(256) void ln_dec_kernel(float* __restrict__ x,
         pk[k][0] = *reinterpret_cast<const f32x4*>(pp + k * pstride);
         pk[k][1] = *reinterpret_cast<const f32x4*>(pp + k * pstride + 4);
       }
-    const f32x4 pb0 = *reinterpret_cast<const f32x4*>(pbias + i0);
-    const f32x4 pb1 = *reinterpret_cast<const f32x4*>(pbias + i0 + 4);
+    pb0 = *reinterpret_cast<const f32x4*>(pbias + i0);
+    pb1 = *reinterpret_cast<const f32x4*>(pbias + i0 + 4);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  const int act_r = active ? active[row] : 1;
+  if (!act_r) {
+    asm volatile("" ::"v"(xa[0]), "v"(xc[0]));  // (the loads stay above the exit)
+    return;
+  }
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[e] = xa[e];
+    v[4 + e] = xc[e];
+  }
+  if (P) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       float acc = pk[0][e >> 2][e & 3];
