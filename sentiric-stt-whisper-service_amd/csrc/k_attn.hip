@@ -537,18 +537,32 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
     const int j = min((bidx) * 256 + wid * 64 + ((half) * UH + uu) * 8 + kg, jmax); \
     buf[uu] = *reinterpret_cast<const f16x8*>(base + (long)j * 64 + c * 8);   \
   }
-  // queries: q = f16(sum of the split-K slabs + bias), head h's 64 columns
+  // queries: q = f16(sum of the split-K slabs + bias), head h's 64 columns.
+  // All slab loads (KS <= 8, clamped) are issued first, then the first key
+  // batch, so the sums wait for one round trip and the keys are in flight
   const long pstride = (long)R * pcols;
-  for (int t = tid; t < NQ * 64; t += 256) {
-    const int q = t >> 6, e = t & 63;
-    const int col = h * 64 + e;
-    const int r = min(row0 + q, R - 1);
-    const float* pp = P + (long)r * pcols + col;
-    float acc = pp[0];
-    for (int k = 1; k < KS; ++k) acc += pp[k * pstride];
-    sq[q][e] = (float)(_Float16)(acc + bias[col]);
+  constexpr int QI = (NQ * 64 + 255) / 256;
+  float pq[QI][8];
+#pragma unroll
+  for (int i = 0; i < QI; ++i) {
+    const int t = tid + 256 * i;
+    const int q = min(t >> 6, NQ - 1), e = t & 63;
+    const float* pp = P + (long)min(row0 + q, R - 1) * pcols + h * 64 + e;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) pq[i][k] = pp[min(k, KS - 1) * pstride];
   }
   LOADROWS(ka, K, 0, 0)
+#pragma unroll
+  for (int i = 0; i < QI; ++i) {
+    const int t = tid + 256 * i;
+    if (t < NQ * 64) {
+      const int q = t >> 6, e = t & 63;
+      float acc = pq[i][0];
+#pragma unroll
+      for (int k = 1; k < 8; ++k) acc += k < KS ? pq[i][k] : 0.0f;
+      sq[q][e] = (float)(_Float16)(acc + bias[h * 64 + e]);
+    }
+  }
   __syncthreads();
   h2 qh[NQ][4];
 #pragma unroll
