@@ -477,12 +477,13 @@ __global__ __launch_bounds__(1024) void gemm_skinny(int epi, const T* __restrict
   __shared__ f32x4 red[16][MT][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, NW = blockDim.x >> 6;
   const int n0 = blockIdx.x * 16;
-  // row block of 64 (grid.y): per-row arithmetic does not depend on M
-  const int m_base = blockIdx.y * 64;
-  const int Mb = min(64, M - m_base);
+  // row block of 16*MT rows (grid.y): per-row arithmetic does not depend on M
+  // nor on the block size (each output is the same MFMA chain over k)
+  const int m_base = blockIdx.y * 16 * MT;
+  const int Mb = min(16 * MT, M - m_base);
   const int kt0 = wid * KCH;
   const T* wt = Wp + ((long)blockIdx.x * KT + kt0) * 512 + lane * 8;
-  const T* at = Ap + ((long)(blockIdx.y * 4) * KT + kt0) * 512 + lane * 8;
+  const T* at = Ap + ((long)(blockIdx.y * MT) * KT + kt0) * 512 + lane * 8;
   V8 bfr[KCH];
   V8 afr[MT][KCH];
 #pragma unroll
@@ -548,7 +549,7 @@ static bool skinny_launch(int epi, const T* Ap, const T* Wp, int M, int N, int K
                           const EpiParams& P, hipStream_t st) {
   int nw = 0, kch = 0;
   if (!skinny_split(K, nw, kch)) return false;
-  const dim3 g((N + 15) / 16, (M + 63) / 64), b(64 * nw);
+  const dim3 g((N + 15) / 16, (M + 16 * MT - 1) / (16 * MT)), b(64 * nw);
   switch (kch) {
 #define SK(C) \
   case C: gemm_skinny<T, MT, C><<<g, b, 0, st>>>(epi, Ap, Wp, K / 32, M, N, P); return true;
@@ -649,7 +650,12 @@ template int gemm_splitk_partials<__bf16>(const __bf16*, const __bf16*, int, int
 template <typename T>
 bool gemm_decode(int epi, const T* Ap, const T* Wp, int M, int N, int K, const EpiParams& P,
                  hipStream_t st) {
-  const int MT = (std::min(M, 64) + 15) / 16;
+  int MT = (std::min(M, 64) + 15) / 16;
+  // M > 64 (beam / best-of rows): row blocks of 32 rows (32 KB of LDS: 5 workgroups
+  // per CU instead of 2; beam 5 703 -> 729 audio-s/s; A/B: MWX_SKINNY_MT = 2..4;
+  // the A tiles read stay inside the 64-row padded buffers for MT = 2..4)
+  static const int mt_big = getenv("MWX_SKINNY_MT") ? atoi(getenv("MWX_SKINNY_MT")) : 2;
+  if (M > 64 && mt_big >= 2 && mt_big <= 4) MT = mt_big;
   if (MT == 1) return skinny_launch<T, 1>(epi, Ap, Wp, M, N, K, P, st);
   if (MT == 2) return skinny_launch<T, 2>(epi, Ap, Wp, M, N, K, P, st);
   if (MT == 3) return skinny_launch<T, 3>(epi, Ap, Wp, M, N, K, P, st);
