@@ -575,11 +575,11 @@ __global__ __launch_bounds__(256) void gemm_splitk(const T* __restrict__ Ap,
   __shared__ f32x4 red[4][MT][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int n0 = blockIdx.x * 16, ks = blockIdx.y;
-  const int m_base = blockIdx.z * 64;  // row block (64 rows per grid.z slice)
-  const int Mb = min(64, M - m_base);
+  const int m_base = blockIdx.z * 16 * MT;  // row block (16*MT rows per grid.z slice)
+  const int Mb = min(16 * MT, M - m_base);
   const int kt0 = (ks * kslice >> 5) + wid * KCH;
   const T* wt = Wp + ((long)blockIdx.x * KT + kt0) * 512 + lane * 8;
-  const T* at = Ap + ((long)(blockIdx.z * 4) * KT + kt0) * 512 + lane * 8;
+  const T* at = Ap + ((long)(blockIdx.z * MT) * KT + kt0) * 512 + lane * 8;
   V8 bfr[KCH];
   V8 afr[MT][KCH];
 #pragma unroll
@@ -628,8 +628,13 @@ int gemm_splitk_partials(const T* Ap, const T* Wp, int M, int N, int K, float* P
   if (ks == 0) return 0;
   const int kslice = K / ks;
   const int kch = kslice / 128;
-  const int MT = (std::min(M, 64) + 15) / 16;
-  const dim3 g((N + 15) / 16, ks, (M + 63) / 64);
+  int MT = (std::min(M, 64) + 15) / 16;
+  // M > 64 (beam / best-of rows): row blocks of 32 rows (beam 5: 722 -> 742
+  // audio-s/s, fewer A-fragment registers per wave); 16*MT rows with
+  // MWX_SPLITK_MT = 2..4 (A/B; per-row arithmetic is the same in any block)
+  static const int mt_big = getenv("MWX_SPLITK_MT") ? atoi(getenv("MWX_SPLITK_MT")) : 2;
+  if (M > 64 && mt_big >= 2 && mt_big <= 4) MT = mt_big;
+  const dim3 g((N + 15) / 16, ks, (M + 16 * MT - 1) / (16 * MT));
 #define SKL(MTV, C)                                                                       \
   if (MT == MTV && kch == C) {                                                            \
     gemm_splitk<T, MTV, C><<<g, 256, 0, st>>>(Ap, Wp, K / 32, M, N, kslice, P);        \
