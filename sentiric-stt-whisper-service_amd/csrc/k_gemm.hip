@@ -634,6 +634,8 @@ int gemm_splitk_partials(const T* Ap, const T* Wp, int M, int N, int K, float* P
   // MWX_SPLITK_MT = 2..4 (A/B; per-row arithmetic is the same in any block)
   static const int mt_big = getenv("MWX_SPLITK_MT") ? atoi(getenv("MWX_SPLITK_MT")) : 2;
   if (M > 64 && mt_big >= 2 && mt_big <= 4) MT = mt_big;
+  static const bool mt1 = !(getenv("MWX_DEC_MT1") && atoi(getenv("MWX_DEC_MT1")) == 0);
+  if (mt1 && M <= 64) MT = 1;  // 16-row blocks (greedy +3%; MWX_DEC_MT1=0 for A/B)
   const dim3 g((N + 15) / 16, ks, (M + 16 * MT - 1) / (16 * MT));
 #define SKL(MTV, C)                                                                       \
   if (MT == MTV && kch == C) {                                                            \
@@ -661,6 +663,8 @@ bool gemm_decode(int epi, const T* Ap, const T* Wp, int M, int N, int K, const E
   // the A tiles read stay inside the 64-row padded buffers for MT = 2..4)
   static const int mt_big = getenv("MWX_SKINNY_MT") ? atoi(getenv("MWX_SKINNY_MT")) : 2;
   if (M > 64 && mt_big >= 2 && mt_big <= 4) MT = mt_big;
+  static const bool mt1 = !(getenv("MWX_DEC_MT1") && atoi(getenv("MWX_DEC_MT1")) == 0);
+  if (mt1 && M <= 64) MT = 1;  // 16-row blocks (greedy +3%; MWX_DEC_MT1=0 for A/B)
   if (MT == 1) return skinny_launch<T, 1>(epi, Ap, Wp, M, N, K, P, st);
   if (MT == 2) return skinny_launch<T, 2>(epi, Ap, Wp, M, N, K, P, st);
   if (MT == 3) return skinny_launch<T, 3>(epi, Ap, Wp, M, N, K, P, st);
