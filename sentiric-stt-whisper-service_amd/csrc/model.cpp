@@ -437,6 +437,9 @@ static bool arch_hparams(const std::string& arch, Hparams& hp) {
       {"small", 51865, 1500, 768, 12, 12, 448, 768, 12, 12, 80},
       {"medium", 51865, 1500, 1024, 16, 24, 448, 1024, 16, 24, 80},
       {"large-v3", 51866, 1500, 1280, 20, 32, 448, 1280, 20, 32, 128},
+      // large-v3 geometry (d 1280, 20 heads, 128 mels, vocab 51866) with 2 + 2
+      // layers: every large-v3 kernel instantiation at an oracle-checkable cost
+      {"large-v3-l2", 51866, 1500, 1280, 20, 2, 448, 1280, 20, 2, 128},
   };
   for (const auto& a : t) {
     if (arch == a.n) {

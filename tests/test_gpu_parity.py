@@ -88,11 +88,18 @@ def service_params(ctx, beam=1, temperature_inc=0.2, language=b"auto"):
     return p
 
 
-def assert_same(segs, osegs, p_tol=5e-3):
+def assert_same(segs, osegs, p_tol=5e-3, tid_tie_tol=0.0):
     """Token ids, segment text/times and token timestamps must match exactly;
     token probabilities within p_tol (logits agree to ~1e-2 abs for f16: the
     activations are rounded to 16 bits at the same points, only the f32
-    summation order differs; bf16 rounding is 8x coarser)."""
+    summation order differs; bf16 rounding is 8x coarser).
+
+    `tid` (the most likely timestamp token of each text token, a diagnostic
+    field of whisper_token_data the service never reads — it consumes id, p,
+    t0, t1: src/stt_engine.cpp:288-296) must match too, except, with
+    tid_tie_tol > 0, where both sides picked a timestamp token at the same
+    probability within tid_tie_tol: two timestamp tokens tied within the
+    logits' rounding noise (weights whose timestamp logits carry no signal)."""
     ids = [t.id for s in segs for t in s.tokens]
     oids = [t.id for s in osegs for t in s.tokens]
     assert ids == oids, next(((i, a, b) for i, (a, b) in enumerate(zip(ids, oids)) if a != b), None)
@@ -103,7 +110,7 @@ def assert_same(segs, osegs, p_tol=5e-3):
         assert (t.t0, t.t1) == (to.t0, to.t1), (
             f"token {i}: dev t0/t1 {t.t0}/{t.t1} pt {t.pt:.6f} ptsum {t.ptsum:.6f} tid {t.tid} | "
             f"oracle {to.t0}/{to.t1} pt {to.pt:.6f} ptsum {to.ptsum:.6f} tid {to.tid}")
-        assert t.tid == to.tid
+        assert t.tid == to.tid or abs(t.pt - to.pt) < tid_tie_tol, (i, t, to)
         assert abs(t.p - to.p) < p_tol and abs(t.plog - to.plog) < 2 * p_tol, (i, t, to)
 
 
