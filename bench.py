@@ -149,11 +149,7 @@ def prosody_bench(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dist = init_dist(world, local)
     import shard
     clips = args.clips if args.clips != 32 else 256
     n_samp = int(args.clip_seconds * 16000)
@@ -270,9 +266,110 @@ def prosody_cpu_baseline(pcm, desc, budget_s=10.0):
             "sample": f"first {i} segments ({done_s:.0f} s of audio), one thread"}
 
 
+def gather_summary(block, clips, per_clip):
+    """Rank 0's view of the last step's record gather: clips received and
+    whether every clip carries its full fixed-length token record."""
+    import shard
+    if block is None:
+        return None
+    recs = shard.unpack_records(block)
+    return {"clips": len(recs), "tokens": sum(len(r) for r in recs),
+            "complete": len(recs) == clips and all(len(r) == per_clip for r in recs)}
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` outside torch.distributed.run: start N fresh rank
+    processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, one GPU each)
+    before this process touches the GPU, wait for all of them and return the
+    first failing exit status (0 if all succeeded). Rank 0 prints the line."""
+    import signal
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0 and rc == 0:
+                rc = r
+                for q in live:  # a failed rank leaves its peers blocked in a collective
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.05)
+    return rc
+
+
+def init_dist(world, local):
+    """torch.distributed over RCCL (backend "nccl") when the rank has a GPU,
+    gloo otherwise (the CPU tests of the launcher / gather path)."""
+    if world <= 1:
+        return None
+    import torch
+    import torch.distributed as dist
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    else:
+        dist.init_process_group("gloo")
+    return dist
+
+
+def dry_run(args, world, rank, local):
+    """--dry-run: the launcher, process group and rank-ordered record gather
+    of the real run with the transcription replaced by deterministic
+    synthetic records (no engine, no GPU needed); rank 0 checks that the
+    gathered records are every rank's, in rank order."""
+    import shard
+    dist = init_dist(world, local)
+    dev = "cuda" if dist is not None and dist.get_backend() == "nccl" else None
+
+    def recs(c):
+        rng = np.random.default_rng(1000 + c)
+        n = int(rng.integers(1, args.decode_steps + 1))
+        return [(int(rng.integers(0, 51866)), 2 * j, 2 * j + 2, float(rng.random())) for j in range(n)]
+
+    ids = shard.clip_ids(rank, args.clips)
+    block = shard.pack_records([recs(c) for c in ids], args.decode_steps)
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    g = shard.gather_to_rank0(dist, block, device=dev)
+    elapsed = time.perf_counter() - t0
+    if rank == 0:
+        got = shard.unpack_records(g)
+        want = [recs(c) for r in range(world) for c in shard.clip_ids(r, args.clips)]
+        ok = len(got) == len(want) and all(
+            [(a, b, c) for a, b, c, _ in x] == [(a, b, c) for a, b, c, _ in y] and
+            np.allclose([p for *_, p in x], [p for *_, p in y], rtol=0, atol=1e-7)
+            for x, y in zip(got, want))
+        print(json.dumps({"metric": METRIC, "dry_run": True, "n_gpus": world,
+                          "backend": dist.get_backend() if dist is not None else None,
+                          "gathered_clips": len(got), "gather_rank_order_ok": bool(ok),
+                          "gather_ms": round(elapsed * 1e3, 3)}), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one GPU each); without torch.distributed.run, bench.py starts "
+                         "them itself")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher + record gather only, synthetic records (no GPU needed)")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--arch", default="large-v3")
@@ -294,18 +391,21 @@ def main():
     ap.add_argument("--prosody", action="store_true",
                     help="segment-prosody leg (SURVEY.md §8 f4) instead of transcription")
     args = ap.parse_args()
-    if args.prosody:
-        return prosody_bench(args)
-
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus > 1 and world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
+    if args.dry_run:
+        return dry_run(args, world, rank, local)
+    if args.prosody:
+        return prosody_bench(args)
+
     import torch
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dist = init_dist(world, local)
 
     def barrier():
         if dist is not None:
@@ -353,9 +453,9 @@ def main():
         rc = run_batch()
         if rc != 0:
             raise RuntimeError(f"mwx_full_batch rc={rc}")
-        block = shard.pack_tokens([mwx.token_ids(ctx.segments(c)) for c in range(args.clips)],
-                                  max_tok)
-        # RCCL over xGMI: every rank's token streams to rank 0
+        block = shard.pack_records([[(t.id, t.t0, t.t1, t.p) for s in ctx.segments(c)
+                                     for t in s.tokens] for c in range(args.clips)], max_tok)
+        # RCCL over xGMI: every rank's token records (id, t0, t1, p) to rank 0
         g = shard.gather_to_rank0(dist, block, device="cuda")
         if g is not None:
             gathered["tokens"] = g
@@ -471,6 +571,7 @@ def main():
             "audio_sec_per_s_per_gpu": round(value / world, 2),
             "rtf": round(elapsed / audio_s * world, 6),
             "x_realtime_per_gpu": round(value / world, 1),
+            "gathered": gather_summary(gathered.get("tokens"), world * args.clips, max_tok),
             "roofline": roof,
             "roofline_encoder": roof_enc,
             "cpu_baseline": cpu,
@@ -482,4 +583,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -4,14 +4,21 @@ One process per GPU; rank r owns clips [r*n, (r+1)*n) (weights replicated, no
 collective on the data path). The only exchange is the final gather of every
 rank's fixed-size token records to rank 0 — an all-gather over RCCL/xGMI on
 the GPU box (backend "nccl"), over gloo in the CPU tests.
+
+Record layout (int32, one row per clip): column 0 = token count, then
+RECORD_FIELDS words per token: id, t0, t1 (10-ms ticks) and p (the raw f32
+bits) — the fields SttEngine reads from whisper_token_data
+(src/stt_engine.cpp:288-296).
 """
 from __future__ import annotations
 
-from typing import List, Optional, Sequence
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
 RECORD_FIELDS = 4  # id, t0, t1, p (as raw f32 bits) per token
+
+Record = Tuple[int, int, int, float]
 
 
 def clip_ids(rank: int, clips_per_rank: int) -> List[int]:
@@ -19,19 +26,40 @@ def clip_ids(rank: int, clips_per_rank: int) -> List[int]:
     return list(range(rank * clips_per_rank, (rank + 1) * clips_per_rank))
 
 
-def pack_tokens(per_clip: Sequence[Sequence[int]], max_tokens: int) -> np.ndarray:
-    """Fixed-size int32 [clips][max_tokens + 1] block: column 0 = token count,
-    then the ids (zero padded), so ranks gather equal-sized tensors."""
-    out = np.zeros((len(per_clip), max_tokens + 1), np.int32)
-    for c, ids in enumerate(per_clip):
-        ids = list(ids)[:max_tokens]
-        out[c, 0] = len(ids)
-        out[c, 1:1 + len(ids)] = ids
+def pack_records(per_clip: Sequence[Sequence[Record]], max_tokens: int) -> np.ndarray:
+    """Fixed-size int32 [clips][1 + RECORD_FIELDS * max_tokens] block so every
+    rank gathers an equal-sized tensor. A clip with more than max_tokens
+    tokens raises: a truncated gather would silently drop transcript."""
+    out = np.zeros((len(per_clip), 1 + RECORD_FIELDS * max_tokens), np.int32)
+    for c, recs in enumerate(per_clip):
+        recs = list(recs)
+        if len(recs) > max_tokens:
+            raise ValueError(f"clip {c}: {len(recs)} tokens exceed the record capacity {max_tokens}")
+        out[c, 0] = len(recs)
+        if recs:
+            a = np.array([(i, t0, t1, 0) for i, t0, t1, _ in recs], np.int64).astype(np.int32)
+            a[:, 3] = np.array([p for *_, p in recs], np.float32).view(np.int32)
+            out[c, 1:1 + RECORD_FIELDS * len(recs)] = a.reshape(-1)
     return out
 
 
+def unpack_records(block: np.ndarray) -> List[List[Record]]:
+    out = []
+    for row in np.asarray(block, np.int32):
+        n = int(row[0])
+        a = row[1:1 + RECORD_FIELDS * n].reshape(n, RECORD_FIELDS)
+        p = a[:, 3].copy().view(np.float32)
+        out.append([(int(a[j, 0]), int(a[j, 1]), int(a[j, 2]), float(p[j])) for j in range(n)])
+    return out
+
+
+def pack_tokens(per_clip: Sequence[Sequence[int]], max_tokens: int) -> np.ndarray:
+    """Token ids only (t0 = t1 = -1, p = 0): pack_records of bare ids."""
+    return pack_records([[(int(i), -1, -1, 0.0) for i in ids] for ids in per_clip], max_tokens)
+
+
 def unpack_tokens(block: np.ndarray) -> List[List[int]]:
-    return [list(map(int, row[1:1 + int(row[0])])) for row in block]
+    return [[r[0] for r in recs] for recs in unpack_records(block)]
 
 
 def gather_to_rank0(dist, block: np.ndarray, device: Optional[str] = None) -> Optional[np.ndarray]:

@@ -2,8 +2,10 @@
 sharding is disjoint and complete, and the token gather delivers every rank's
 records to rank 0 in rank order (the same shard.gather_to_rank0 bench.py runs
 over RCCL on the GPU box)."""
+import json
 import os
 import socket
+import subprocess
 import sys
 
 import numpy as np
@@ -47,10 +49,16 @@ def test_clip_sharding_disjoint_and_complete():
 
 
 def test_pack_unpack_roundtrip():
-    toks = [[1, 2, 3], [], list(range(300))]
+    toks = [[1, 2, 3], [], list(range(220))]
     b = shard.pack_tokens(toks, 220)
-    assert b.shape == (3, 221)
-    assert shard.unpack_tokens(b) == [[1, 2, 3], [], list(range(220))]
+    assert b.shape == (3, 1 + shard.RECORD_FIELDS * 220)
+    assert shard.unpack_tokens(b) == toks
+    recs = [[(50365, 0, 12, 0.5), (7, 12, 40, 0.123456789)], []]
+    got = shard.unpack_records(shard.pack_records(recs, 4))
+    assert got[1] == [] and [r[:3] for r in got[0]] == [r[:3] for r in recs[0]]
+    assert [r[3] for r in got[0]] == [float(np.float32(r[3])) for r in recs[0]]
+    with pytest.raises(ValueError):  # truncation fails loudly
+        shard.pack_records([[(1, 0, 0, 0.0)] * 5], 4)
 
 
 @pytest.mark.timeout(120)
@@ -72,3 +80,73 @@ def test_gloo_world2_gather_to_rank0():
     got = shard.unpack_tokens(np.array(res[0][1], np.int32))
     want = [_fake_tokens(c, max_tok) for r in range(world) for c in shard.clip_ids(r, clips)]
     assert got == want
+
+
+def _oracle_records(model_path, clip_id):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import mwx
+    import orc
+    o = orc.Oracle(model_path, threads=2)
+    opt = orc.FullOptions.service_defaults()
+    opt.temperature_inc = 0.0
+    opt.language = "en"
+    pcm = mwx.pcm16_to_f32(mwx.synth_pcm16(clip_id, 8 * 16000))
+    _, segs, _, _ = o.full(pcm, opt)
+    o.close()
+    return [(t.id, t.t0, t.t1, t.p) for sg in segs for t in sg.tokens]
+
+
+def _oracle_worker(rank, world, port, clips, max_tok, model_path, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    block = shard.pack_records([_oracle_records(model_path, c) for c in shard.clip_ids(rank, clips)],
+                               max_tok)
+    g = shard.gather_to_rank0(dist, block)
+    q.put((rank, None if g is None else g.tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_gloo_world2_gathers_transcription_records(make_model):
+    """Each rank transcribes its own clips (the CPU oracle standing in for the
+    engine: no GPU here) and gathers full token records (id, t0, t1, p) to
+    rank 0, which receives every clip's records in rank order, bit for bit."""
+    import torch.multiprocessing as mp
+    path = make_model("micro-rich")
+    world, clips, max_tok = 2, 2, 448
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_oracle_worker, args=(r, world, port, clips, max_tok, path, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=280) for _ in range(world))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert res[1] is None
+    got = shard.unpack_records(np.array(res[0], np.int32))
+    want = [_oracle_records(path, c) for r in range(world) for c in shard.clip_ids(r, clips)]
+    assert got == [[(i, a, b, float(np.float32(p))) for i, a, b, p in w] for w in want]
+    assert all(len(w) > 0 for w in want)
+
+
+@pytest.mark.timeout(300)
+def test_bench_gpus2_launches_two_ranks():
+    """`bench.py --gpus 2` without torch.distributed.run starts two rank
+    processes itself (RANK / WORLD_SIZE / MASTER_* set before any GPU call in
+    the parent); here, with no GPU, over gloo and with synthetic records."""
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run",
+                        "--clips", "3", "--decode-steps", "20"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    line = lines[0]
+    assert line["n_gpus"] == 2 and line["gathered_clips"] == 6 and line["gather_rank_order_ok"]
