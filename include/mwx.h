@@ -22,6 +22,8 @@
  *   mwx_token_to_str                      <- whisper_token_to_str                src/stt_engine.cpp:289
  *   mwx_token_eot                         <- whisper_token_eot                   src/stt_engine.cpp:290
  *   mwx_log_set                           <- whisper_log_set                     src/main.cpp:71
+ *   mwx_resample                          <- SttEngine::resample_audio (libsamplerate
+ *                                            src_simple, SRC_SINC_FASTEST) src/stt_engine.cpp:87-106
  *
  * New (no whisper.h counterpart): mwx_full_batch runs B independent clips in one
  * batched GPU pass (the data-parallel unit of this engine), and
@@ -275,6 +277,22 @@ int mwx_prosody_batch_device(struct mwx_context* ctx, struct mwx_state* state,
                              const float* d_pcm, const int64_t* d_desc, int n_seg,
                              int64_t total_frames, int sample_rate,
                              const mwx_prosody_params* params, mwx_prosody* d_out);
+
+/* --- resampling -------------------------------------------------------------
+ * SttEngine::resample_audio (src/stt_engine.cpp:87-106, called for every
+ * request whose sample rate is not 16 kHz, :138-145): libsamplerate's
+ * src_simple(SRC_SINC_FASTEST, mono, end_of_input = 0) restated on the GPU —
+ * the same output count (the converter holds back the last filter half-width
+ * of input) and alignment; the coefficient table is a reconstruction of the
+ * "fastest" table's geometry (libsamplerate is absent, parity unpinned).
+ * `in` / `out` may be host or device memory of the context's GPU. Returns the
+ * frames generated (the reference's output_frames_gen; 0 when
+ * src_rate == dst_rate or n_in == 0, where the reference keeps the input), or
+ * < 0 on bad arguments / a ratio outside libsamplerate's [1/256, 256] / a
+ * device error. Runs on the state's stream; synchronous. */
+long mwx_resample_max_frames(int n_in, int src_rate, int dst_rate); /* (long)(n_in*ratio)+100 */
+int mwx_resample(struct mwx_context* ctx, struct mwx_state* state, const float* in, int n_in,
+                 int src_rate, int dst_rate, float* out, int out_cap);
 
 /* --- vocabulary / model ------------------------------------------------- */
 const char* mwx_token_to_str(struct mwx_context* ctx, mwx_token token);

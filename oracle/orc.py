@@ -81,6 +81,8 @@ def lib() -> C.CDLL:
     L.orc_full_window_tokens.argtypes = [P, C.c_int, C.POINTER(C.c_int), C.c_int]
     L.orc_prosody.restype = None
     L.orc_prosody.argtypes = [fp, C.c_int64, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, P]
+    L.orc_resample.restype = C.c_long
+    L.orc_resample.argtypes = [fp, C.c_long, C.c_int, C.c_int, fp, C.c_long]
     L.orc_clusterer_new.restype = P
     L.orc_clusterer_new.argtypes = [C.c_float]
     L.orc_clusterer_free.argtypes = [P]
@@ -353,3 +355,19 @@ class Clusterer:
             lib().orc_clusterer_free(self.h)
             self.h = None
 
+
+
+# ---------------------------------------------------------------------------
+# Resampling (resample_oracle.cpp; SttEngine::resample_audio, src/stt_engine.cpp:87-106)
+# ---------------------------------------------------------------------------
+def resample(pcm: np.ndarray, src_rate: int, dst_rate: int) -> Optional[np.ndarray]:
+    """libsamplerate src_simple(SRC_SINC_FASTEST, 1, end_of_input = 0) restated;
+    None where the reference returns an empty buffer (same rate, empty input)
+    and keeps the original."""
+    a = np.ascontiguousarray(pcm, np.float32)
+    cap = int(len(a) * (dst_rate / src_rate)) + 100
+    out = np.empty(max(cap, 1), np.float32)
+    n = lib().orc_resample(_fp(a), len(a), src_rate, dst_rate, _fp(out), cap)
+    if n < 0:
+        raise ValueError(f"orc_resample failed ({n})")
+    return out[:n].copy() if n > 0 else None

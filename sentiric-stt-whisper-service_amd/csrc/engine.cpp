@@ -131,6 +131,7 @@ struct State {
   DBuf aq, as;  // MX-fp8 activations (codes [rows][K], scales [rows][K/32])
   DBuf ibuf;  // small int arrays (slot maps)
   DBuf pro_pcm, pro_desc, pro_fs, pro_ft, pro_fc, pro_out;  // segment prosody
+  DBuf rs_in, rs_out, rs_pos, rs_coef;                      // resampler
   // pinned host staging of the per-step decode control / result records
   // (DMA straight from / to page-locked memory: no runtime bounce buffer)
   void* pin = nullptr;

@@ -228,6 +228,16 @@ void sample_draws(const float* probs, const float* logprobs, int V, const double
                   const int* ndraw, int KD, Draw* out, int* need, int R, hipStream_t st,
                   int force_exact = -1);
 
+// Sinc resampler (k_resample.hip): libsamplerate SRC_SINC_FASTEST's filter
+// sum per output sample; fixed-point filter indices with 12 fractional bits
+// (src_sinc.c SHIFT_BITS).
+constexpr int RS_SHIFT = 12;
+constexpr int RS_FRAC_MASK = (1 << RS_SHIFT) - 1;
+constexpr double RS_INV_FP_ONE = 1.0 / (double)(1 << RS_SHIFT);
+void resample_launch(const float* in, int half, const float* coeffs, int coeff_half_len,
+                     int increment, double scale, const int2* pos, int n_out, float* out,
+                     hipStream_t st);
+
 // Segment prosody (k_prosody.hip): reference extract_prosody per segment.
 struct ProsodySeg {
   long start;      // first sample in the clip

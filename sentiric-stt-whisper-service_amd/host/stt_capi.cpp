@@ -3,6 +3,7 @@
 // be a partial UTF-8 sequence).
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <string>
 
 #include "stt_engine.h"
@@ -154,12 +155,29 @@ void* mwx_stt_new_ex(const char* model_dir, const char* model_filename, int para
 
 // StreamSession over an engine: feed one chunk (len 0 = end of speech);
 // returns the events as JSON (strings hex-encoded) like mwx_stt_transcribe_pcm16.
-void* mwx_stt_stream_new(void* eng) { return new StreamSession(*static_cast<SttEngine*>(eng)); }
-void mwx_stt_stream_free(void* s) { delete static_cast<StreamSession*>(s); }
+// If `cap` is too small the chunk is still consumed: the events are kept and
+// -(needed + 2) is returned; mwx_stt_stream_drain then delivers them (never
+// feed the chunk again).
+struct StreamHandle {
+  explicit StreamHandle(SttEngine& e) : session(e) {}
+  StreamSession session;
+  std::string pending;  // undelivered events JSON
+};
+void* mwx_stt_stream_new(void* eng) { return new StreamHandle(*static_cast<SttEngine*>(eng)); }
+void mwx_stt_stream_free(void* s) { delete static_cast<StreamHandle*>(s); }
+
+int mwx_stt_stream_drain(void* s, char* out, int cap) {
+  StreamHandle* h = static_cast<StreamHandle*>(s);
+  const int r = emit(h->pending.empty() ? std::string("[]") : h->pending, out, cap);
+  if (r >= 0) h->pending.clear();
+  return r < -1 ? r - 2 : r;
+}
 
 int mwx_stt_stream_feed(void* s, const uint8_t* data, int len, char* out, int cap) {
+  StreamHandle* h = static_cast<StreamHandle*>(s);
+  if (!h->pending.empty()) return -1;  // undelivered events: drain first
   try {
-    const auto evs = static_cast<StreamSession*>(s)->feed(data, len > 0 ? (size_t)len : 0);
+    const auto evs = h->session.feed(data, len > 0 ? (size_t)len : 0);
     std::string o = "[";
     char buf[512];
     for (size_t i = 0; i < evs.size(); ++i) {
@@ -190,6 +208,7 @@ int mwx_stt_stream_feed(void* s, const uint8_t* data, int len, char* out, int ca
     }
     o += "]";
     const int r = emit(o, out, cap);
+    if (r < -1) h->pending = o;
     return r < -1 ? r - 2 : r;
   } catch (const EngineBusyException&) {
     return -2;
@@ -203,7 +222,38 @@ long mwx_stt_batches(void* eng) { return static_cast<SttEngine*>(eng)->batches_r
 void mwx_stt_free(void* eng) { delete static_cast<SttEngine*>(eng); }
 
 // 0.. = JSON length written; -1 = error; -2 = EngineBusyException;
-// < -2 = -(needed capacity)
+// < -2 = -(needed capacity). abort_after >= 0: RequestOptions::should_abort
+// answers true from its (abort_after + 1)-th call on (the service's abort
+// hook, src/stt_engine.cpp:17-23,215-219); < 0: no abort callback.
+int mwx_stt_transcribe_pcm16_ex(void* eng, const int16_t* pcm, int n, int sample_rate,
+                                const char* language, int beam_size, float temperature, char* out,
+                                int cap, double* metrics3, int abort_after, int* abort_calls) {
+  RequestOptions o;
+  o.language = language ? language : "";
+  o.beam_size = beam_size;
+  o.temperature = temperature;
+  auto calls = std::make_shared<int>(0);
+  if (abort_after >= 0)
+    o.should_abort = [calls, abort_after] { return (*calls)++ >= abort_after; };
+  SttEngine::PerformanceMetrics m{0, 0, 0};
+  try {
+    const auto rs = static_cast<SttEngine*>(eng)->transcribe_pcm16(
+        std::vector<int16_t>(pcm, pcm + n), sample_rate, o, &m);
+    if (metrics3) {
+      metrics3[0] = m.queue_time_ms;
+      metrics3[1] = m.processing_time_ms;
+      metrics3[2] = m.token_count;
+    }
+    if (abort_calls) *abort_calls = *calls;
+    const int r = emit(to_json(rs), out, cap);
+    return r < -1 ? r - 2 : r;
+  } catch (const EngineBusyException&) {
+    return -2;
+  } catch (...) {
+    return -1;
+  }
+}
+
 int mwx_stt_transcribe_pcm16(void* eng, const int16_t* pcm, int n, int sample_rate,
                              const char* language, int beam_size, float temperature, char* out,
                              int cap, double* metrics3) {

@@ -90,6 +90,9 @@ SttEngine::SttEngine(const Settings& settings) : settings_(settings) {
   cp.gpu_device = settings_.gpu_device;
   ctx_ = mwx_init_from_file_with_params(path.c_str(), cp);
   if (!ctx_) throw std::runtime_error("Whisper model initialization failed");
+  aux_state_ = mwx_init_state(ctx_);
+  if (!aux_state_) throw std::runtime_error("Whisper state initialization failed");
+  all_states_.push_back(aux_state_);
   const int pool = std::max(1, settings_.parallel_requests);
   if (settings_.max_batch > 1) {
     // one batcher thread per pool slot, each with its own max_batch states
@@ -147,7 +150,9 @@ std::vector<TranscriptionResult> SttEngine::transcribe_batched(const std::vector
   req->t_enq = std::chrono::steady_clock::now();
   std::unique_lock<std::mutex> lock(q_mutex_);
   queue_.push_back(req);
-  q_cv_.notify_one();
+  // every batcher: one already gathering another key would swallow a single
+  // wakeup while an idle batcher sleeps
+  q_cv_.notify_all();
   // EngineBusyException when no batcher picks the request up in time
   // (the state-pool queue timeout of src/stt_engine.cpp:63-85)
   if (!done_cv_.wait_for(lock, std::chrono::milliseconds(settings_.request_queue_timeout_ms),
@@ -199,6 +204,9 @@ void SttEngine::batcher_loop(std::vector<mwx_state*> states) {
           ++it;
         }
       }
+      // requests left behind (other keys, or beyond max_batch) go to an idle
+      // batcher now rather than after this batch
+      if (!queue_.empty()) q_cv_.notify_all();
     }
     done_cv_.notify_all();
     if (batch.empty()) continue;
@@ -391,7 +399,12 @@ std::vector<TranscriptionResult> SttEngine::transcribe(const std::vector<float>&
   const auto t_start = std::chrono::steady_clock::now();
   if (!ctx_) return {};
   if (options.should_abort && options.should_abort()) return {};
-  (void)input_sample_rate;  // non-16 kHz input is passed through (see header)
+  // src/stt_engine.cpp:136-145: non-16 kHz input is resampled; an empty
+  // result (failure) keeps the original buffer
+  std::vector<float> resampled;
+  if (input_sample_rate != 16000)
+    resampled = resample_audio(pcmf32.data(), pcmf32.size(), input_sample_rate, 16000);
+  if (!resampled.empty()) return transcribe(resampled, 16000, options, out_metrics);
   const size_t pcm_size = pcmf32.size();
   const size_t min_samples = static_cast<size_t>((settings_.vad_ms_min_duration * 16000) / 1000);
   if (pcm_size < min_samples) {
@@ -419,20 +432,41 @@ std::vector<TranscriptionResult> SttEngine::transcribe(const std::vector<float>&
                  out_metrics ? &out_metrics->token_count : nullptr);
 }
 
+std::vector<float> SttEngine::resample_audio(const float* input, size_t input_size, int src_rate,
+                                             int target_rate) {
+  if (src_rate == target_rate || input_size == 0) return {};
+  const long cap = mwx_resample_max_frames(static_cast<int>(input_size), src_rate, target_rate);
+  if (cap <= 0) return {};
+  std::vector<float> out(static_cast<size_t>(cap));
+  int n = 0;
+  {
+    std::lock_guard<std::mutex> lock(aux_mutex_);
+    n = mwx_resample(ctx_, aux_state_, input, static_cast<int>(input_size), src_rate, target_rate,
+                     out.data(), static_cast<int>(cap));
+  }
+  if (n <= 0) {
+    std::fprintf(stderr, "SttEngine: resampling %d -> %d Hz failed (%d)\n", src_rate, target_rate, n);
+    return {};
+  }
+  out.resize(static_cast<size_t>(n));
+  return out;
+}
+
 std::vector<std::vector<TranscriptionResult>> SttEngine::transcribe_batch(
     const std::vector<std::vector<float>>& clips, const RequestOptions& options) {
   std::vector<std::vector<TranscriptionResult>> out(clips.size());
   if (!ctx_ || clips.empty()) return out;
-  std::vector<mwx_state*> states;
+  std::lock_guard<std::mutex> batch_lock(batch_mutex_);
+  while (batch_states_.size() < clips.size()) {
+    mwx_state* st = mwx_init_state(ctx_);
+    if (!st) return out;
+    batch_states_.push_back(st);
+    all_states_.push_back(st);
+  }
+  std::vector<mwx_state*> states(batch_states_.begin(), batch_states_.begin() + clips.size());
   std::vector<const float*> ptrs;
   std::vector<int> lens;
   for (const auto& c : clips) {
-    mwx_state* st = mwx_init_state(ctx_);
-    if (!st) {
-      for (mwx_state* s : states) mwx_free_state(s);
-      return out;
-    }
-    states.push_back(st);
     ptrs.push_back(c.data());
     lens.push_back(static_cast<int>(c.size()));
   }
@@ -448,7 +482,6 @@ std::vector<std::vector<TranscriptionResult>> SttEngine::transcribe_batch(
         out[b] = collect(states[b], lang, clips[b].data(), clips[b].size(), options.prosody_opts,
                          nullptr);
   }
-  for (mwx_state* s : states) mwx_free_state(s);
   return out;
 }
 

@@ -9,9 +9,11 @@
 // phrases, tokens with id >= eot skipped, average token p < 0.40 drops the
 // segment), per-segment prosody (src/stt_engine.cpp:313-337: computed on the
 // GPU by mwx_prosody_batch, bit-identical to src/prosody_extractor.cpp) and
-// speaker clustering (src/speaker_cluster.cpp, restated below). Out of scope
-// (SURVEY.md §8): VAD and resampling (non-16 kHz input is passed through, as
-// the reference does when libsamplerate fails, :141).
+// speaker clustering (src/speaker_cluster.cpp, restated below), and
+// resampling of non-16 kHz input (resample_audio, :87-106, :138-145: on the
+// GPU by mwx_resample; the input is kept when resampling yields nothing, as
+// the reference keeps it when libsamplerate fails, :141). Out of scope
+// (SURVEY.md §8): VAD.
 #pragma once
 
 #include <atomic>
@@ -174,10 +176,18 @@ class SttEngine {
                                                     const RequestOptions& options,
                                                     PerformanceMetrics* out_metrics = nullptr);
 
-  // Batched entry (no reference counterpart): B independent clips in one GPU
-  // pass, each result list filtered exactly as transcribe() filters it.
+  // Batched entry (no reference counterpart): B independent 16 kHz clips in
+  // one GPU pass, each result list filtered exactly as transcribe() filters
+  // it. Runs on states kept for batch calls (grown on demand, reused; one
+  // batch call at a time).
   std::vector<std::vector<TranscriptionResult>> transcribe_batch(
       const std::vector<std::vector<float>>& clips, const RequestOptions& options);
+
+  // SttEngine::resample_audio (src/stt_engine.cpp:87-106) on the GPU
+  // (mwx_resample): empty when src_rate == target_rate, the input is empty or
+  // resampling fails — the caller then keeps its input, as the reference does.
+  std::vector<float> resample_audio(const float* input, size_t input_size, int src_rate,
+                                    int target_rate);
 
   // Batches run by the request batcher so far (max_batch > 1).
   long batches_run() const { return batches_run_.load(); }
@@ -222,6 +232,10 @@ class SttEngine {
   std::mutex pool_mutex_;
   std::condition_variable pool_cv_;
   std::vector<mwx_state*> all_states_;
+  mwx_state* aux_state_ = nullptr;  // resampling (its own stream)
+  std::mutex aux_mutex_;
+  std::vector<mwx_state*> batch_states_;  // transcribe_batch
+  std::mutex batch_mutex_;
 
   struct StateGuard {
     SttEngine& engine;

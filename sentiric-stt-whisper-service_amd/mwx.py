@@ -200,6 +200,10 @@ def lib() -> C.CDLL:
     L.mwx_test_sample_draws.argtypes = [P, fpp, fpp, C.c_int, C.c_int, C.POINTER(C.c_double),
                                         C.POINTER(C.c_int), C.c_int, C.c_int, C.c_int,
                                         C.POINTER(C.c_int), C.POINTER(C.c_double)]
+    L.mwx_resample_max_frames.restype = C.c_long
+    L.mwx_resample_max_frames.argtypes = [C.c_int, C.c_int, C.c_int]
+    L.mwx_resample.restype = C.c_int
+    L.mwx_resample.argtypes = [P, P, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int]
     L.mwx_prosody_default_params.restype = ProsodyParams
     L.mwx_prosody_default_params.argtypes = []
     i64p = C.POINTER(C.c_int64)
@@ -433,6 +437,24 @@ class Context:
         if rc != 0:
             raise RuntimeError(f"mwx_prosody_batch failed ({rc})")
         return list(out)[:len(st)]
+
+    def resample(self, pcm, src_rate: int, dst_rate: int = 16000, state_index: int = 0):
+        """mwx_resample (SttEngine::resample_audio on the GPU): the 16 kHz
+        samples, or None where the reference returns an empty buffer (equal
+        rates, empty input). `pcm` may be a numpy array or a DevicePCM."""
+        L = lib()
+        if isinstance(pcm, DevicePCM):
+            ptr, n = pcm.ptr, pcm.n
+        else:
+            a = np.ascontiguousarray(pcm, np.float32)
+            ptr, n = a.ctypes.data, len(a)
+        cap = L.mwx_resample_max_frames(n, src_rate, dst_rate)
+        out = np.empty(max(cap, 1), np.float32)
+        r = L.mwx_resample(self.ctx, self.state(state_index), ptr, n, src_rate, dst_rate,
+                           out.ctypes.data, cap)
+        if r < 0:
+            raise RuntimeError(f"mwx_resample failed ({r})")
+        return out[:r].copy() if r > 0 else None
 
     def test_sample_draws(self, probs: np.ndarray, logprobs: np.ndarray, u: np.ndarray,
                           ndraw: np.ndarray, exact: bool = False, reps: int = 1):

@@ -1,0 +1,184 @@
+"""Resampling of non-16 kHz requests (SttEngine::resample_audio,
+src/stt_engine.cpp:87-106, called at :138-145 for every request whose sample
+rate is not 16 kHz; the unary gRPC and HTTP paths pass the WAV's own rate,
+src/grpc_server.cpp:59, src/http_server.cpp:166).
+
+The reference uses libsamplerate's SRC_SINC_FASTEST, which is not in the
+image: oracle/resample_oracle.cpp restates its sinc converter with a
+reconstructed coefficient table (parity with libsamplerate unpinned). CPU
+tests pin the restatement's behaviour (output length of src_simple with
+end_of_input = 0, alignment, passband, stop band); GPU tests hold the device
+resampler to the restatement bit for bit and SttEngine at 8 and 48 kHz to
+the oracle transcribing the restated 16 kHz signal."""
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import mwx
+import orc
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+RATES = (8000, 11025, 22050, 44100, 48000, 96000)
+
+
+def tone(sr, f, seconds=1.0, amp=0.5):
+    t = np.arange(int(sr * seconds)) / sr
+    return (amp * np.sin(2 * np.pi * f * t)).astype(np.float32)
+
+
+def half_len(sr):
+    ratio = 16000 / sr
+    count = 2464 / 128
+    if ratio < 1:
+        count /= ratio
+    return int(np.rint(count)) + 1
+
+
+@pytest.mark.parametrize("sr", RATES)
+def test_oracle_output_length_and_alignment(sr):
+    """src_simple with end_of_input = 0 holds back the input's last
+    half-filter width: outputs exist for input positions < n - half; output
+    n sits at input position n / ratio (no delay)."""
+    x = tone(sr, 300.0, 1.5)
+    y = orc.resample(x, sr, 16000)
+    ratio = 16000 / sr
+    pos = np.arange(len(y)) / ratio
+    assert np.all(pos < len(x) - half_len(sr))
+    assert (len(y) / ratio) >= len(x) - half_len(sr) - 1 / ratio - 1e-9
+    ref = tone(16000, 300.0, 2.0)[:len(y)]
+    core = slice(64, len(y) - 64)
+    assert np.abs(y[core] - ref[core]).max() < 2e-4
+
+
+def test_oracle_identity_and_errors():
+    x = tone(16000, 300.0)
+    assert orc.resample(x, 16000, 16000) is None  # reference: {} -> input kept
+    assert orc.resample(x[:0], 48000, 16000) is None
+    with pytest.raises(ValueError):
+        orc.resample(x, 16000 * 300, 16000)  # ratio below 1/256
+
+
+@pytest.mark.parametrize("sr", (44100, 48000))
+def test_oracle_stop_band(sr):
+    """A tone above 8 kHz (the 16 kHz Nyquist) is removed, not folded back."""
+    y = orc.resample(tone(sr, 11000.0, 1.0), sr, 16000)
+    assert np.abs(y[200:-200]).max() < 0.5 * 10 ** (-60 / 20)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sr", RATES)
+def test_device_resampler_matches_oracle_bit_exact(make_model, sr):
+    path = make_model("micro")
+    rng = np.random.default_rng(sr)
+    x = (rng.standard_normal(int(sr * 3.7) + 3) * 0.2).astype(np.float32)
+    with mwx.Context.open(path) as ctx:
+        got = ctx.resample(x, sr, 16000)
+        dev = ctx.upload(x)
+        try:
+            got_dev = ctx.resample(dev, sr, 16000)
+        finally:
+            dev.free()
+        assert ctx.resample(x, 16000, 16000) is None
+    want = orc.resample(x, sr, 16000)
+    assert got.shape == want.shape
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(got_dev, want)
+
+
+def _stt_lib():
+    L = C.CDLL(os.path.join(ROOT, "sentiric-stt-whisper-service_amd", "libmwx_stt.so"))
+    L.mwx_stt_new.restype = C.c_void_p
+    L.mwx_stt_new.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_char_p,
+                              C.c_int, C.c_int]
+    L.mwx_stt_free.argtypes = [C.c_void_p]
+    L.mwx_stt_transcribe_pcm16_ex.argtypes = [C.c_void_p, C.POINTER(C.c_int16), C.c_int, C.c_int,
+                                              C.c_char_p, C.c_int, C.c_float, C.c_char_p, C.c_int,
+                                              C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_int)]
+    return L
+
+
+def stt_transcribe(L, eng, pcm16, sr, abort_after=-1):
+    cap = 1 << 20
+    buf = C.create_string_buffer(cap)
+    m = (C.c_double * 3)()
+    calls = C.c_int(0)
+    p = np.ascontiguousarray(pcm16, np.int16)
+    r = L.mwx_stt_transcribe_pcm16_ex(eng, p.ctypes.data_as(C.POINTER(C.c_int16)), len(p), sr,
+                                      b"en", 1, -1.0, buf, cap, m, abort_after, C.byref(calls))
+    return r, (json.loads(buf.value.decode()) if r >= 0 else None), calls.value
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sr", (8000, 48000))
+def test_stt_engine_resamples_before_transcribing(tmp_path, sr):
+    """transcribe_pcm16 at 8 / 48 kHz == the oracle's pipeline on the
+    restated SRC_SINC_FASTEST output (and != the same samples read as if
+    they were 16 kHz, which is what ignoring the rate would produce)."""
+    import service_filters as sf
+    from test_stt_engine import check_prosody
+    path = str(tmp_path / "ggml-micro.bin")
+    mwx.write_synthetic_model(path, "micro-rich", mwx.GGML_F16, 0)
+    pcm16 = mwx.synth_pcm16(11, n=int(sr * 20), sr=sr)
+    L = _stt_lib()
+    eng = L.mwx_stt_new(str(tmp_path).encode(), b"ggml-micro.bin", 1, 5000, 1, b"en", 500, 0)
+    rc, res, _ = stt_transcribe(L, eng, pcm16, sr)
+    L.mwx_stt_free(eng)
+    assert rc >= 0
+    x16 = orc.resample(mwx.pcm16_to_f32(pcm16), sr, 16000)
+    o = orc.Oracle(path)
+    opt = orc.FullOptions.service_defaults(beam_size=1)
+    opt.language = "en"
+    _, segs, _, _ = o.full(x16, opt)
+    want = sf.postprocess(
+        [(s.raw, s.t0, s.t1, [(t.id, t.p, t.t0, t.t1) for t in s.tokens]) for s in segs],
+        o.eot, o.token_bytes)
+    _, segs_raw, _, _ = o.full(mwx.pcm16_to_f32(pcm16), opt)
+    o.close()
+    assert len(res) == len(want) > 0
+    for g, w in zip(res, want):
+        assert bytes.fromhex(g["text"]) == w["text"]
+        assert (g["t0"], g["t1"]) == (w["t0"], w["t1"])
+        assert [bytes.fromhex(t["text"]) for t in g["tokens"]] == [t[0] for t in w["tokens"]]
+    check_prosody(res, x16)
+    assert [(s.t0, s.t1) for s in segs_raw] != [(s.t0, s.t1) for s in segs]
+
+
+@pytest.mark.gpu
+def test_abort_callback(tmp_path):
+    """RequestOptions::should_abort (src/stt_engine.cpp:17-23,215-219): true
+    before the call -> empty result without running; true once decoding has
+    started -> whisper_full returns an error and the request an empty result;
+    never true -> the normal result. The callback is polled every step."""
+    path = str(tmp_path / "ggml-micro.bin")
+    mwx.write_synthetic_model(path, "micro-rich", mwx.GGML_F16, 0)
+    pcm16 = mwx.synth_pcm16(1, n=30 * 16000)
+    L = _stt_lib()
+    eng = L.mwx_stt_new(str(tmp_path).encode(), b"ggml-micro.bin", 1, 5000, 1, b"en", 500, 0)
+    try:
+        rc, res, calls = stt_transcribe(L, eng, pcm16, 16000, abort_after=-1)
+        assert rc >= 0 and len(res) > 0
+        rc, res0, calls0 = stt_transcribe(L, eng, pcm16, 16000, abort_after=0)
+        assert rc >= 0 and res0 == [] and calls0 == 1  # checked at entry: nothing runs
+        rc, res5, calls5 = stt_transcribe(L, eng, pcm16, 16000, abort_after=5)
+        assert rc >= 0 and res5 == [] and calls5 >= 6
+        rc, res_big, calls_big = stt_transcribe(L, eng, pcm16, 16000, abort_after=100000)
+        assert rc >= 0 and len(res_big) == len(res) and calls_big > 20
+    finally:
+        L.mwx_stt_free(eng)
+    # the C ABI directly: whisper_full's abort code
+    with mwx.Context.open(path) as ctx:
+        p = ctx.default_params(mwx.SAMPLING_GREEDY)
+        p.language = b"en"
+        n = [0]
+
+        def cb(_):
+            n[0] += 1
+            return n[0] > 3
+        keep = mwx.ABORT_CB(cb)
+        p.abort_callback = keep
+        assert ctx.full(mwx.pcm16_to_f32(pcm16), p) < 0
+        assert n[0] == 4
