@@ -225,9 +225,28 @@ void mwx_stt_free(void* eng) { delete static_cast<SttEngine*>(eng); }
 // < -2 = -(needed capacity). abort_after >= 0: RequestOptions::should_abort
 // answers true from its (abort_after + 1)-th call on (the service's abort
 // hook, src/stt_engine.cpp:17-23,215-219); < 0: no abort callback.
+static int transcribe_any(void* eng, const int16_t* pcm16, const float* pcmf, int n,
+                          int sample_rate, const char* language, int beam_size, float temperature,
+                          char* out, int cap, double* metrics3, int abort_after, int* abort_calls);
+
 int mwx_stt_transcribe_pcm16_ex(void* eng, const int16_t* pcm, int n, int sample_rate,
                                 const char* language, int beam_size, float temperature, char* out,
                                 int cap, double* metrics3, int abort_after, int* abort_calls) {
+  return transcribe_any(eng, pcm, nullptr, n, sample_rate, language, beam_size, temperature, out,
+                        cap, metrics3, abort_after, abort_calls);
+}
+
+// As mwx_stt_transcribe_pcm16_ex over f32 PCM (SttEngine::transcribe).
+int mwx_stt_transcribe_f32_ex(void* eng, const float* pcm, int n, int sample_rate,
+                              const char* language, int beam_size, float temperature, char* out,
+                              int cap, double* metrics3, int abort_after, int* abort_calls) {
+  return transcribe_any(eng, nullptr, pcm, n, sample_rate, language, beam_size, temperature, out,
+                        cap, metrics3, abort_after, abort_calls);
+}
+
+static int transcribe_any(void* eng, const int16_t* pcm16, const float* pcmf, int n,
+                          int sample_rate, const char* language, int beam_size, float temperature,
+                          char* out, int cap, double* metrics3, int abort_after, int* abort_calls) {
   RequestOptions o;
   o.language = language ? language : "";
   o.beam_size = beam_size;
@@ -237,8 +256,9 @@ int mwx_stt_transcribe_pcm16_ex(void* eng, const int16_t* pcm, int n, int sample
     o.should_abort = [calls, abort_after] { return (*calls)++ >= abort_after; };
   SttEngine::PerformanceMetrics m{0, 0, 0};
   try {
-    const auto rs = static_cast<SttEngine*>(eng)->transcribe_pcm16(
-        std::vector<int16_t>(pcm, pcm + n), sample_rate, o, &m);
+    SttEngine* e = static_cast<SttEngine*>(eng);
+    const auto rs = pcm16 ? e->transcribe_pcm16(std::vector<int16_t>(pcm16, pcm16 + n), sample_rate, o, &m)
+                          : e->transcribe(std::vector<float>(pcmf, pcmf + n), sample_rate, o, &m);
     if (metrics3) {
       metrics3[0] = m.queue_time_ms;
       metrics3[1] = m.processing_time_ms;

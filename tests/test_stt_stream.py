@@ -241,3 +241,38 @@ def test_concurrent_streams_share_batches(tmp_path):
     n_calls = sum(1 for c in chunk_lists for ch in c if ch)  # each non-empty chunk re-transcribes
     assert out == alone
     assert batches < n_calls, (batches, n_calls)
+
+
+@pytest.mark.gpu
+def test_stream_events_kept_when_buffer_too_small(tmp_path):
+    """A too-small output buffer does not lose a chunk's events: the chunk is
+    consumed, the call returns -(needed + 2), and mwx_stt_stream_drain hands
+    the same events over (feeding again before draining is refused)."""
+    path = str(tmp_path / "ggml-micro.bin")
+    mwx.write_synthetic_model(path, "micro-rich", mwx.GGML_F16, 0)
+    L = lib()
+    L.mwx_stt_stream_drain.restype = C.c_int
+    L.mwx_stt_stream_drain.argtypes = [C.c_void_p, C.c_char_p, C.c_int]
+    pcm = mwx.synth_pcm16(3, n=2 * STEP).tobytes()
+    d = str(tmp_path).encode()
+    evs = []
+    for small in (False, True):
+        eng = L.mwx_stt_new_ex(d, b"ggml-micro.bin", 1, 5000, 1, b"en", 500, 0, 1, 0, STEP)
+        s = L.mwx_stt_stream_new(eng)
+        try:
+            if not small:
+                evs.append(feed(L, s, pcm))
+                continue
+            tiny = C.create_string_buffer(4)
+            r = L.mwx_stt_stream_feed(s, pcm, len(pcm), tiny, 4)
+            assert r < -2
+            assert L.mwx_stt_stream_feed(s, pcm, len(pcm), tiny, 4) == -1  # drain first
+            cap = -r - 2
+            buf = C.create_string_buffer(cap)
+            assert L.mwx_stt_stream_drain(s, buf, cap) >= 0
+            evs.append(json.loads(buf.value.decode()))
+            assert L.mwx_stt_stream_drain(s, buf, cap) >= 0 and json.loads(buf.value.decode()) == []
+        finally:
+            L.mwx_stt_stream_free(s)
+            L.mwx_stt_free(eng)
+    assert evs[0] == evs[1] and len(evs[0]) > 0
