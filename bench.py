@@ -78,12 +78,40 @@ def kernel_model(arch, kclass, clips, rows, launches, prompt_len, steps, windows
     raise ValueError(kclass)
 
 
-def cpu_baseline(model_path, arch, threads, prompt_len, steps):
-    """Times the oracle (CPU restatement of the reference path, scalar C++ +
-    OpenMP) on a bounded sample of ONE clip: full log-mel, conv stem + 1 of the
-    encoder layers, 1 of the cross K/V layers and 4 decode steps; the per-clip
-    time is extrapolated to all layers and prompt + 220 steps."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def oracle_stt_transcribe(o, pcm16, steps):
+    """SttEngine::transcribe_pcm16 restated on the CPU oracle: int16 / 32768
+    (src/stt_engine.cpp:117-125), whisper_full with the service's parameters
+    (:204-243; greedy, language en, decode length fixed like the GPU leg) and
+    the post-filters of :258-311 (oracle/service_filters.py). Returns the kept
+    segments."""
+    import mwx
+    import orc
+    import service_filters as sf
+    opt = orc.FullOptions.service_defaults()
+    opt.language = "en"
+    opt.temperature_inc = 0.0
+    opt.bench_fixed_steps = steps
+    _, segs, _, _ = o.full(mwx.pcm16_to_f32(pcm16), opt)
+    return sf.postprocess([(s.raw, s.t0, s.t1, [(t.id, t.p, t.t0, t.t1) for t in s.tokens])
+                           for s in segs], o.eot, o.token_bytes)
+
+
+def cpu_large_sample(model_path, arch, threads, prompt_len, steps):
+    """The oracle (scalar C++ + OpenMP) on a bounded sample of ONE clip of the
+    benched model: full log-mel, conv stem + 1 of the encoder layers, and 4
+    decode steps measured; the per-clip time is extrapolated to all layers,
+    the cross K/V and prompt + `steps` decode steps (a full large-v3 clip
+    takes minutes on the CPU)."""
     import mwx
     import orc
     L = orc.lib()
@@ -99,30 +127,60 @@ def cpu_baseline(model_path, arch, threads, prompt_len, steps):
     t_conv = time.perf_counter() - t0
     L.orc_set_enc_layer_limit(1)
     t0 = time.perf_counter()
-    enc = o.encode(mel)
+    o.encode(mel)
     t_layer = time.perf_counter() - t0 - t_conv
     L.orc_set_enc_layer_limit(-1)
-    # cross K/V and decode against random-free stand-in: reuse one layer's cost
     k = np.zeros((Ld, 1500, d), np.float32)
     t0 = time.perf_counter()
     o.decode_seq(k, k, [o.sot, 300, 301, 302])
     t_dec = (time.perf_counter() - t0) / 4
-    # one cross layer = 2 GEMMs [1500 x d] x [d x d]: 1/4 of an encoder layer's
-    # QKV+out GEMM work -> scale the measured layer by its FLOP share
     layer_flops = 2 * 1500 * d * 12 * d + 4 * 1500 * 1500 * d
     t_cross = t_layer * (2 * 1500 * d * 2 * d * Ld) / layer_flops
     t_clip = t_mel + t_conv + Le * t_layer + t_cross + (prompt_len + steps) * t_dec
     o.close()
-    sampled = t_mel + t_conv + t_layer + 4 * t_dec
-    return {
-        "value": round(30.0 / t_clip, 4),
-        "unit": "audio-sec/s",
-        "cores": threads,
-        "kind": "port",
-        "sample": (f"1 clip of 30 s, {arch}: full log-mel + conv + 1/{Le} encoder layers + "
-                   f"4 decode steps measured ({sampled:.1f} s), extrapolated to {Le} layers, "
-                   f"cross K/V and {prompt_len + steps} decode steps: {t_clip:.1f} s/clip"),
-    }
+    return 30.0 / t_clip, t_mel + t_conv + t_layer + 4 * t_dec, t_clip
+
+
+def cpu_baseline(model_path, arch, threads, prompt_len, steps):
+    """Reported CPU baseline (BASELINE.md "CPU-baseline plan"): the CPU
+    restatement of the reference path (oracle/, whisper.cpp v1.8.2 semantics)
+    on this host, at the reference's n_threads = 4 (src/config.h:40) and at
+    all granted cores. value: the benched model (bounded sample, see
+    cpu_large_sample); c1: config C1 (tiny.en greedy, one 30-s clip) measured
+    end to end through the SttEngine steps (oracle_stt_transcribe)."""
+    import mwx
+    import orc
+    out = {"unit": "audio-sec/s", "kind": "port", "cpu_model": cpu_model(),
+           "host_cpus": os.cpu_count(), "label": "CPU restatement of the reference path "
+                                                 "(whisper.cpp v1.8.2 semantics)"}
+    legs = {}
+    for th in sorted({4, threads}):
+        v, sampled, t_clip = cpu_large_sample(model_path, arch, th, prompt_len, steps)
+        legs[th] = {"value": round(v, 4), "cores": th,
+                    "sample": (f"1 clip of 30 s, {arch}: full log-mel + conv + 1/{ARCH[arch][3]} "
+                               f"encoder layers + 4 decode steps measured ({sampled:.1f} s), "
+                               f"extrapolated to all layers, cross K/V and {prompt_len + steps} "
+                               f"decode steps: {t_clip:.1f} s/clip")}
+    out.update(legs[threads])
+    out["threads4"] = legs[4]
+    tiny = os.path.join(os.environ.get("TMPDIR", "/tmp"), "mwx_bench_tiny.en_f16.bin")
+    if not os.path.exists(tiny):
+        tmp = tiny + f".tmp{os.getpid()}"
+        mwx.write_synthetic_model(tmp, "tiny.en", mwx.GGML_F16, 0)
+        os.replace(tmp, tiny)
+    c1 = {}
+    for th in sorted({4, threads}):
+        o = orc.Oracle(tiny, threads=th)
+        t0 = time.perf_counter()
+        res = oracle_stt_transcribe(o, mwx.synth_pcm16(0), steps)
+        el = time.perf_counter() - t0
+        o.close()
+        c1[f"threads{th}"] = {"value": round(30.0 / el, 3), "seconds": round(el, 3),
+                              "segments": len(res)}
+    out["c1_tiny_en"] = dict(c1, config="C1: tiny.en greedy, one 30-s 16 kHz clip, "
+                                        f"{steps} decode steps, end to end (mel, encoder, "
+                                        "decode, post-filters), measured")
+    return out
 
 
 def prosody_segments(n_samp, seed):
@@ -538,8 +596,10 @@ def main():
                         "work_per_launch": ework, "work_desc": edesc}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
+            # all cores granted to this job (OMP_NUM_THREADS on the GPU box)
             threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
             try:
+                sys.path.insert(0, os.path.join(ROOT, "oracle"))
                 cpu = cpu_baseline(path, args.arch, threads, prompt_len, args.decode_steps)
             except Exception as ex:  # reported, never fatal to the GPU number
                 cpu = {"error": str(ex)}

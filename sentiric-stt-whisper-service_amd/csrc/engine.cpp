@@ -881,12 +881,84 @@ struct Driver {
     float* Pqkv = (float*)S.pqkv.p + (size_t)8 * r0 * 3 * d;
     float* Pres = (float*)S.pres.p + (size_t)8 * r0 * d;
     float* Pq = (float*)S.pq.p + (size_t)8 * r0 * d;
-    // The d- and 3d-wide projections run as split-K GEMMs writing f32 partial
-    // slabs; each consumer (LN: bias + residual, attention: bias/scale/f16 and
-    // the KV-cache append) folds the slabs in, so no launch is added.
+    static const bool fused = !(getenv("MWX_DEC_FUSED") && atoi(getenv("MWX_DEC_FUSED")) == 0);
+    if (fused) {
+      // 8 launches per layer: the three LayerNorms run inside the GEMMs that
+      // consume them (gemm_ln: QKV, cross-Q, FFN1), the residual-writing
+      // projections (out, cross-out, FFN2) add bias + residual in their
+      // epilogue, so the residual stream xd is complete after each of them
+      for (int l = 0; l < L_dec; ++l) {
+        const DecLayerW& W = C.dec[l];
+        _Float16* ks = (_Float16*)S.kself.p + l * layer_self + (size_t)r0 * H * Tctx * 64;
+        _Float16* vs = (_Float16*)S.vself.p + l * layer_self + (size_t)r0 * H * Tctx * 64;
+        EpiParams e;
+        e.c32 = Pqkv;
+        e.ldc = 3 * d;
+        bool ok;
+        { PerfScope ps(S, "dec_gemm", s);
+          ok = gemm_ln_launch<T>(EPI_F32, xd, W.ln1_w, W.ln1_b, Wt(W.qkv_w), n, 3 * d, d, e, s); }
+        { PerfScope ps(S, "dec_attn_self", s);
+          dec_attention<T>(Pqkv, 1, 3 * d, W.qkv_b, kqs, kqs, ks, vs, nullptr, pos, act, 0, Tctx,
+                           od, n, H, 1.0f, s, (const int*)S.kvmap.p + (size_t)r0 * Tctx,
+                           (const int*)S.kvown.p + r0, r0, xgroup); }
+        e = EpiParams();
+        e.c32 = xd;
+        e.r32 = xd;
+        e.ldc = d;
+        e.active = act;
+        e.bias = W.o_b;
+        { PerfScope ps(S, "dec_gemm", s);
+          ok &= gemm_decode<T>(EPI_RES, od, Wt(W.o_w), n, d, d, e, s); }
+        e = EpiParams();
+        e.c32 = Pq;
+        e.ldc = d;
+        { PerfScope ps(S, "dec_gemm", s);
+          ok &= gemm_ln_launch<T>(EPI_F32, xd, W.lnc_w, W.lnc_b, Wt(W.cq_w), n, d, d, e, s); }
+        { PerfScope ps(S, "dec_attn_cross", s);
+          if (xgroup < 2 ||
+              !dec_cross_attention_grouped<T>(Pq, 1, d, W.cq_b,
+                                              (const _Float16*)S.cross_k.p + l * layer_cross,
+                                              (const _Float16*)S.cross_v.p + l * layer_cross, xidx,
+                                              act, hp.n_audio_ctx, hp.n_audio_ctx, od, n, H, kqs,
+                                              xgroup, s))
+            dec_attention<T>(Pq, 1, d, W.cq_b, 1.0f, 1.0f,
+                             (_Float16*)S.cross_k.p + l * layer_cross,
+                             (_Float16*)S.cross_v.p + l * layer_cross, xidx, pos, act,
+                             hp.n_audio_ctx, hp.n_audio_ctx, od, n, H, kqs, s, nullptr, nullptr, 0,
+                             xgroup); }
+        e = EpiParams();
+        e.c32 = xd;
+        e.r32 = xd;
+        e.ldc = d;
+        e.active = act;
+        e.bias = W.co_b;
+        { PerfScope ps(S, "dec_gemm", s);
+          ok &= gemm_decode<T>(EPI_RES, od, Wt(W.co_w), n, d, d, e, s); }
+        e = EpiParams();
+        e.bias = W.fc1_b;
+        e.c16 = ffd;
+        e.ldc = 4 * d;
+        { PerfScope ps(S, "dec_gemm", s);
+          ok &= gemm_ln_launch<T>(EPI_GELU, xd, W.ln2_w, W.ln2_b, Wt(W.fc1_w), n, 4 * d, d, e, s); }
+        e = EpiParams();
+        e.c32 = xd;
+        e.r32 = xd;
+        e.ldc = d;
+        e.active = act;
+        e.bias = W.fc2_b;
+        { PerfScope ps(S, "dec_gemm", s);
+          ok &= gemm_decode<T>(EPI_RES, ffd, Wt(W.fc2_w), n, d, 4 * d, e, s); }
+        if (!ok) throw std::runtime_error("mwx: unsupported decode GEMM shape");
+      }
+      layer_norm_dec<T>(xd, C.dec_ln_w, C.dec_ln_b, hd, n, d, act, s, nullptr, 0, nullptr);
+    }
+    // Legacy chain (MWX_DEC_FUSED=0): the d- and 3d-wide projections run as
+    // split-K GEMMs writing f32 partial slabs; each consumer (LN: bias +
+    // residual, attention: bias/scale/f16 and the KV-cache append) folds the
+    // slabs in.
     int ks_prev = 0;
     const float* bias_prev = nullptr;
-    for (int l = 0; l < L_dec; ++l) {
+    for (int l = 0; !fused && l < L_dec; ++l) {
       const DecLayerW& W = C.dec[l];
       _Float16* ks = (_Float16*)S.kself.p + l * layer_self + (size_t)r0 * H * Tctx * 64;
       _Float16* vs = (_Float16*)S.vself.p + l * layer_self + (size_t)r0 * H * Tctx * 64;
@@ -937,7 +1009,8 @@ struct Driver {
       bias_prev = W.fc2_b;
       if (!k1 || !k2 || !k3 || !k4 || !k5 || !ks_prev) throw std::runtime_error("mwx: unsupported split-K shape");
     }
-    layer_norm_dec<T>(xd, C.dec_ln_w, C.dec_ln_b, hd, n, d, act, s, Pres, ks_prev, bias_prev);
+    if (!fused)
+      layer_norm_dec<T>(xd, C.dec_ln_w, C.dec_ln_b, hd, n, d, act, s, Pres, ks_prev, bias_prev);
     EpiParams e;
     e.c32 = (float*)S.logits.p + (size_t)r0 * V;
     e.ldc = V;

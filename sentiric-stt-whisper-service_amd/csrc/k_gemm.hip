@@ -51,6 +51,7 @@ __device__ __forceinline__ void epi_store(const EpiParams& P, int bz, int m, int
     else
       ((T*)P.c16)[idx] = to_t<T>(g);
   } else if constexpr (EPI == EPI_RES) {
+    if (P.active && !P.active[m]) return;  // (decode: an inactive row's residual is left alone)
     const long idx = (long)bz * P.c_bstride + (long)m * P.ldc + n;
     const float b = P.bias ? P.bias[n] : 0.0f;
     P.c32[idx] = (acc + b) + P.r32[idx];
@@ -674,6 +675,143 @@ template bool gemm_decode<_Float16>(int, const _Float16*, const _Float16*, int, 
                                     const EpiParams&, hipStream_t);
 template bool gemm_decode<__bf16>(int, const __bf16*, const __bf16*, int, int, int,
                                   const EpiParams&, hipStream_t);
+
+// ---------------------------------------------------------------------------
+// LayerNorm-prologue decode GEMM: y[m][n] = sum_k LN(x)[m][k] * W[n][k] with
+// LN(x) = ggml_norm(x) * lnw + lnb of the f32 residual rows x [M][K], computed
+// inside the GEMM (no LayerNorm launch, no normalised copy in HBM). One
+// workgroup = one 16-row block x NS 16-column strips; its 4 waves split K into
+// quarters (KCH 32-deep k-steps each). Each lane loads exactly the x values
+// of its A fragments (row lane & 15, 8 consecutive k per k-step), so every x
+// element is read once per workgroup: the row statistics are per-lane partial
+// sums (double, k order) combined across the lane groups of a row and then
+// across the 4 waves in a fixed order — batch-independent, like every decode
+// kernel. The A fragments are formed in registers
+// (((x - mean) * rstd) * w + b rounded to T, ggml's formula) and go straight
+// into the MFMAs with the weight fragments, which are requested first.
+// Epilogues: EPI_F32 = the raw f32 product as a single split-K slab (KS = 1)
+// for the attention kernels, which add bias / scale and append the KV cache;
+// EPI_GELU = FFN1 (+ bias, ggml GELU) written as the next GEMM's A tiles.
+// ---------------------------------------------------------------------------
+template <typename T, int KCH, int NS, int EPI>
+__global__ __launch_bounds__(256) void gemm_ln(const float* __restrict__ x,
+                                               const float* __restrict__ lnw,
+                                               const float* __restrict__ lnb,
+                                               const T* __restrict__ Wp, int M, int N,
+                                               EpiParams P) {
+  using V8 = typename Elt<T>::v8;
+  constexpr int NW = 4, KT = NW * KCH, K = KT * 32;
+  __shared__ f32x4 red[NW][NS][64];
+  __shared__ double rs[2][NW][16];
+  __shared__ float swb[2][K];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int nstrips = (N + 15) / 16;
+  const int s0 = blockIdx.x * NS;
+  const int m_base = blockIdx.y * 16;
+  const int row = min(m_base + r, M - 1);  // rows past M: clamped, outputs dropped
+  const int kt0 = wid * KCH;
+  V8 bfr[NS][KCH];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const T* wt = Wp + ((long)min(s0 + s, nstrips - 1) * KT + kt0) * 512 + lane * 8;
+#pragma unroll
+    for (int c = 0; c < KCH; ++c) bfr[s][c] = ld8(wt + c * 512);
+  }
+  f32x4 xa[KCH][2];
+  const float* xr = x + (long)row * K + kt0 * 32 + g * 8;
+#pragma unroll
+  for (int c = 0; c < KCH; ++c) {
+    xa[c][0] = *reinterpret_cast<const f32x4*>(xr + c * 32);
+    xa[c][1] = *reinterpret_cast<const f32x4*>(xr + c * 32 + 4);
+  }
+  for (int i = threadIdx.x; i < K; i += 256) {
+    swb[0][i] = lnw[i];
+    swb[1][i] = lnb[i];
+  }
+  double sd = 0.0;
+#pragma unroll
+  for (int c = 0; c < KCH; ++c)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sd += (double)xa[c][e >> 2][e & 3];
+  sd += __shfl_xor(sd, 16, 64);
+  sd += __shfl_xor(sd, 32, 64);
+  if (g == 0) rs[0][wid][r] = sd;
+  __syncthreads();
+  sd = (rs[0][0][r] + rs[0][1][r]) + (rs[0][2][r] + rs[0][3][r]);
+  const float mean = (float)(sd / K);
+  double sd2 = 0.0;
+#pragma unroll
+  for (int c = 0; c < KCH; ++c)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float d = xa[c][e >> 2][e & 3] - mean;
+      sd2 += (double)(d * d);
+    }
+  sd2 += __shfl_xor(sd2, 16, 64);
+  sd2 += __shfl_xor(sd2, 32, 64);
+  if (g == 0) rs[1][wid][r] = sd2;
+  __syncthreads();
+  sd2 = (rs[1][0][r] + rs[1][1][r]) + (rs[1][2][r] + rs[1][3][r]);
+  const float variance = (float)(sd2 / K);
+  const float scale = 1.0f / sqrtf(variance + 1e-5f);
+  f32x4 acc[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) acc[s] = f32x4{0, 0, 0, 0};
+#pragma unroll
+  for (int c = 0; c < KCH; ++c) {
+    V8 a;
+    const int k0 = (kt0 + c) * 32 + g * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      a[e] = to_t<T>(((xa[c][e >> 2][e & 3] - mean) * scale) * swb[0][k0 + e] + swb[1][k0 + e]);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) acc[s] = Elt<T>::mfma(a, bfr[s][c], acc[s]);
+  }
+#pragma unroll
+  for (int s = 0; s < NS; ++s) red[wid][s][lane] = acc[s];
+  __syncthreads();
+  for (int s = wid; s < NS; s += NW) {
+    if (s0 + s >= nstrips) continue;
+    const f32x4 v = (red[0][s][lane] + red[1][s][lane]) + (red[2][s][lane] + red[3][s][lane]);
+    const int n = (s0 + s) * 16 + (lane & 15);
+    if (n >= N) continue;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int m = m_base + (lane >> 4) * 4 + rr;
+      if (m >= M) continue;
+      if constexpr (EPI == EPI_F32)
+        P.c32[(long)m * P.ldc + n] = v[rr];
+      else
+        reinterpret_cast<T*>(P.c16)[pack_index(m, n, P.ldc)] = to_t<T>(gelu_ggml(v[rr] + P.bias[n]));
+    }
+  }
+}
+
+template <typename T>
+bool gemm_ln_launch(int epi, const float* x, const float* lnw, const float* lnb, const T* Wp,
+                    int M, int N, int K, const EpiParams& P, hipStream_t st) {
+  if (K % 128 || (epi != EPI_F32 && epi != EPI_GELU)) return false;
+  const int kch = K / 128;
+  // strips per workgroup: 2 for the wide outputs (QKV 3d, FFN1 4d) unless
+  // MWX_LN_NS overrides (A/B)
+  static const int ns_env = getenv("MWX_LN_NS") ? atoi(getenv("MWX_LN_NS")) : 0;
+  int ns = ns_env ? ns_env : (N >= 2 * K ? 2 : 1);
+  if (ns != 1 && ns != 2 && ns != 4) ns = 1;
+  const dim3 g(((N + 15) / 16 + ns - 1) / ns, (M + 15) / 16);
+#define GLN(C, S, E)                                                                    if (kch == C && ns == S && epi == E) {                                                  gemm_ln<T, C, S, E><<<g, 256, 0, st>>>(x, lnw, lnb, Wp, M, N, P);                     return true;                                                                        }
+#define GLNK(C) GLN(C, 1, EPI_F32) GLN(C, 2, EPI_F32) GLN(C, 4, EPI_F32) \
+                GLN(C, 1, EPI_GELU) GLN(C, 2, EPI_GELU) GLN(C, 4, EPI_GELU)
+  GLNK(1) GLNK(3) GLNK(4) GLNK(6) GLNK(8) GLNK(10)
+#undef GLNK
+#undef GLN
+  return false;
+}
+template bool gemm_ln_launch<_Float16>(int, const float*, const float*, const float*,
+                                       const _Float16*, int, int, int, const EpiParams&,
+                                       hipStream_t);
+template bool gemm_ln_launch<__bf16>(int, const float*, const float*, const float*, const __bf16*,
+                                     int, int, int, const EpiParams&, hipStream_t);
 
 // ---------------------------------------------------------------------------
 // dispatch

@@ -92,6 +92,14 @@ int gemm_splitk_partials(const T* Ap, const T* Wp, int M, int N, int K, float* P
 template <typename T>
 bool gemm_decode(int epi, const T* Ap, const T* Wp, int M, int N, int K, const EpiParams& P,
                  hipStream_t st);
+// Decode GEMM with the LayerNorm of its A operand fused into its prologue:
+// A = LN(x) of the f32 residual rows x [M][K] (weight lnw, bias lnb, eps
+// 1e-5), K % 128 == 0. epi EPI_F32: the product as one split-K slab (KS = 1)
+// P.c32 [M][P.ldc]; EPI_GELU: gelu(acc + P.bias) as decode-GEMM A tiles
+// (pack_index, K = P.ldc). Returns false if the shape is unsupported.
+template <typename T>
+bool gemm_ln_launch(int epi, const float* x, const float* lnw, const float* lnb, const T* Wp,
+                    int M, int N, int K, const EpiParams& P, hipStream_t st);
 
 void launch_mel(const float* pcm, int n, int n_len, int n_fft_frames, const float* filters,
                 int n_mels, const float* tables, float* out, hipStream_t st);
