@@ -43,6 +43,27 @@ __global__ void fill_kernel(uint16_t* p, size_t n, uint32_t seed) {
   }
 }
 
+// pure streaming read of the cross-attention's bytes: one workgroup per
+// (row, head) reads its K rows then its V rows (1500 x 128 B each), 16 B per
+// lane, 8 loads in flight per lane, one value kept so nothing is elided
+__global__ __launch_bounds__(256) void stream_kv_kernel(const uint4* __restrict__ K,
+                                                        const uint4* __restrict__ V, int n16,
+                                                        float* out) {
+  const long base = (long)blockIdx.x * n16;
+  uint32_t acc = 0;
+  for (int pass = 0; pass < 2; ++pass) {
+    const uint4* p = (pass ? V : K) + base;
+    for (int i = threadIdx.x; i < n16; i += 256 * 8) {
+      uint4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = p[min(i + u * 256, n16 - 1)];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u].x ^ v[u].w;
+    }
+  }
+  if (acc == 0x12345u) out[threadIdx.x] = (float)acc;
+}
+
 int main(int argc, char** argv) {
   const int R = argc > 1 ? atoi(argv[1]) : 32;
   const int reps = argc > 2 ? atoi(argv[2]) : 10;
@@ -83,6 +104,58 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&act, R * 4));
   std::vector<int> ha(R, 1);
   CK(hipMemcpy(act, ha.data(), R * 4, hipMemcpyHostToDevice));
+  // attention / logits operands (large-v3: 20 heads x 64, 1500 audio ctx, 448 text ctx)
+  const int H = 20, Lc = 1500, Tctx = 448, V = 51866;
+  const size_t cross_elems = (size_t)R * H * Lc * 64;
+  uint16_t *ck, *cv, *kself, *vself;
+  CK(hipMalloc(&ck, 2 * cross_elems * 2));  // two layer copies (alternating: no MALL reuse)
+  CK(hipMalloc(&cv, 2 * cross_elems * 2));
+  fill_kernel<<<4096, 256>>>(ck, 2 * cross_elems, 7);
+  fill_kernel<<<4096, 256>>>(cv, 2 * cross_elems, 8);
+  const size_t self_elems = (size_t)R * H * Tctx * 64;
+  CK(hipMalloc(&kself, 2 * self_elems * 2));
+  CK(hipMalloc(&vself, 2 * self_elems * 2));
+  fill_kernel<<<4096, 256>>>(kself, 2 * self_elems, 9);
+  fill_kernel<<<4096, 256>>>(vself, 2 * self_elems, 10);
+  int *pos, *xidx, *kvmap, *kvown;
+  CK(hipMalloc(&pos, R * 4));
+  CK(hipMalloc(&xidx, R * 4));
+  CK(hipMalloc(&kvmap, (size_t)R * Tctx * 4));
+  CK(hipMalloc(&kvown, R * 4));
+  std::vector<int> hp(R, 112), hxi(R);
+  for (int r = 0; r < R; ++r) hxi[r] = r;
+  CK(hipMemcpy(pos, hp.data(), R * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(xidx, hxi.data(), R * 4, hipMemcpyHostToDevice));
+  CK(hipMemset(kvmap, 0, (size_t)R * Tctx * 4));
+  CK(hipMemset(kvown, 0, R * 4));
+  uint16_t* temb;
+  const size_t Vp = (V + 15) / 16 * 16;
+  CK(hipMalloc(&temb, Vp * d * 2));
+  fill_kernel<<<4096, 256>>>(temb, Vp * d, 11);
+  float *logits, *smask, *flt;
+  CK(hipMalloc(&logits, (size_t)R * V * 4));
+  CK(hipMalloc(&smask, (size_t)V * 4));
+  CK(hipMalloc(&flt, (size_t)R * V * 4));
+  CK(hipMemset(smask, 0, (size_t)V * 4));
+  RowCtl* ctl;
+  TokOut* tout;
+  LPPart* parts;
+  LPRes* lres;
+  CK(hipMalloc(&ctl, R * sizeof(RowCtl)));
+  CK(hipMalloc(&tout, R * sizeof(TokOut)));
+  CK(hipMalloc(&parts, R * LP_G * sizeof(LPPart)));
+  CK(hipMalloc(&lres, R * LP_G * sizeof(LPRes)));
+  std::vector<RowCtl> hc(R);
+  for (auto& c : hc) {
+    c = RowCtl{};
+    c.active = 1;
+    c.sample = 1;
+    c.penult_ts = 1;
+    c.seek_delta = 3000;
+  }
+  CK(hipMemcpy(ctl, hc.data(), R * sizeof(RowCtl), hipMemcpyHostToDevice));
+  LogitsConst LCo{V, 50257, 50365, 220, 1, -1, 50363};
+  const float kqs = 0.35355339f;
   CK(hipDeviceSynchronize());
   hipStream_t s;
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
@@ -133,6 +206,41 @@ int main(int argc, char** argv) {
       {"splitk_fc2", 1, [&](int l) { gemm_splitk_partials<T>(ffd, wl(l, 5), R, d, 4 * d, slab, s); }},
       {"ln_dec (KS 5 slabs)", 1,
        [&](int) { layer_norm_dec<T>(x, lnw, lnb, hd, R, d, act, s, slab, 5, bias); }},
+      // the same weights every launch: they stay in L2 / the Infinity Cache
+      // (what a perfect prefetch of the next GEMM's weights could give)
+      {"WARM splitk_qkv", 1, [&](int) { gemm_splitk_partials<T>(hd, wl(0, 0), R, 3 * d, d, slab, s); }},
+      {"WARM splitk_o", 1, [&](int) { gemm_splitk_partials<T>(od, wl(0, 1), R, d, d, slab, s); }},
+      {"WARM splitk_fc2", 1, [&](int) { gemm_splitk_partials<T>(ffd, wl(0, 5), R, d, 4 * d, slab, s); }},
+      {"WARM skinny_fc1", 1,
+       [&](int) { gemm_decode<T>(EPI_GELU, hd, wl(0, 4), R, 4 * d, d, ep_gelu(), s); }},
+      {"stream_kv (cross bytes, pure read)", 1,
+       [&](int l) {
+         stream_kv_kernel<<<R * H, 256, 0, s>>>((const uint4*)(ck + (l & 1) * cross_elems),
+                                                (const uint4*)(cv + (l & 1) * cross_elems), Lc * 64 * 2 / 16,
+                                                x);
+       }},
+      {"cross_attn (KS 5 query slabs)", 1,
+       [&](int l) {
+         dec_attention<T>(slab, 5, d, bias, 1.0f, 1.0f, (_Float16*)ck + (l & 1) * cross_elems,
+                          (_Float16*)cv + (l & 1) * cross_elems, xidx, pos, act, Lc, Lc, od, R, H, kqs, s);
+       }},
+      {"self_attn (pos 112, KS 5)", 1,
+       [&](int l) {
+         dec_attention<T>(slab, 5, 3 * d, bias, kqs, kqs, (_Float16*)kself + (l & 1) * self_elems,
+                          (_Float16*)vself + (l & 1) * self_elems, nullptr, pos, act, 0, Tctx, od, R, H,
+                          1.0f, s, kvmap, kvown, 0, 1);
+       }},
+      {"logits GEMM (per step)", 1,
+       [&](int l) {
+         EpiParams e;
+         e.c32 = logits;
+         e.ldc = V;
+         gemm_decode<T>(EPI_F32, hd, (const T*)temb, R, V, d, e, s);
+       }},
+      {"logits_process (per step)", 1,
+       [&](int) {
+         logits_process(logits, smask, ctl, tout, nullptr, nullptr, LCo, R, LPScratch{flt, parts, lres}, s);
+       }},
       {"FUSED layer GEMMs (6 launches)", 6,
        [&](int l) {
          gemm_ln_launch<T>(EPI_F32, x, lnw, lnb, wl(l, 0), R, 3 * d, d, ep_slab(3 * d), s);
@@ -181,6 +289,102 @@ int main(int argc, char** argv) {
     printf("%-38s %10.2f %12.2f\n", op.name.c_str(), per_layer / op.launches_per_layer, per_layer);
     CK(hipGraphExecDestroy(ge));
     CK(hipGraphDestroy(g));
+  }
+  // ---- concurrency: a GEMM chain of row group A beside the cross-attention of
+  // row group B (R/2 rows each): one stream (sequential), two streams with two
+  // graphs, one graph with two branches
+  if (!only || std::string(only) == "conc") {
+    const int Rh = R / 2;
+    hipStream_t s2;
+    CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+    auto chainA = [&](hipStream_t st) {
+      for (int l = 0; l < L; ++l) {
+        layer_norm_dec<T>(x, lnw, lnb, hd, Rh, d, act, st, slab, 8, bias);
+        gemm_splitk_partials<T>(hd, wl(l, 0), Rh, 3 * d, d, slab, st);
+        gemm_splitk_partials<T>(od, wl(l, 1), Rh, d, d, slab, st);
+        layer_norm_dec<T>(x, lnw, lnb, hd, Rh, d, act, st, slab, 5, bias);
+        gemm_splitk_partials<T>(hd, wl(l, 2), Rh, d, d, slab, st);
+        gemm_splitk_partials<T>(od, wl(l, 3), Rh, d, d, slab, st);
+        layer_norm_dec<T>(x, lnw, lnb, hd, Rh, d, act, st, slab, 5, bias);
+        gemm_decode<T>(EPI_GELU, hd, wl(l, 4), Rh, 4 * d, d, ep_gelu(), st);
+        gemm_splitk_partials<T>(ffd, wl(l, 5), Rh, d, 4 * d, slab, st);
+      }
+    };
+    T* od2;
+    float* slab2;
+    CK(hipMalloc(&od2, R64 * d * 2));
+    CK(hipMalloc(&slab2, (size_t)8 * R * 3 * d * 4));
+    auto chainB = [&](hipStream_t st) {
+      for (int l = 0; l < L; ++l)
+        dec_attention<T>(slab2, 5, d, bias, 1.0f, 1.0f, (_Float16*)ck + (l & 1) * cross_elems,
+                         (_Float16*)cv + (l & 1) * cross_elems, xidx + Rh, pos, act, Lc, Lc, od2, Rh, H,
+                         kqs, st);
+    };
+    auto time_graph = [&](hipGraphExec_t ge, hipStream_t st) {
+      CK(hipGraphLaunch(ge, st));
+      CK(hipStreamSynchronize(st));
+      hipEvent_t a, b;
+      CK(hipEventCreate(&a));
+      CK(hipEventCreate(&b));
+      CK(hipEventRecord(a, st));
+      for (int r = 0; r < reps; ++r) CK(hipGraphLaunch(ge, st));
+      CK(hipEventRecord(b, st));
+      CK(hipStreamSynchronize(st));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, a, b));
+      return ms * 1e3 / reps / L;
+    };
+    auto capture = [&](hipStream_t st, const std::function<void()>& f) {
+      hipGraph_t g;
+      hipGraphExec_t ge;
+      CK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
+      f();
+      CK(hipStreamEndCapture(st, &g));
+      CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+      return ge;
+    };
+    hipGraphExec_t gA = capture(s, [&] { chainA(s); });
+    hipGraphExec_t gB = capture(s, [&] { chainB(s); });
+    hipGraphExec_t gAB = capture(s, [&] { chainA(s); chainB(s); });
+    printf("concurrency (%d + %d rows), us per layer:\n", Rh, Rh);
+    printf("  A alone (GEMM+LN chain)            %8.2f\n", time_graph(gA, s));
+    printf("  B alone (cross-attention)          %8.2f\n", time_graph(gB, s));
+    printf("  A then B, one stream               %8.2f\n", time_graph(gAB, s));
+    // two graphs on two streams
+    hipGraphExec_t gB2 = capture(s2, [&] { chainB(s2); });
+    CK(hipGraphLaunch(gA, s));
+    CK(hipGraphLaunch(gB2, s2));
+    CK(hipDeviceSynchronize());
+    hipEvent_t a, b, c;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    CK(hipEventCreate(&c));
+    CK(hipEventRecord(a, s));
+    CK(hipStreamWaitEvent(s2, a, 0));
+    for (int r = 0; r < reps; ++r) {
+      CK(hipGraphLaunch(gA, s));
+      CK(hipGraphLaunch(gB2, s2));
+    }
+    CK(hipEventRecord(c, s2));
+    CK(hipStreamWaitEvent(s, c, 0));
+    CK(hipEventRecord(b, s));
+    CK(hipStreamSynchronize(s));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    printf("  A || B, two streams / two graphs   %8.2f\n", ms * 1e3 / reps / L);
+    // one graph, two branches (fork / join through events during capture)
+    hipEvent_t fk, jn;
+    CK(hipEventCreateWithFlags(&fk, hipEventDisableTiming));
+    CK(hipEventCreateWithFlags(&jn, hipEventDisableTiming));
+    hipGraphExec_t gF = capture(s, [&] {
+      CK(hipEventRecord(fk, s));
+      CK(hipStreamWaitEvent(s2, fk, 0));
+      chainB(s2);
+      CK(hipEventRecord(jn, s2));
+      chainA(s);
+      CK(hipStreamWaitEvent(s, jn, 0));
+    });
+    printf("  A || B, one graph, two branches    %8.2f\n", time_graph(gF, s));
   }
   return 0;
 }

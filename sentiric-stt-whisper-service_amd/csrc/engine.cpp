@@ -881,7 +881,7 @@ struct Driver {
     float* Pqkv = (float*)S.pqkv.p + (size_t)8 * r0 * 3 * d;
     float* Pres = (float*)S.pres.p + (size_t)8 * r0 * d;
     float* Pq = (float*)S.pq.p + (size_t)8 * r0 * d;
-    static const bool fused = !(getenv("MWX_DEC_FUSED") && atoi(getenv("MWX_DEC_FUSED")) == 0);
+    static const bool fused = getenv("MWX_DEC_FUSED") && atoi(getenv("MWX_DEC_FUSED")) == 1;
     if (fused) {
       // 8 launches per layer: the three LayerNorms run inside the GEMMs that
       // consume them (gemm_ln: QKV, cross-Q, FFN1), the residual-writing
@@ -952,7 +952,7 @@ struct Driver {
       }
       layer_norm_dec<T>(xd, C.dec_ln_w, C.dec_ln_b, hd, n, d, act, s, nullptr, 0, nullptr);
     }
-    // Legacy chain (MWX_DEC_FUSED=0): the d- and 3d-wide projections run as
+    // Default chain (MWX_DEC_FUSED unset or 0): the d- and 3d-wide projections run as
     // split-K GEMMs writing f32 partial slabs; each consumer (LN: bias +
     // residual, attention: bias/scale/f16 and the KV-cache append) folds the
     // slabs in.
@@ -1014,6 +1014,12 @@ struct Driver {
     EpiParams e;
     e.c32 = (float*)S.logits.p + (size_t)r0 * V;
     e.ldc = V;
+    // tied-embedding logits: the 133-MB (large-v3) weight exceeds every L2,
+    // so all rows of a block share one read of it: 32-row blocks (up to 64
+    // rows: ceil(n/16) tiles per block). Per-row arithmetic is the same MFMA
+    // chain in any block, so the logits are bit-identical (38.2 -> 23.0 us per
+    // launch at 32 rows, scripts/probe/dec_chain_probe.hip).
+    e.mt = n <= 64 ? std::max(1, (n + 15) / 16) : 2;
     { PerfScope ps(S, "logits_gemm", s);
     if (!gemm_decode<T>(EPI_F32, hd, Wt(C.tok_emb_p), n, V, d, e, s))
       throw std::runtime_error("mwx: unsupported logits GEMM shape"); }

@@ -533,7 +533,8 @@ __global__ __launch_bounds__(1024) void gemm_skinny(int epi, const T* __restrict
 static bool skinny_split(int K, int& nw, int& kch) {
   if (K % 32) return false;
   const int S = K / 32;
-  for (int w = 16; w >= 1; --w) {
+  static const int wmax = getenv("MWX_SKINNY_NW") ? atoi(getenv("MWX_SKINNY_NW")) : 16;
+  for (int w = std::min(16, std::max(1, wmax)); w >= 1; --w) {
     if (S % w) continue;
     const int c = S / w;
     if (c == 1 || c == 2 || c == 3 || c == 4 || c == 6 || c == 8 || c == 10) {
@@ -617,7 +618,8 @@ __global__ __launch_bounds__(256) void gemm_splitk(const T* __restrict__ Ap,
 int splitk_factor(int K) {
   if (K % 128) return 0;
   const int S = K / 32;  // 32-deep k-steps
-  for (int ks = 8; ks >= 1; --ks)
+  static const int ksmax = getenv("MWX_SPLITK_KSMAX") ? atoi(getenv("MWX_SPLITK_KSMAX")) : 8;
+  for (int ks = std::min(8, std::max(1, ksmax)); ks >= 1; --ks)
     if (S % ks == 0 && (S / ks) % 4 == 0 && (S / ks) / 4 <= 5) return ks;
   return 0;
 }
@@ -666,6 +668,7 @@ bool gemm_decode(int epi, const T* Ap, const T* Wp, int M, int N, int K, const E
   if (M > 64 && mt_big >= 2 && mt_big <= 4) MT = mt_big;
   static const bool mt1 = !(getenv("MWX_DEC_MT1") && atoi(getenv("MWX_DEC_MT1")) == 0);
   if (mt1 && M <= 64) MT = 1;  // 16-row blocks (greedy +3%; MWX_DEC_MT1=0 for A/B)
+  if (P.mt >= 1 && P.mt <= 4) MT = P.mt;
   if (MT == 1) return skinny_launch<T, 1>(epi, Ap, Wp, M, N, K, P, st);
   if (MT == 2) return skinny_launch<T, 2>(epi, Ap, Wp, M, N, K, P, st);
   if (MT == 3) return skinny_launch<T, 3>(epi, Ap, Wp, M, N, K, P, st);

@@ -47,6 +47,7 @@ struct EpiParams {
   long sa_bstride = 0;
   const uint8_t* sw = nullptr;
   bool xcd_remap = true;  // gemm_big: XCD-aware tile order
+  int mt = 0;             // gemm_decode: rows per block = 16 * mt (0: the default rule)
 };
 
 // The encoder GEMMs on MX-fp8 operands (e4m3 bytes + E8M0 scale per 32 k,
