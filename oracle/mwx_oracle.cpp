@@ -708,6 +708,12 @@ static void cross(const Model& m, const std::vector<float>& enc, Cross& c) {
            m.flags & ORC_MXFP8);
     add_bias(tmp.data(), m.w(p + ".cross_attn.value.bias"), M, D);
     for (size_t i = 0; i < tmp.size(); ++i) c.v[(size_t)il * M * D + i] = m.r16(tmp[i]);
+    if (m.flags & ORC_MXFP8) {
+      // fp8 cross K/V cache: the f16 values of each 32-block of a (time,
+      // head) row MX-rounded (the engine stores codes + E8M0 scales)
+      mx_round_rows(c.k.data() + (size_t)il * M * D, M, D);
+      mx_round_rows(c.v.data() + (size_t)il * M * D, M, D);
+    }
   }
 }
 
@@ -1599,15 +1605,27 @@ void* orc_load(const char* path, int flags) {
     return nullptr;
   }
   if (flags & ORC_MXFP8) {
-    // the engine quantizes these (16-bit) weights to MX-fp8 at load
+    // the engine quantizes these (16-bit) weights to MX-fp8 at load: the
+    // encoder projections, the cross K/V projections, and (bf16 models) every
+    // decoder projection plus the tied token embedding (decoder GEMMs on fp8
+    // weights dequantized in registers; the embedding rows are gathered from
+    // the same rounded values)
+    const bool dec_w = m->wtype == 30;  // GGML_BF16
     for (auto& kv : m->t) {
       const std::string& n = kv.first;
+      const bool wt = n.size() > 7 && n.compare(n.size() - 7, 7, ".weight") == 0;
       const bool enc = n.rfind("encoder.blocks.", 0) == 0 &&
                        (n.find(".attn.") != std::string::npos || n.find(".mlp.") != std::string::npos) &&
-                       n.size() > 7 && n.compare(n.size() - 7, 7, ".weight") == 0;
+                       wt;
       const bool cross = n.find(".cross_attn.key.weight") != std::string::npos ||
                          n.find(".cross_attn.value.weight") != std::string::npos;
-      if (!enc && !cross) continue;
+      const bool dec = dec_w && wt && n.rfind("decoder.blocks.", 0) == 0 &&
+                       (n.find(".attn.") != std::string::npos ||
+                        n.find(".cross_attn.query.") != std::string::npos ||
+                        n.find(".cross_attn.out.") != std::string::npos ||
+                        n.find(".mlp.") != std::string::npos);
+      const bool emb = dec_w && n == "decoder.token_embedding.weight";
+      if (!enc && !cross && !dec && !emb) continue;
       Tensor& t = kv.second;
       const int K = (int)t.ne[0];
       if (K % 32) {

@@ -190,12 +190,6 @@ int main(int argc, char** argv) {
   };
   std::vector<Op> ops = {
       {"empty 512 WG", 1, [&](int) { empty_kernel<<<512, 256, 0, s>>>(nullptr); }},
-      {"ln_qkv (gemm_ln QKV)", 1,
-       [&](int l) { gemm_ln_launch<T>(EPI_F32, x, lnw, lnb, wl(l, 0), R, 3 * d, d, ep_slab(3 * d), s); }},
-      {"ln_cq (gemm_ln d x d)", 1,
-       [&](int l) { gemm_ln_launch<T>(EPI_F32, x, lnw, lnb, wl(l, 2), R, d, d, ep_slab(d), s); }},
-      {"ln_fc1 (gemm_ln FFN1+GELU)", 1,
-       [&](int l) { gemm_ln_launch<T>(EPI_GELU, x, lnw, lnb, wl(l, 4), R, 4 * d, d, ep_gelu(), s); }},
       {"res_o (skinny RES K=d)", 1, [&](int l) { gemm_decode<T>(EPI_RES, od, wl(l, 1), R, d, d, ep_res(), s); }},
       {"res_fc2 (skinny RES K=4d)", 1,
        [&](int l) { gemm_decode<T>(EPI_RES, ffd, wl(l, 5), R, d, 4 * d, ep_res(), s); }},
@@ -240,15 +234,6 @@ int main(int argc, char** argv) {
       {"logits_process (per step)", 1,
        [&](int) {
          logits_process(logits, smask, ctl, tout, nullptr, nullptr, LCo, R, LPScratch{flt, parts, lres}, s);
-       }},
-      {"FUSED layer GEMMs (6 launches)", 6,
-       [&](int l) {
-         gemm_ln_launch<T>(EPI_F32, x, lnw, lnb, wl(l, 0), R, 3 * d, d, ep_slab(3 * d), s);
-         gemm_decode<T>(EPI_RES, od, wl(l, 1), R, d, d, ep_res(), s);
-         gemm_ln_launch<T>(EPI_F32, x, lnw, lnb, wl(l, 2), R, d, d, ep_slab(d), s);
-         gemm_decode<T>(EPI_RES, od, wl(l, 3), R, d, d, ep_res(), s);
-         gemm_ln_launch<T>(EPI_GELU, x, lnw, lnb, wl(l, 4), R, 4 * d, d, ep_gelu(), s);
-         gemm_decode<T>(EPI_RES, ffd, wl(l, 5), R, d, 4 * d, ep_res(), s);
        }},
       {"LEGACY layer GEMMs+LN (9 launches)", 9,
        [&](int l) {

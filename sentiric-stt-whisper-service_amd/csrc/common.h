@@ -37,6 +37,7 @@ void ggml_quantize(int type, const float* src, uint8_t* dst, int64_t n);
 int ggml_ftype_of(int type);
 // one row of K (multiple of 32) values -> MX-fp8 codes q[K] + E8M0 scales s[K/32]
 void mx_quantize_row(const float* x, int K, uint8_t* q, uint8_t* s);
+float mx_dequant(uint8_t code, uint8_t s);  // e4m3fn code x 2^(s - 127)
 
 // The 11 int32 header fields of a whisper ggml .bin file, in file order
 // (whisper.cpp whisper_model_load; upstream converter convert-pt-to-ggml.py).

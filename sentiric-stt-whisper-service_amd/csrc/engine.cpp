@@ -72,9 +72,16 @@ struct EncLayerW {
   const float *qkv_b, *o_b, *fc1_b, *fc2_b;
   MxW qkv_x, o_x, fc1_x, fc2_x;  // compute = MXFP8
 };
+// decode-GEMM weight: 16-bit fragment tiles (w) or MX-fp8 fragment tiles
+// (q codes + s scales; MWX_COMPUTE_MXFP8 with a bf16 model)
+struct DecWeight {
+  const void* w = nullptr;
+  const uint8_t* q = nullptr;
+  const uint8_t* s = nullptr;
+};
 struct DecLayerW {
   const float *ln1_w, *ln1_b, *lnc_w, *lnc_b, *ln2_w, *ln2_b;
-  const void *qkv_w, *o_w, *cq_w, *co_w, *fc1_w, *fc2_w;
+  DecWeight qkv, o, cq, co, fc1, fc2;
   const float *qkv_b, *o_b, *cq_b, *co_b, *fc1_b, *fc2_b;
 };
 
@@ -95,13 +102,15 @@ struct Context {
   const float* enc_pe = nullptr;
   std::vector<EncLayerW> enc;
   const float *enc_ln_w = nullptr, *enc_ln_b = nullptr;
-  const void* tok_emb = nullptr;    // [n_vocab][d] rows (embedding gather)
-  const void* tok_emb_p = nullptr;  // fragment-tiled copy (logits GEMM)
+  const void* tok_emb = nullptr;  // [n_vocab][d] rows (embedding gather)
+  DecWeight tok_p;                // fragment-tiled copy (logits GEMM)
   const float* dec_pe = nullptr;
   std::vector<DecLayerW> dec;
   const void* cross_w = nullptr;
   const float* cross_b = nullptr;
   bool mx = false;  // MX-fp8 encoder / cross-K/V GEMMs
+  bool dec8 = false;  // MX-fp8 decoder weights (mx with a bf16 model)
+  bool kv8 = false;   // MX-fp8 cross K/V cache (mx)
   MxW cross_x;
   const float *dec_ln_w = nullptr, *dec_ln_b = nullptr;
   int space_id = -1;
@@ -127,6 +136,8 @@ struct State {
   hipEvent_t ev_in = nullptr, ev_done[MWX_MAX_GROUPS] = {};
   // encoder workspace (clip-batched)
   DBuf pcm, mel, melmax, melT, h1p, x, h, q, k, vt, o, ff, enc, cross_k, cross_v;
+  DBuf cross_ks, cross_vs;  // MX-fp8 cross cache: E8M0 scales (kv8)
+  bool cross_kv8 = false;   // layout of cross_k / cross_v
   DBuf energy, pcm16;
   DBuf aq, as;  // MX-fp8 activations (codes [rows][K], scales [rows][K/32])
   DBuf ibuf;  // small int arrays (slot maps)
@@ -385,8 +396,13 @@ static bool upload_model(Context& C, const ModelFile& mf) {
     A.add(q.data(), q.size(), (const void**)&mx->q);
     A.add(sc.data(), sc.size(), (const void**)&mx->s);
   };
-  // decode-GEMM fragment tiles (see kernels.h: pack_index)
-  auto w16p = [&](const std::vector<std::string>& names, int64_t K, const void** slot) {
+  // decode-GEMM fragment tiles (see kernels.h: pack_index); with dec8 the
+  // MX-fp8 form instead: codes in the same order (1 byte per element) and the
+  // E8M0 scale of each (row, 32-deep k-step) at [(strip * K/32 + kt) * 16 +
+  // row % 16]. `rounded` (optional) receives the MX-rounded values in the
+  // model type (exact in bf16), for the embedding gather copy.
+  auto w16p = [&](const std::vector<std::string>& names, int64_t K, DecWeight* slot,
+                  std::vector<uint16_t>* rounded = nullptr) {
     std::vector<uint16_t> w;
     int64_t rows = 0;
     if (!rows16(names, K, w, rows)) return;
@@ -396,10 +412,29 @@ static bool upload_model(Context& C, const ModelFile& mf) {
       return;
     }
     const int64_t np = (rows + 15) / 16 * 16;
-    std::vector<uint16_t> p((size_t)np * K, 0);
-    for (int64_t n = 0; n < rows; ++n)
-      for (int64_t k = 0; k < K; ++k) p[pack_index(n, k, K)] = w[(size_t)n * K + k];
-    A.add(p.data(), p.size() * 2, slot);
+    if (!C.dec8) {
+      std::vector<uint16_t> p((size_t)np * K, 0);
+      for (int64_t n = 0; n < rows; ++n)
+        for (int64_t k = 0; k < K; ++k) p[pack_index(n, k, K)] = w[(size_t)n * K + k];
+      A.add(p.data(), p.size() * 2, &slot->w);
+      return;
+    }
+    const int64_t KT = K / 32;
+    std::vector<uint8_t> q((size_t)np * K, 0), sc((size_t)(np / 16) * KT * 16, 127);
+    std::vector<float> row(K);
+    std::vector<uint8_t> rq(K), rs(KT);
+    if (rounded) rounded->assign(w.size(), 0);
+    for (int64_t n = 0; n < rows; ++n) {
+      for (int64_t k = 0; k < K; ++k) row[k] = bf16_to_f32(w[(size_t)n * K + k]);
+      mx_quantize_row(row.data(), (int)K, rq.data(), rs.data());
+      for (int64_t k = 0; k < K; ++k) q[pack_index(n, k, K)] = rq[k];
+      for (int64_t kt = 0; kt < KT; ++kt) sc[((n >> 4) * KT + kt) * 16 + (n & 15)] = rs[kt];
+      if (rounded)
+        for (int64_t k = 0; k < K; ++k)
+          (*rounded)[(size_t)n * K + k] = f32_to_bf16(mx_dequant(rq[k], rs[k / 32]));
+    }
+    A.add(q.data(), q.size(), (const void**)&slot->q);
+    A.add(sc.data(), sc.size(), (const void**)&slot->s);
   };
   // filters + mel tables
   A.add(mf.filters.data(), mf.filters.size() * 4, (const void**)&C.d_filters);
@@ -466,8 +501,17 @@ static bool upload_model(Context& C, const ModelFile& mf) {
   }
   f32v("encoder.ln_post.weight", &C.enc_ln_w, d);
   f32v("encoder.ln_post.bias", &C.enc_ln_b, d);
-  w16({"decoder.token_embedding.weight"}, dt, &C.tok_emb);
-  w16p({"decoder.token_embedding.weight"}, dt, &C.tok_emb_p);
+  C.dec8 = C.mx && bf;
+  C.kv8 = C.mx;
+  if (C.dec8) {
+    // the gather rows hold the same MX-rounded values as the logits tiles
+    std::vector<uint16_t> r;
+    w16p({"decoder.token_embedding.weight"}, dt, &C.tok_p, &r);
+    if (ok) A.add(r.data(), r.size() * 2, &C.tok_emb);
+  } else {
+    w16({"decoder.token_embedding.weight"}, dt, &C.tok_emb);
+    w16p({"decoder.token_embedding.weight"}, dt, &C.tok_p);
+  }
   f32v("decoder.positional_embedding", &C.dec_pe, (int64_t)hp.n_text_ctx * dt);
   C.dec.resize(hp.n_text_layer);
   std::vector<std::string> cross_names;
@@ -481,7 +525,7 @@ static bool upload_model(Context& C, const ModelFile& mf) {
     f32v(p + ".cross_attn_ln.bias", &L.lnc_b, dt);
     f32v(p + ".mlp_ln.weight", &L.ln2_w, dt);
     f32v(p + ".mlp_ln.bias", &L.ln2_b, dt);
-    w16p({p + ".attn.query.weight", p + ".attn.key.weight", p + ".attn.value.weight"}, dt, &L.qkv_w);
+    w16p({p + ".attn.query.weight", p + ".attn.key.weight", p + ".attn.value.weight"}, dt, &L.qkv);
     {
       const FileTensor* qb = need(p + ".attn.query.bias");
       const FileTensor* vb = need(p + ".attn.value.bias");
@@ -494,15 +538,15 @@ static bool upload_model(Context& C, const ModelFile& mf) {
       }
       A.add(b.data(), b.size() * 4, (const void**)&L.qkv_b);
     }
-    w16p({p + ".attn.out.weight"}, dt, &L.o_w);
+    w16p({p + ".attn.out.weight"}, dt, &L.o);
     f32v(p + ".attn.out.bias", &L.o_b, dt);
-    w16p({p + ".cross_attn.query.weight"}, dt, &L.cq_w);
+    w16p({p + ".cross_attn.query.weight"}, dt, &L.cq);
     f32v(p + ".cross_attn.query.bias", &L.cq_b, dt);
-    w16p({p + ".cross_attn.out.weight"}, dt, &L.co_w);
+    w16p({p + ".cross_attn.out.weight"}, dt, &L.co);
     f32v(p + ".cross_attn.out.bias", &L.co_b, dt);
-    w16p({p + ".mlp.0.weight"}, dt, &L.fc1_w);
+    w16p({p + ".mlp.0.weight"}, dt, &L.fc1);
     f32v(p + ".mlp.0.bias", &L.fc1_b, 4 * dt);
-    w16p({p + ".mlp.2.weight"}, 4 * dt, &L.fc2_w);
+    w16p({p + ".mlp.2.weight"}, 4 * dt, &L.fc2);
     f32v(p + ".mlp.2.bias", &L.fc2_b, dt);
     cross_names.push_back(p + ".cross_attn.key.weight");
     cross_names.push_back(p + ".cross_attn.value.weight");
@@ -607,6 +651,9 @@ struct Driver {
   }
 
   const T* Wt(const void* p) const { return (const T*)p; }
+  DecW<T> Dw(const DecWeight& x) const {
+    return x.q ? DecW<T>(x.q, x.s) : DecW<T>((const T*)x.w);
+  }
 
   // static suppression mask for this call's params
   void build_static_mask() {
@@ -744,6 +791,10 @@ struct Driver {
     e.bias = C.cross_b;
     e.k = (_Float16*)S.cross_k.p;
     e.v = (_Float16*)S.cross_v.p;
+    if (C.kv8) {  // codes in cross_k / cross_v, scales beside them
+      e.ks8 = (uint8_t*)S.cross_ks.p;
+      e.vs8 = (uint8_t*)S.cross_vs.p;
+    }
     e.L = Lc;
     e.H = H;
     e.d = d;
@@ -755,13 +806,23 @@ struct Driver {
   }
 
   void ensure_cross(int n_slots) {
-    const size_t per = (size_t)L_dec * hp.n_audio_ctx * d * 2;
-    if (S.cross_cap < n_slots) {
+    // f16 cache: 2 B per element; MX-fp8 cache: 1-B codes + 2 scale bytes per
+    // (time, head) row of 64
+    const size_t per = (size_t)L_dec * hp.n_audio_ctx * d * (C.kv8 ? 1 : 2);
+    if (S.cross_cap < n_slots || S.cross_kv8 != C.kv8) {
       S.cross_k.release();
       S.cross_v.release();
+      S.cross_ks.release();
+      S.cross_vs.release();
       S.cross_k.get(per * n_slots);
       S.cross_v.get(per * n_slots);
+      if (C.kv8) {
+        const size_t ps = (size_t)L_dec * hp.n_audio_ctx * H * 2;
+        S.cross_ks.get(ps * n_slots);
+        S.cross_vs.get(ps * n_slots);
+      }
       S.cross_cap = n_slots;
+      S.cross_kv8 = C.kv8;
     }
   }
 
@@ -876,89 +937,18 @@ struct Driver {
     const float kqs = powf(64.0f, -0.25f);
     embed<T>(Wt(C.tok_emb), C.dec_pe, tok, pos, act, xd, n, d, s);
     const size_t layer_self = (size_t)S.row_cap * H * Tctx * 64;
-    const size_t layer_cross = (size_t)S.cross_cap * H * hp.n_audio_ctx * 64;
+    const size_t layer_cross = (size_t)S.cross_cap * H * hp.n_audio_ctx * 64;  // elements
+    const size_t layer_xs = (size_t)S.cross_cap * H * hp.n_audio_ctx * 2;      // kv8 scales
     // the group's split-K slabs [KS][n][N] live inside the R-row slab buffers
     float* Pqkv = (float*)S.pqkv.p + (size_t)8 * r0 * 3 * d;
     float* Pres = (float*)S.pres.p + (size_t)8 * r0 * d;
     float* Pq = (float*)S.pq.p + (size_t)8 * r0 * d;
-    static const bool fused = getenv("MWX_DEC_FUSED") && atoi(getenv("MWX_DEC_FUSED")) == 1;
-    if (fused) {
-      // 8 launches per layer: the three LayerNorms run inside the GEMMs that
-      // consume them (gemm_ln: QKV, cross-Q, FFN1), the residual-writing
-      // projections (out, cross-out, FFN2) add bias + residual in their
-      // epilogue, so the residual stream xd is complete after each of them
-      for (int l = 0; l < L_dec; ++l) {
-        const DecLayerW& W = C.dec[l];
-        _Float16* ks = (_Float16*)S.kself.p + l * layer_self + (size_t)r0 * H * Tctx * 64;
-        _Float16* vs = (_Float16*)S.vself.p + l * layer_self + (size_t)r0 * H * Tctx * 64;
-        EpiParams e;
-        e.c32 = Pqkv;
-        e.ldc = 3 * d;
-        bool ok;
-        { PerfScope ps(S, "dec_gemm", s);
-          ok = gemm_ln_launch<T>(EPI_F32, xd, W.ln1_w, W.ln1_b, Wt(W.qkv_w), n, 3 * d, d, e, s); }
-        { PerfScope ps(S, "dec_attn_self", s);
-          dec_attention<T>(Pqkv, 1, 3 * d, W.qkv_b, kqs, kqs, ks, vs, nullptr, pos, act, 0, Tctx,
-                           od, n, H, 1.0f, s, (const int*)S.kvmap.p + (size_t)r0 * Tctx,
-                           (const int*)S.kvown.p + r0, r0, xgroup); }
-        e = EpiParams();
-        e.c32 = xd;
-        e.r32 = xd;
-        e.ldc = d;
-        e.active = act;
-        e.bias = W.o_b;
-        { PerfScope ps(S, "dec_gemm", s);
-          ok &= gemm_decode<T>(EPI_RES, od, Wt(W.o_w), n, d, d, e, s); }
-        e = EpiParams();
-        e.c32 = Pq;
-        e.ldc = d;
-        { PerfScope ps(S, "dec_gemm", s);
-          ok &= gemm_ln_launch<T>(EPI_F32, xd, W.lnc_w, W.lnc_b, Wt(W.cq_w), n, d, d, e, s); }
-        { PerfScope ps(S, "dec_attn_cross", s);
-          if (xgroup < 2 ||
-              !dec_cross_attention_grouped<T>(Pq, 1, d, W.cq_b,
-                                              (const _Float16*)S.cross_k.p + l * layer_cross,
-                                              (const _Float16*)S.cross_v.p + l * layer_cross, xidx,
-                                              act, hp.n_audio_ctx, hp.n_audio_ctx, od, n, H, kqs,
-                                              xgroup, s))
-            dec_attention<T>(Pq, 1, d, W.cq_b, 1.0f, 1.0f,
-                             (_Float16*)S.cross_k.p + l * layer_cross,
-                             (_Float16*)S.cross_v.p + l * layer_cross, xidx, pos, act,
-                             hp.n_audio_ctx, hp.n_audio_ctx, od, n, H, kqs, s, nullptr, nullptr, 0,
-                             xgroup); }
-        e = EpiParams();
-        e.c32 = xd;
-        e.r32 = xd;
-        e.ldc = d;
-        e.active = act;
-        e.bias = W.co_b;
-        { PerfScope ps(S, "dec_gemm", s);
-          ok &= gemm_decode<T>(EPI_RES, od, Wt(W.co_w), n, d, d, e, s); }
-        e = EpiParams();
-        e.bias = W.fc1_b;
-        e.c16 = ffd;
-        e.ldc = 4 * d;
-        { PerfScope ps(S, "dec_gemm", s);
-          ok &= gemm_ln_launch<T>(EPI_GELU, xd, W.ln2_w, W.ln2_b, Wt(W.fc1_w), n, 4 * d, d, e, s); }
-        e = EpiParams();
-        e.c32 = xd;
-        e.r32 = xd;
-        e.ldc = d;
-        e.active = act;
-        e.bias = W.fc2_b;
-        { PerfScope ps(S, "dec_gemm", s);
-          ok &= gemm_decode<T>(EPI_RES, ffd, Wt(W.fc2_w), n, d, 4 * d, e, s); }
-        if (!ok) throw std::runtime_error("mwx: unsupported decode GEMM shape");
-      }
-      layer_norm_dec<T>(xd, C.dec_ln_w, C.dec_ln_b, hd, n, d, act, s, nullptr, 0, nullptr);
-    }
-    // Default chain (MWX_DEC_FUSED unset or 0): the d- and 3d-wide projections run as
-    // split-K GEMMs writing f32 partial slabs; each consumer (LN: bias +
-    // residual, attention: bias/scale/f16 and the KV-cache append) folds the
-    // slabs in.
+    // The d- and 3d-wide projections run as split-K GEMMs writing f32 partial
+    // slabs; each consumer (LN: bias + residual, attention: bias/scale/f16 and
+    // the KV-cache append) folds the slabs in, so no launch is added.
     int ks_prev = 0;
     const float* bias_prev = nullptr;
-    for (int l = 0; !fused && l < L_dec; ++l) {
+    for (int l = 0; l < L_dec; ++l) {
       const DecLayerW& W = C.dec[l];
       _Float16* ks = (_Float16*)S.kself.p + l * layer_self + (size_t)r0 * H * Tctx * 64;
       _Float16* vs = (_Float16*)S.vself.p + l * layer_self + (size_t)r0 * H * Tctx * 64;
@@ -966,22 +956,31 @@ struct Driver {
                         ks_prev, bias_prev);
       int k1;
       { PerfScope ps(S, "dec_gemm", s);
-        k1 = gemm_splitk_partials<T>(hd, Wt(W.qkv_w), n, 3 * d, d, Pqkv, s); }
+        k1 = gemm_splitk_partials<T>(hd, Dw(W.qkv), n, 3 * d, d, Pqkv, s); }
       { PerfScope ps(S, "dec_attn_self", s);
         dec_attention<T>(Pqkv, k1, 3 * d, W.qkv_b, kqs, kqs, ks, vs, nullptr, pos, act, 0, Tctx,
                          od, n, H, 1.0f, s, (const int*)S.kvmap.p + (size_t)r0 * Tctx,
                          (const int*)S.kvown.p + r0, r0, xgroup); }
       int k2;
       { PerfScope ps(S, "dec_gemm", s);
-        k2 = gemm_splitk_partials<T>(od, Wt(W.o_w), n, d, d, Pres, s); }
+        k2 = gemm_splitk_partials<T>(od, Dw(W.o), n, d, d, Pres, s); }
       layer_norm_dec<T>(xd, W.lnc_w, W.lnc_b, hd, n, d, act, s, Pres, k2, W.o_b);
       int k3;
       { PerfScope ps(S, "dec_gemm", s);
-        k3 = gemm_splitk_partials<T>(hd, Wt(W.cq_w), n, d, d, Pq, s); }
+        k3 = gemm_splitk_partials<T>(hd, Dw(W.cq), n, d, d, Pq, s); }
       { PerfScope ps(S, "dec_attn_cross", s);
         // the decoders of a beam / best-of group share their clip's cross K/V:
-        // stream it once per group
-        if (xgroup < 2 ||
+        // stream it once per group; an MX-fp8 cache is read by the grouped
+        // kernel for any group size
+        if (C.kv8) {
+          if (!dec_cross_attention_grouped<T>(
+                  Pq, k3, d, W.cq_b, (const uint8_t*)S.cross_k.p + l * layer_cross,
+                  (const uint8_t*)S.cross_v.p + l * layer_cross, xidx, act, hp.n_audio_ctx,
+                  hp.n_audio_ctx, od, n, H, kqs, std::max(1, xgroup), s,
+                  (const uint8_t*)S.cross_ks.p + l * layer_xs,
+                  (const uint8_t*)S.cross_vs.p + l * layer_xs))
+            throw std::runtime_error("mwx: unsupported fp8 cross-attention group");
+        } else if (xgroup < 2 ||
             !dec_cross_attention_grouped<T>(Pq, k3, d, W.cq_b,
                                             (const _Float16*)S.cross_k.p + l * layer_cross,
                                             (const _Float16*)S.cross_v.p + l * layer_cross, xidx,
@@ -994,7 +993,7 @@ struct Driver {
                            xgroup); }
       int k4;
       { PerfScope ps(S, "dec_gemm", s);
-        k4 = gemm_splitk_partials<T>(od, Wt(W.co_w), n, d, d, Pres, s); }
+        k4 = gemm_splitk_partials<T>(od, Dw(W.co), n, d, d, Pres, s); }
       layer_norm_dec<T>(xd, W.ln2_w, W.ln2_b, hd, n, d, act, s, Pres, k4, W.co_b);
       EpiParams e;
       e.bias = W.fc1_b;
@@ -1003,14 +1002,13 @@ struct Driver {
       e.pack_out = true;
       bool k5;
       { PerfScope ps(S, "dec_gemm", s);
-        k5 = gemm_decode<T>(EPI_GELU, hd, Wt(W.fc1_w), n, 4 * d, d, e, s); }
+        k5 = gemm_decode<T>(EPI_GELU, hd, Dw(W.fc1), n, 4 * d, d, e, s); }
       { PerfScope ps(S, "dec_gemm", s);
-        ks_prev = gemm_splitk_partials<T>(ffd, Wt(W.fc2_w), n, d, 4 * d, Pres, s); }
+        ks_prev = gemm_splitk_partials<T>(ffd, Dw(W.fc2), n, d, 4 * d, Pres, s); }
       bias_prev = W.fc2_b;
       if (!k1 || !k2 || !k3 || !k4 || !k5 || !ks_prev) throw std::runtime_error("mwx: unsupported split-K shape");
     }
-    if (!fused)
-      layer_norm_dec<T>(xd, C.dec_ln_w, C.dec_ln_b, hd, n, d, act, s, Pres, ks_prev, bias_prev);
+    layer_norm_dec<T>(xd, C.dec_ln_w, C.dec_ln_b, hd, n, d, act, s, Pres, ks_prev, bias_prev);
     EpiParams e;
     e.c32 = (float*)S.logits.p + (size_t)r0 * V;
     e.ldc = V;
@@ -1021,7 +1019,7 @@ struct Driver {
     // launch at 32 rows, scripts/probe/dec_chain_probe.hip).
     e.mt = n <= 64 ? std::max(1, (n + 15) / 16) : 2;
     { PerfScope ps(S, "logits_gemm", s);
-    if (!gemm_decode<T>(EPI_F32, hd, Wt(C.tok_emb_p), n, V, d, e, s))
+    if (!gemm_decode<T>(EPI_F32, hd, Dw(C.tok_p), n, V, d, e, s))
       throw std::runtime_error("mwx: unsupported logits GEMM shape"); }
     float* pr = nullptr;
     float* lp = nullptr;

@@ -496,10 +496,28 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
 // once per row. Every row's arithmetic (scores, softmax, P.V reduction order)
 // is exactly that of dec_attn_kernel<T, false>, so results do not depend on
 // the grouping.
-template <typename T, int NQ>
+// KV8 (MWX_COMPUTE_MXFP8): the cross K/V cache holds MX-fp8 rows (64 e4m3
+// codes per (time, head) and two E8M0 scales, one per 32-element half), half
+// the bytes of the f16 cache. A lane's 8 codes lie in one half, so they are
+// widened to f16 with that half's scale (v_cvt_scalef32_pk_f16_fp8: exact,
+// the values are f16-representable) and every score / P.V operation then runs
+// on f16 exactly as for the f16 cache. Each lane loads the scale pair of one
+// of its wave's 64 rows per batch; the pair a row needs is read from the lane
+// that loaded it (__shfl).
+__device__ __forceinline__ f16x8 dequant_h8(uint2 raw, uint32_t e) {
+  const float sc = e ? __uint_as_float(e << 23) : __uint_as_float(0x00400000u);
+  const h2 a = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(raw.x, sc, false);
+  const h2 b = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(raw.x, sc, true);
+  const h2 c = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(raw.y, sc, false);
+  const h2 d = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(raw.y, sc, true);
+  return f16x8{a[0], a[1], b[0], b[1], c[0], c[1], d[0], d[1]};
+}
+
+template <typename T, int NQ, bool KV8 = false>
 __global__ __launch_bounds__(256) void dec_xattn_kernel(
     const float* __restrict__ P, int KS, int pcols, const float* __restrict__ bias,
-    const _Float16* __restrict__ kbase, const _Float16* __restrict__ vbase,
+    const void* __restrict__ kbase, const void* __restrict__ vbase,
+    const uint8_t* __restrict__ kscale8, const uint8_t* __restrict__ vscale8,
     const int* __restrict__ kv_index, const int* __restrict__ active, int n, int cap, int R,
     T* __restrict__ o, int H, float scale) {
   __shared__ float sc[NQ][DEC_MAX_KEYS];
@@ -523,8 +541,13 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
   asm volatile("" ::"s"(slot));
   if (!any) return;
   const int D = H * 64;
-  const _Float16* K = kbase + (((long)slot * H + h) * cap) * 64;
-  const _Float16* V = vbase + (((long)slot * H + h) * cap) * 64;
+  const long rbase = ((long)slot * H + h) * cap;  // first (time) row of this (slot, head)
+  const _Float16* K = reinterpret_cast<const _Float16*>(kbase) + rbase * 64;
+  const _Float16* V = reinterpret_cast<const _Float16*>(vbase) + rbase * 64;
+  const uint8_t* K8 = reinterpret_cast<const uint8_t*>(kbase) + rbase * 64;
+  const uint8_t* V8 = reinterpret_cast<const uint8_t*>(vbase) + rbase * 64;
+  const uint8_t* KS8 = KV8 ? kscale8 + rbase * 2 : nullptr;
+  const uint8_t* VS8 = KV8 ? vscale8 + rbase * 2 : nullptr;
   // the key/value rows of a batch are those of dec_attn_kernel (row
   // bidx*256 + wid*64 + u*8 + kg, u < 8) but are streamed in halves of 4 rows
   // per lane group (u = 4*half + uu), so fewer registers hold loads in flight
@@ -532,10 +555,24 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
   const int nb = (n + 255) >> 8;
   const int jmax = n - 1;
   f16x8 ka[UH], kb2[UH];
-#define LOADROWS(buf, base, bidx, half)                                        \
+  uint2 qa[KV8 ? UH : 1], qb[KV8 ? UH : 1];  // fp8 rows in flight
+  uint32_t sa = 0, sb = 0;                   // scale pairs (lane: row wid*64 + lane)
+#define LOADROWS16(buf, base, bidx, half)                                      \
   _Pragma("unroll") for (int uu = 0; uu < UH; ++uu) {                         \
     const int j = min((bidx) * 256 + wid * 64 + ((half) * UH + uu) * 8 + kg, jmax); \
     buf[uu] = *reinterpret_cast<const f16x8*>(base + (long)j * 64 + c * 8);   \
+  }
+#define LOADROWS8(qbuf, sreg, base8, sbase, bidx, half)                              \
+  _Pragma("unroll") for (int uu = 0; uu < UH; ++uu) {                               \
+    const int j = min((bidx) * 256 + wid * 64 + ((half) * UH + uu) * 8 + kg, jmax);   \
+    qbuf[uu] = *reinterpret_cast<const uint2*>(base8 + (long)j * 64 + c * 8);         \
+  }                                                                                 \
+  sreg = *reinterpret_cast<const uint16_t*>(                                        \
+      sbase + (long)min((bidx) * 256 + wid * 64 + lane, jmax) * 2);
+#define WIDEN8(buf, qbuf, sreg, half)                                               \
+  _Pragma("unroll") for (int uu = 0; uu < UH; ++uu) {                               \
+    const uint32_t pr = (uint32_t)__shfl((int)(sreg), ((half) * UH + uu) * 8 + kg, 64); \
+    buf[uu] = dequant_h8(qbuf[uu], (pr >> (8 * (c >> 2))) & 0xffu);                 \
   }
   // queries: q = f16(sum of the split-K slabs + bias), head h's 64 columns.
   // All slab loads (KS <= 8, clamped) are issued first, then the first key
@@ -551,7 +588,11 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
 #pragma unroll
     for (int k = 0; k < 8; ++k) pq[i][k] = pp[min(k, KS - 1) * pstride];
   }
-  LOADROWS(ka, K, 0, 0)
+  if constexpr (KV8) {
+    LOADROWS8(qa, sa, K8, KS8, 0, 0)
+  } else {
+    LOADROWS16(ka, K, 0, 0)
+  }
 #pragma unroll
   for (int i = 0; i < QI; ++i) {
     const int t = tid + 256 * i;
@@ -586,12 +627,25 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
     }
   };
   for (int b = 0; b < nb; ++b) {
-    LOADROWS(kb2, K, b, 1)
-    score_batch(ka, b, 0);
-    LOADROWS(ka, K, b + 1, 0)
-    score_batch(kb2, b, 1);
+    if constexpr (KV8) {
+      LOADROWS8(qb, sb, K8, KS8, b, 1)
+      WIDEN8(ka, qa, sa, 0)
+      score_batch(ka, b, 0);
+      LOADROWS8(qa, sa, K8, KS8, b + 1, 0)
+      WIDEN8(kb2, qb, sb, 1)
+      score_batch(kb2, b, 1);
+    } else {
+      LOADROWS16(kb2, K, b, 1)
+      score_batch(ka, b, 0);
+      LOADROWS16(ka, K, b + 1, 0)
+      score_batch(kb2, b, 1);
+    }
   }
-  LOADROWS(ka, V, 0, 0)
+  if constexpr (KV8) {
+    LOADROWS8(qa, sa, V8, VS8, 0, 0)
+  } else {
+    LOADROWS16(ka, V, 0, 0)
+  }
   __syncthreads();
   // softmax per query (block_max_256 / block_sum_256d order)
   float mx[NQ];
@@ -656,12 +710,23 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
     }
   };
   for (int b = 0; b < nb; ++b) {
-    LOADROWS(kb2, V, b, 1)
-    pv_batch(ka, b, 0);
-    LOADROWS(ka, V, b + 1, 0)
-    pv_batch(kb2, b, 1);
+    if constexpr (KV8) {
+      LOADROWS8(qb, sb, V8, VS8, b, 1)
+      WIDEN8(ka, qa, sa, 0)
+      pv_batch(ka, b, 0);
+      LOADROWS8(qa, sa, V8, VS8, b + 1, 0)
+      WIDEN8(kb2, qb, sb, 1)
+      pv_batch(kb2, b, 1);
+    } else {
+      LOADROWS16(kb2, V, b, 1)
+      pv_batch(ka, b, 0);
+      LOADROWS16(ka, V, b + 1, 0)
+      pv_batch(kb2, b, 1);
+    }
   }
-#undef LOADROWS
+#undef LOADROWS16
+#undef LOADROWS8
+#undef WIDEN8
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
 #pragma unroll
@@ -688,30 +753,41 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
 
 template <typename T>
 bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float* bias,
-                                 const _Float16* kbase, const _Float16* vbase,
-                                 const int* kv_index, const int* active, int n_keys, int cap,
-                                 T* o, int R, int H, float scale, int nq, hipStream_t st) {
+                                 const void* kbase, const void* vbase, const int* kv_index,
+                                 const int* active, int n_keys, int cap, T* o, int R, int H,
+                                 float scale, int nq, hipStream_t st, const uint8_t* kscale8,
+                                 const uint8_t* vscale8) {
   if (n_keys > DEC_MAX_KEYS || KS > 8) return false;
   const dim3 g(H, (R + nq - 1) / nq);
+  const bool kv8 = kscale8 != nullptr;
+  if (!kv8 && nq == 1) return false;  // (f16 single rows: dec_attention)
   switch (nq) {
-#define XQ(N)                                                                                 \
-  case N:                                                                                     \
-    dec_xattn_kernel<T, N><<<g, 256, 0, st>>>(P, KS, pcols, bias, kbase, vbase, kv_index,   \
-                                              active, n_keys, cap, R, o, H, scale);           \
+#define XQ(N)                                                                                   \
+  case N:                                                                                       \
+    if (kv8)                                                                                    \
+      dec_xattn_kernel<T, N, true><<<g, 256, 0, st>>>(P, KS, pcols, bias, kbase, vbase,        \
+                                                      kscale8, vscale8, kv_index, active,       \
+                                                      n_keys, cap, R, o, H, scale);             \
+    else                                                                                        \
+      dec_xattn_kernel<T, N, false><<<g, 256, 0, st>>>(P, KS, pcols, bias, kbase, vbase,       \
+                                                       nullptr, nullptr, kv_index, active,      \
+                                                       n_keys, cap, R, o, H, scale);            \
     return true;
-    XQ(2) XQ(3) XQ(4) XQ(5) XQ(6) XQ(8)
+    XQ(1) XQ(2) XQ(3) XQ(4) XQ(5) XQ(6) XQ(8)
 #undef XQ
     default: return false;
   }
 }
 template bool dec_cross_attention_grouped<_Float16>(const float*, int, int, const float*,
-                                                    const _Float16*, const _Float16*, const int*,
+                                                    const void*, const void*, const int*,
                                                     const int*, int, int, _Float16*, int, int,
-                                                    float, int, hipStream_t);
+                                                    float, int, hipStream_t, const uint8_t*,
+                                                    const uint8_t*);
 template bool dec_cross_attention_grouped<__bf16>(const float*, int, int, const float*,
-                                                  const _Float16*, const _Float16*, const int*,
+                                                  const void*, const void*, const int*,
                                                   const int*, int, int, __bf16*, int, int, float,
-                                                  int, hipStream_t);
+                                                  int, hipStream_t, const uint8_t*,
+                                                  const uint8_t*);
 
 template <typename T>
 void dec_attention(const float* P, int KS, int pcols, const float* bias, float qscale,

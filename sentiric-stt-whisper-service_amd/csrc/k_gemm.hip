@@ -98,6 +98,34 @@ __device__ __forceinline__ typename Elt<T>::v8 ld8(const T* p) {
   return *reinterpret_cast<const typename Elt<T>::v8*>(p);
 }
 
+// MX-fp8 decode weights (MWX_COMPUTE_MXFP8, bf16 models): the fragment tiles
+// hold e4m3 codes (1 byte per element, pack_index order) and one E8M0 scale
+// per (column, 32-deep k-step): S[(strip * KT + kt) * 16 + column % 16]. A
+// lane's 8 codes of a k-step share that scale; they are widened to bf16 in
+// registers (v_cvt_scalef32_pk_bf16_fp8: code x 2^(scale - 127), exact) and
+// the MFMA runs on bf16 as for 16-bit weights (weight-only fp8: half the
+// weight bytes, activations unchanged).
+__device__ __forceinline__ float e8m0_to_f32(uint32_t e) {
+  return e ? __uint_as_float(e << 23) : __uint_as_float(0x00400000u);
+}
+template <typename T>
+__device__ __forceinline__ typename Elt<T>::v8 dequant8(uint2 raw, float sc) {
+  typedef T t2 __attribute__((ext_vector_type(2)));
+  t2 a, b, c, d;
+  if constexpr (std::is_same<T, __bf16>::value) {
+    a = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(raw.x, sc, false);
+    b = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(raw.x, sc, true);
+    c = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(raw.y, sc, false);
+    d = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(raw.y, sc, true);
+  } else {
+    a = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(raw.x, sc, false);
+    b = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(raw.x, sc, true);
+    c = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(raw.y, sc, false);
+    d = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(raw.y, sc, true);
+  }
+  return typename Elt<T>::v8{a[0], a[1], b[0], b[1], c[0], c[1], d[0], d[1]};
+}
+
 // ---------------------------------------------------------------------------
 // big tile GEMM (encoder, conv stem, cross K/V: M = clips x 1500 rows)
 //
@@ -375,6 +403,38 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
           const int m = wr0 + row;
           if (m >= M) continue;
           const uint4 v = *reinterpret_cast<const uint4*>(&wl[row * 64 + ch * 8]);
+          if constexpr (EPI == EPI_CROSS_KV) {
+            if (P.ks8) {
+              // MX-fp8 cross K/V cache: each (time, head) row of 64 f16
+              // values is two MX blocks of 32 (4 lanes x 8 values each):
+              // block amax over the 4 lanes, E8M0 exponent, e4m3 codes
+              const int b = m / P.L, t = m - b * P.L;
+              const long ridx = (((long)layer * P.ncap + P.slot[b]) * P.H + h) * P.L + t;
+              const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+              float f[8];
+              float amax = 0.0f;
+#pragma unroll
+              for (int e = 0; e < 8; ++e) {
+                const uint16_t hb = (uint16_t)(w4[e >> 1] >> (16 * (e & 1)));
+                f[e] = (float)__builtin_bit_cast(_Float16, hb);
+                amax = fmaxf(amax, fabsf(f[e]));
+              }
+              amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+              amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
+              const int ex = mx_exp(amax);
+              const float inv = ldexpf(1.0f, -ex);
+              uint32_t lo = 0, hi = 0;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                lo |= (uint32_t)e4m3_rne(f[e] * inv) << (8 * e);
+                hi |= (uint32_t)e4m3_rne(f[4 + e] * inv) << (8 * e);
+              }
+              uint8_t* dq = reinterpret_cast<uint8_t*>(part ? P.v : P.k) + ridx * 64 + ch * 8;
+              *reinterpret_cast<uint2*>(dq) = uint2{lo, hi};
+              if ((ch & 3) == 0) (part ? P.vs8 : P.ks8)[ridx * 2 + (ch >> 2)] = (uint8_t)(127 + ex);
+              continue;
+            }
+          }
           _Float16* dst;
           if constexpr (EPI == EPI_GELU) {
             dst = reinterpret_cast<_Float16*>(P.c16) + (long)bz * P.c_bstride + (long)m * P.ldc +
@@ -470,9 +530,10 @@ __device__ __forceinline__ void skinny_store(const EpiParams& P, int m, int n, f
   epi_store<EPI, T, OUT16>(P, 0, m, n, v);
 }
 
-template <typename T, int MT, int KCH>
+template <typename T, int MT, int KCH, bool W8 = false>
 __global__ __launch_bounds__(1024) void gemm_skinny(int epi, const T* __restrict__ Ap,
-                                                    const T* __restrict__ Wp, int KT, int M,
+                                                    const void* __restrict__ Wv,
+                                                    const uint8_t* __restrict__ Ws, int KT, int M,
                                                     int N, EpiParams P) {
   using V8 = typename Elt<T>::v8;
   __shared__ f32x4 red[16][MT][64];
@@ -483,16 +544,32 @@ __global__ __launch_bounds__(1024) void gemm_skinny(int epi, const T* __restrict
   const int m_base = blockIdx.y * 16 * MT;
   const int Mb = min(16 * MT, M - m_base);
   const int kt0 = wid * KCH;
-  const T* wt = Wp + ((long)blockIdx.x * KT + kt0) * 512 + lane * 8;
+  const long f0 = (long)blockIdx.x * KT + kt0;  // first weight fragment of this wave
   const T* at = Ap + ((long)(blockIdx.y * MT) * KT + kt0) * 512 + lane * 8;
   V8 bfr[KCH];
   V8 afr[MT][KCH];
+  uint2 wraw[W8 ? KCH : 1];
+  uint32_t wsc[W8 ? KCH : 1];
+  if constexpr (W8) {
+    const uint8_t* wq = reinterpret_cast<const uint8_t*>(Wv) + f0 * 512 + lane * 8;
 #pragma unroll
-  for (int c = 0; c < KCH; ++c) bfr[c] = ld8(wt + c * 512);
+    for (int c = 0; c < KCH; ++c) {
+      wraw[c] = *reinterpret_cast<const uint2*>(wq + c * 512);
+      wsc[c] = Ws[(f0 + c) * 16 + (lane & 15)];
+    }
+  } else {
+    const T* wt = reinterpret_cast<const T*>(Wv) + f0 * 512 + lane * 8;
+#pragma unroll
+    for (int c = 0; c < KCH; ++c) bfr[c] = ld8(wt + c * 512);
+  }
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
     for (int c = 0; c < KCH; ++c) afr[mt][c] = ld8(at + ((long)mt * KT + c) * 512);
+  if constexpr (W8) {
+#pragma unroll
+    for (int c = 0; c < KCH; ++c) bfr[c] = dequant8<T>(wraw[c], e8m0_to_f32(wsc[c]));
+  }
   f32x4 acc[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
@@ -546,15 +623,15 @@ static bool skinny_split(int K, int& nw, int& kch) {
   return false;
 }
 
-template <typename T, int MT>
-static bool skinny_launch(int epi, const T* Ap, const T* Wp, int M, int N, int K,
-                          const EpiParams& P, hipStream_t st) {
+template <typename T, int MT, bool W8>
+static bool skinny_launch(int epi, const T* Ap, const void* Wp, const uint8_t* Ws, int M, int N,
+                          int K, const EpiParams& P, hipStream_t st) {
   int nw = 0, kch = 0;
   if (!skinny_split(K, nw, kch)) return false;
   const dim3 g((N + 15) / 16, (M + 16 * MT - 1) / (16 * MT)), b(64 * nw);
   switch (kch) {
 #define SK(C) \
-  case C: gemm_skinny<T, MT, C><<<g, b, 0, st>>>(epi, Ap, Wp, K / 32, M, N, P); return true;
+  case C: gemm_skinny<T, MT, C, W8><<<g, b, 0, st>>>(epi, Ap, Wp, Ws, K / 32, M, N, P); return true;
     SK(1) SK(2) SK(3) SK(4) SK(6) SK(8) SK(10)
 #undef SK
     default: return false;
@@ -569,9 +646,10 @@ static bool skinny_launch(int epi, const T* Ap, const T* Wp, int M, int N, int K
 // order) by the consumer kernel together with the epilogue ggml applies
 // (bias, residual, scale, f16 rounding), so the reduction costs no launch.
 // ---------------------------------------------------------------------------
-template <typename T, int MT, int KCH>
+template <typename T, int MT, int KCH, bool W8 = false>
 __global__ __launch_bounds__(256) void gemm_splitk(const T* __restrict__ Ap,
-                                                   const T* __restrict__ Wp, int KT, int M,
+                                                   const void* __restrict__ Wv,
+                                                   const uint8_t* __restrict__ Ws, int KT, int M,
                                                    int N, int kslice, float* __restrict__ P) {
   using V8 = typename Elt<T>::v8;
   __shared__ f32x4 red[4][MT][64];
@@ -580,16 +658,32 @@ __global__ __launch_bounds__(256) void gemm_splitk(const T* __restrict__ Ap,
   const int m_base = blockIdx.z * 16 * MT;  // row block (16*MT rows per grid.z slice)
   const int Mb = min(16 * MT, M - m_base);
   const int kt0 = (ks * kslice >> 5) + wid * KCH;
-  const T* wt = Wp + ((long)blockIdx.x * KT + kt0) * 512 + lane * 8;
+  const long f0 = (long)blockIdx.x * KT + kt0;
   const T* at = Ap + ((long)(blockIdx.z * MT) * KT + kt0) * 512 + lane * 8;
   V8 bfr[KCH];
   V8 afr[MT][KCH];
+  uint2 wraw[W8 ? KCH : 1];
+  uint32_t wsc[W8 ? KCH : 1];
+  if constexpr (W8) {
+    const uint8_t* wq = reinterpret_cast<const uint8_t*>(Wv) + f0 * 512 + lane * 8;
 #pragma unroll
-  for (int c = 0; c < KCH; ++c) bfr[c] = ld8(wt + c * 512);
+    for (int c = 0; c < KCH; ++c) {
+      wraw[c] = *reinterpret_cast<const uint2*>(wq + c * 512);
+      wsc[c] = Ws[(f0 + c) * 16 + (lane & 15)];
+    }
+  } else {
+    const T* wt = reinterpret_cast<const T*>(Wv) + f0 * 512 + lane * 8;
+#pragma unroll
+    for (int c = 0; c < KCH; ++c) bfr[c] = ld8(wt + c * 512);
+  }
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
     for (int c = 0; c < KCH; ++c) afr[mt][c] = ld8(at + ((long)mt * KT + c) * 512);
+  if constexpr (W8) {
+#pragma unroll
+    for (int c = 0; c < KCH; ++c) bfr[c] = dequant8<T>(wraw[c], e8m0_to_f32(wsc[c]));
+  }
   f32x4 acc[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
@@ -625,8 +719,11 @@ int splitk_factor(int K) {
 }
 
 template <typename T>
-int gemm_splitk_partials(const T* Ap, const T* Wp, int M, int N, int K, float* P,
+int gemm_splitk_partials(const T* Ap, const DecW<T>& Wd, int M, int N, int K, float* P,
                          hipStream_t st) {
+  const void* Wp = Wd.q ? (const void*)Wd.q : (const void*)Wd.w;
+  const uint8_t* Ws = Wd.s;
+  const bool w8 = Wd.q != nullptr;
   const int ks = splitk_factor(K);
   if (ks == 0) return 0;
   const int kslice = K / ks;
@@ -642,7 +739,10 @@ int gemm_splitk_partials(const T* Ap, const T* Wp, int M, int N, int K, float* P
   const dim3 g((N + 15) / 16, ks, (M + 16 * MT - 1) / (16 * MT));
 #define SKL(MTV, C)                                                                       \
   if (MT == MTV && kch == C) {                                                            \
-    gemm_splitk<T, MTV, C><<<g, 256, 0, st>>>(Ap, Wp, K / 32, M, N, kslice, P);        \
+    if (w8)                                                                               \
+      gemm_splitk<T, MTV, C, true><<<g, 256, 0, st>>>(Ap, Wp, Ws, K / 32, M, N, kslice, P); \
+    else                                                                                  \
+      gemm_splitk<T, MTV, C, false><<<g, 256, 0, st>>>(Ap, Wp, Ws, K / 32, M, N, kslice, P); \
     return ks;                                                                            \
   }
 #define SKM(MTV) SKL(MTV, 1) SKL(MTV, 2) SKL(MTV, 3) SKL(MTV, 4) SKL(MTV, 5)
@@ -652,14 +752,16 @@ int gemm_splitk_partials(const T* Ap, const T* Wp, int M, int N, int K, float* P
   return 0;
 }
 
-template int gemm_splitk_partials<_Float16>(const _Float16*, const _Float16*, int, int, int, float*,
-                                            hipStream_t);
-template int gemm_splitk_partials<__bf16>(const __bf16*, const __bf16*, int, int, int, float*,
+template int gemm_splitk_partials<_Float16>(const _Float16*, const DecW<_Float16>&, int, int, int,
+                                            float*, hipStream_t);
+template int gemm_splitk_partials<__bf16>(const __bf16*, const DecW<__bf16>&, int, int, int, float*,
                                           hipStream_t);
 
 template <typename T>
-bool gemm_decode(int epi, const T* Ap, const T* Wp, int M, int N, int K, const EpiParams& P,
+bool gemm_decode(int epi, const T* Ap, const DecW<T>& Wd, int M, int N, int K, const EpiParams& P,
                  hipStream_t st) {
+  const void* Wp = Wd.q ? (const void*)Wd.q : (const void*)Wd.w;
+  const uint8_t* Ws = Wd.s;
   int MT = (std::min(M, 64) + 15) / 16;
   // M > 64 (beam / best-of rows): row blocks of 32 rows (32 KB of LDS: 5 workgroups
   // per CU instead of 2; beam 5 703 -> 729 audio-s/s; A/B: MWX_SKINNY_MT = 2..4;
@@ -669,152 +771,18 @@ bool gemm_decode(int epi, const T* Ap, const T* Wp, int M, int N, int K, const E
   static const bool mt1 = !(getenv("MWX_DEC_MT1") && atoi(getenv("MWX_DEC_MT1")) == 0);
   if (mt1 && M <= 64) MT = 1;  // 16-row blocks (greedy +3%; MWX_DEC_MT1=0 for A/B)
   if (P.mt >= 1 && P.mt <= 4) MT = P.mt;
-  if (MT == 1) return skinny_launch<T, 1>(epi, Ap, Wp, M, N, K, P, st);
-  if (MT == 2) return skinny_launch<T, 2>(epi, Ap, Wp, M, N, K, P, st);
-  if (MT == 3) return skinny_launch<T, 3>(epi, Ap, Wp, M, N, K, P, st);
-  return skinny_launch<T, 4>(epi, Ap, Wp, M, N, K, P, st);
-}
-template bool gemm_decode<_Float16>(int, const _Float16*, const _Float16*, int, int, int,
-                                    const EpiParams&, hipStream_t);
-template bool gemm_decode<__bf16>(int, const __bf16*, const __bf16*, int, int, int,
-                                  const EpiParams&, hipStream_t);
-
-// ---------------------------------------------------------------------------
-// LayerNorm-prologue decode GEMM: y[m][n] = sum_k LN(x)[m][k] * W[n][k] with
-// LN(x) = ggml_norm(x) * lnw + lnb of the f32 residual rows x [M][K], computed
-// inside the GEMM (no LayerNorm launch, no normalised copy in HBM). One
-// workgroup = one 16-row block x NS 16-column strips; its 4 waves split K into
-// quarters (KCH 32-deep k-steps each). Each lane loads exactly the x values
-// of its A fragments (row lane & 15, 8 consecutive k per k-step), so every x
-// element is read once per workgroup: the row statistics are per-lane partial
-// sums (double, k order) combined across the lane groups of a row and then
-// across the 4 waves in a fixed order — batch-independent, like every decode
-// kernel. The A fragments are formed in registers
-// (((x - mean) * rstd) * w + b rounded to T, ggml's formula) and go straight
-// into the MFMAs with the weight fragments, which are requested first.
-// Epilogues: EPI_F32 = the raw f32 product as a single split-K slab (KS = 1)
-// for the attention kernels, which add bias / scale and append the KV cache;
-// EPI_GELU = FFN1 (+ bias, ggml GELU) written as the next GEMM's A tiles.
-// ---------------------------------------------------------------------------
-template <typename T, int KCH, int NS, int EPI>
-__global__ __launch_bounds__(256) void gemm_ln(const float* __restrict__ x,
-                                               const float* __restrict__ lnw,
-                                               const float* __restrict__ lnb,
-                                               const T* __restrict__ Wp, int M, int N,
-                                               EpiParams P) {
-  using V8 = typename Elt<T>::v8;
-  constexpr int NW = 4, KT = NW * KCH, K = KT * 32;
-  __shared__ f32x4 red[NW][NS][64];
-  __shared__ double rs[2][NW][16];
-  __shared__ float swb[2][K];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int r = lane & 15, g = lane >> 4;
-  const int nstrips = (N + 15) / 16;
-  const int s0 = blockIdx.x * NS;
-  const int m_base = blockIdx.y * 16;
-  const int row = min(m_base + r, M - 1);  // rows past M: clamped, outputs dropped
-  const int kt0 = wid * KCH;
-  V8 bfr[NS][KCH];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const T* wt = Wp + ((long)min(s0 + s, nstrips - 1) * KT + kt0) * 512 + lane * 8;
-#pragma unroll
-    for (int c = 0; c < KCH; ++c) bfr[s][c] = ld8(wt + c * 512);
-  }
-  f32x4 xa[KCH][2];
-  const float* xr = x + (long)row * K + kt0 * 32 + g * 8;
-#pragma unroll
-  for (int c = 0; c < KCH; ++c) {
-    xa[c][0] = *reinterpret_cast<const f32x4*>(xr + c * 32);
-    xa[c][1] = *reinterpret_cast<const f32x4*>(xr + c * 32 + 4);
-  }
-  for (int i = threadIdx.x; i < K; i += 256) {
-    swb[0][i] = lnw[i];
-    swb[1][i] = lnb[i];
-  }
-  double sd = 0.0;
-#pragma unroll
-  for (int c = 0; c < KCH; ++c)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) sd += (double)xa[c][e >> 2][e & 3];
-  sd += __shfl_xor(sd, 16, 64);
-  sd += __shfl_xor(sd, 32, 64);
-  if (g == 0) rs[0][wid][r] = sd;
-  __syncthreads();
-  sd = (rs[0][0][r] + rs[0][1][r]) + (rs[0][2][r] + rs[0][3][r]);
-  const float mean = (float)(sd / K);
-  double sd2 = 0.0;
-#pragma unroll
-  for (int c = 0; c < KCH; ++c)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float d = xa[c][e >> 2][e & 3] - mean;
-      sd2 += (double)(d * d);
-    }
-  sd2 += __shfl_xor(sd2, 16, 64);
-  sd2 += __shfl_xor(sd2, 32, 64);
-  if (g == 0) rs[1][wid][r] = sd2;
-  __syncthreads();
-  sd2 = (rs[1][0][r] + rs[1][1][r]) + (rs[1][2][r] + rs[1][3][r]);
-  const float variance = (float)(sd2 / K);
-  const float scale = 1.0f / sqrtf(variance + 1e-5f);
-  f32x4 acc[NS];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) acc[s] = f32x4{0, 0, 0, 0};
-#pragma unroll
-  for (int c = 0; c < KCH; ++c) {
-    V8 a;
-    const int k0 = (kt0 + c) * 32 + g * 8;
-#pragma unroll
-    for (int e = 0; e < 8; ++e)
-      a[e] = to_t<T>(((xa[c][e >> 2][e & 3] - mean) * scale) * swb[0][k0 + e] + swb[1][k0 + e]);
-#pragma unroll
-    for (int s = 0; s < NS; ++s) acc[s] = Elt<T>::mfma(a, bfr[s][c], acc[s]);
-  }
-#pragma unroll
-  for (int s = 0; s < NS; ++s) red[wid][s][lane] = acc[s];
-  __syncthreads();
-  for (int s = wid; s < NS; s += NW) {
-    if (s0 + s >= nstrips) continue;
-    const f32x4 v = (red[0][s][lane] + red[1][s][lane]) + (red[2][s][lane] + red[3][s][lane]);
-    const int n = (s0 + s) * 16 + (lane & 15);
-    if (n >= N) continue;
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int m = m_base + (lane >> 4) * 4 + rr;
-      if (m >= M) continue;
-      if constexpr (EPI == EPI_F32)
-        P.c32[(long)m * P.ldc + n] = v[rr];
-      else
-        reinterpret_cast<T*>(P.c16)[pack_index(m, n, P.ldc)] = to_t<T>(gelu_ggml(v[rr] + P.bias[n]));
-    }
-  }
-}
-
-template <typename T>
-bool gemm_ln_launch(int epi, const float* x, const float* lnw, const float* lnb, const T* Wp,
-                    int M, int N, int K, const EpiParams& P, hipStream_t st) {
-  if (K % 128 || (epi != EPI_F32 && epi != EPI_GELU)) return false;
-  const int kch = K / 128;
-  // strips per workgroup: 2 for the wide outputs (QKV 3d, FFN1 4d) unless
-  // MWX_LN_NS overrides (A/B)
-  static const int ns_env = getenv("MWX_LN_NS") ? atoi(getenv("MWX_LN_NS")) : 0;
-  int ns = ns_env ? ns_env : (N >= 2 * K ? 2 : 1);
-  if (ns != 1 && ns != 2 && ns != 4) ns = 1;
-  const dim3 g(((N + 15) / 16 + ns - 1) / ns, (M + 15) / 16);
-#define GLN(C, S, E)                                                                    if (kch == C && ns == S && epi == E) {                                                  gemm_ln<T, C, S, E><<<g, 256, 0, st>>>(x, lnw, lnb, Wp, M, N, P);                     return true;                                                                        }
-#define GLNK(C) GLN(C, 1, EPI_F32) GLN(C, 2, EPI_F32) GLN(C, 4, EPI_F32) \
-                GLN(C, 1, EPI_GELU) GLN(C, 2, EPI_GELU) GLN(C, 4, EPI_GELU)
-  GLNK(1) GLNK(3) GLNK(4) GLNK(6) GLNK(8) GLNK(10)
-#undef GLNK
-#undef GLN
+#define SKM(MTV)                                                                          \
+  if (MT == MTV)                                                                          \
+    return Wd.q ? skinny_launch<T, MTV, true>(epi, Ap, Wp, Ws, M, N, K, P, st)            \
+                : skinny_launch<T, MTV, false>(epi, Ap, Wp, Ws, M, N, K, P, st);
+  SKM(1) SKM(2) SKM(3) SKM(4)
+#undef SKM
   return false;
 }
-template bool gemm_ln_launch<_Float16>(int, const float*, const float*, const float*,
-                                       const _Float16*, int, int, int, const EpiParams&,
-                                       hipStream_t);
-template bool gemm_ln_launch<__bf16>(int, const float*, const float*, const float*, const __bf16*,
-                                     int, int, int, const EpiParams&, hipStream_t);
+template bool gemm_decode<_Float16>(int, const _Float16*, const DecW<_Float16>&, int, int, int,
+                                    const EpiParams&, hipStream_t);
+template bool gemm_decode<__bf16>(int, const __bf16*, const DecW<__bf16>&, int, int, int,
+                                  const EpiParams&, hipStream_t);
 
 // ---------------------------------------------------------------------------
 // dispatch

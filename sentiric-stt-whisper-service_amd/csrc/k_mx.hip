@@ -9,29 +9,6 @@
 
 namespace mwx {
 
-__device__ __forceinline__ int mx_exp(float amax) {
-  if (!(amax > 0.0f)) return 0;
-  int e0;
-  const float m = frexpf(amax, &e0);  // amax = m * 2^e0, m in [0.5, 1)
-  int e = (e0 - 1) - 8 + (2.0f * m > 1.75f ? 1 : 0);
-  return max(-127, min(127, e));
-}
-
-__device__ __forceinline__ uint8_t e4m3_rne(float v) {
-  const uint8_t sgn = v < 0.0f ? 0x80 : 0;
-  const float a = fabsf(v);
-  if (a < 0.015625f) return sgn | (uint8_t)rintf(a * 512.0f);  // subnormals (8 -> 2^-6)
-  int E;
-  const float m = frexpf(a, &E);  // a = m * 2^E
-  int q = (int)rintf(m * 16.0f);   // a / 2^(E-1-3), in [8, 16]
-  int ex = E - 1;
-  if (q == 16) {
-    q = 8;
-    ++ex;
-  }
-  return sgn | (uint8_t)(((ex + 7) << 3) | (q - 8));
-}
-
 template <typename T>
 __global__ __launch_bounds__(256) void mx_quantize_kernel(const T* __restrict__ x, long ld, int M,
                                                           int nb, uint8_t* __restrict__ q,

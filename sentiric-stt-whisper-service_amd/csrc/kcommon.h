@@ -55,6 +55,33 @@ __device__ __forceinline__ float gelu_ggml(float x) {
   return (float)(_Float16)gelu_f32(xh);
 }
 
+// OCP MX-fp8 block rule (k_mx.hip, the cross K/V cache epilogue; host:
+// quant.cpp mx_quantize_row, oracle mx_round_rows): the E8M0 exponent of a
+// 32-element block is the smallest e with amax <= 448 * 2^e (no clipping);
+// codes are e4m3fn round-to-nearest-even of x / 2^e.
+__device__ __forceinline__ int mx_exp(float amax) {
+  if (!(amax > 0.0f)) return 0;
+  int e0;
+  const float m = frexpf(amax, &e0);  // amax = m * 2^e0, m in [0.5, 1)
+  int e = (e0 - 1) - 8 + (2.0f * m > 1.75f ? 1 : 0);
+  return max(-127, min(127, e));
+}
+
+__device__ __forceinline__ uint8_t e4m3_rne(float v) {
+  const uint8_t sgn = v < 0.0f ? 0x80 : 0;
+  const float a = fabsf(v);
+  if (a < 0.015625f) return sgn | (uint8_t)rintf(a * 512.0f);  // subnormals (8 -> 2^-6)
+  int E;
+  const float m = frexpf(a, &E);  // a = m * 2^E
+  int q = (int)rintf(m * 16.0f);   // a / 2^(E-1-3), in [8, 16]
+  int ex = E - 1;
+  if (q == 16) {
+    q = 8;
+    ++ex;
+  }
+  return sgn | (uint8_t)(((ex + 7) << 3) | (q - 8));
+}
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

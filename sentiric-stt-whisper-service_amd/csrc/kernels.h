@@ -48,6 +48,10 @@ struct EpiParams {
   const uint8_t* sw = nullptr;
   bool xcd_remap = true;  // gemm_big: XCD-aware tile order
   int mt = 0;             // gemm_decode: rows per block = 16 * mt (0: the default rule)
+  // EPI_CROSS_KV with an MX-fp8 cache: k / v hold e4m3 codes, ks8 / vs8 the
+  // E8M0 scales (two per (time, head) row of 64)
+  uint8_t* ks8 = nullptr;
+  uint8_t* vs8 = nullptr;
 };
 
 // The encoder GEMMs on MX-fp8 operands (e4m3 bytes + E8M0 scale per 32 k,
@@ -84,24 +88,28 @@ void gemm(int epi, bool out_f16, const T* A, long lda, long a_bstride, const T* 
 // f32 partial slabs P[KS][M][N] (no epilogue) and returns KS (0 if the shape is
 // unsupported). The consumer kernel sums the slabs and applies the epilogue.
 int splitk_factor(int K);
+// A decode weight in fragment tiles: 16-bit (w) or MX-fp8 (q codes in
+// pack_index order + s, one E8M0 scale per (column, 32-deep k-step) at
+// s[(strip * K/32 + kt) * 16 + column % 16]; MWX_COMPUTE_MXFP8, bf16 models).
 template <typename T>
-int gemm_splitk_partials(const T* Ap, const T* Wp, int M, int N, int K, float* P, hipStream_t st);
+struct DecW {
+  const T* w = nullptr;
+  const uint8_t* q = nullptr;
+  const uint8_t* s = nullptr;
+  DecW() = default;
+  DecW(const T* w_) : w(w_) {}
+  DecW(const uint8_t* q_, const uint8_t* s_) : q(q_), s(s_) {}
+};
+template <typename T>
+int gemm_splitk_partials(const T* Ap, const DecW<T>& W, int M, int N, int K, float* P,
+                         hipStream_t st);
 // Decode full-K GEMM over fragment-tiled weights with a fused epilogue
 // (EPI_GELU / EPI_RES / EPI_F32 / EPI_STORE16 / EPI_DEC_QKV), rows in blocks of
 // 64 so a row's arithmetic does not depend on the batch. Returns false if K is
 // unsupported.
 template <typename T>
-bool gemm_decode(int epi, const T* Ap, const T* Wp, int M, int N, int K, const EpiParams& P,
+bool gemm_decode(int epi, const T* Ap, const DecW<T>& W, int M, int N, int K, const EpiParams& P,
                  hipStream_t st);
-// Decode GEMM with the LayerNorm of its A operand fused into its prologue:
-// A = LN(x) of the f32 residual rows x [M][K] (weight lnw, bias lnb, eps
-// 1e-5), K % 128 == 0. epi EPI_F32: the product as one split-K slab (KS = 1)
-// P.c32 [M][P.ldc]; EPI_GELU: gelu(acc + P.bias) as decode-GEMM A tiles
-// (pack_index, K = P.ldc). Returns false if the shape is unsupported.
-template <typename T>
-bool gemm_ln_launch(int epi, const float* x, const float* lnw, const float* lnb, const T* Wp,
-                    int M, int N, int K, const EpiParams& P, hipStream_t st);
-
 void launch_mel(const float* pcm, int n, int n_len, int n_fft_frames, const float* filters,
                 int n_mels, const float* tables, float* out, hipStream_t st);
 void launch_mel_norm(float* mel, long clip_stride, long count, int n_clips, float* mx,
@@ -159,11 +167,15 @@ void dec_attention(const float* P, int KS, int pcols, const float* bias, float q
 // slot (beam-search / best-of decoders of a clip; kv_index[row] equal within a
 // group): K/V of the slot are streamed once per group. Same per-row results as
 // dec_attention. Returns false if nq is not supported (2, 3, 4, 5, 6, 8).
+// kscale8 / vscale8 != nullptr: the cache is MX-fp8 (kbase / vbase hold e4m3
+// codes [slot][H][cap][64], the scales [slot][H][cap][2] E8M0), any nq >= 1.
 template <typename T>
 bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float* bias,
-                                 const _Float16* kbase, const _Float16* vbase,
-                                 const int* kv_index, const int* active, int n_keys, int cap,
-                                 T* o, int R, int H, float scale, int nq, hipStream_t st);
+                                 const void* kbase, const void* vbase, const int* kv_index,
+                                 const int* active, int n_keys, int cap, T* o, int R, int H,
+                                 float scale, int nq, hipStream_t st,
+                                 const uint8_t* kscale8 = nullptr,
+                                 const uint8_t* vscale8 = nullptr);
 
 struct RowCtl {
   int active;        // row participates in this step

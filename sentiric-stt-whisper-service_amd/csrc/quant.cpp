@@ -241,6 +241,13 @@ static uint8_t e4m3_rne_host(float v) {
   return sgn | (uint8_t)(((ex + 7) << 3) | (q - 8));
 }
 
+// value of an e4m3fn code times the E8M0 scale 2^(s - 127)
+float mx_dequant(uint8_t code, uint8_t s) {
+  const int e = (code >> 3) & 15, m = code & 7;
+  const float a = e == 0 ? ldexpf((float)m, -9) : ldexpf((float)(8 + m), e - 10);
+  return ldexpf(code & 0x80 ? -a : a, (int)s - 127);
+}
+
 void mx_quantize_row(const float* x, int K, uint8_t* q, uint8_t* s) {
   for (int b = 0; b < K / 32; ++b) {
     float amax = 0.0f;

@@ -564,3 +564,45 @@ def test_mxfp8_greedy_tokens_track_mx_oracle(make_model):
         ids = [t.id for sg in segs for t in sg.tokens]
         oids = [t.id for sg in osegs for t in sg.tokens]
         assert ids[:16] == oids[:16]
+
+
+def test_mxfp8_decoder_logits_match_mx_oracle(make_model):
+    """MWX_COMPUTE_MXFP8 decoder: MX-fp8 decoder weights and tied embedding
+    (dequantized in registers, bf16 MFMA) over the MX-fp8 cross K/V cache.
+    Teacher-forced logits against the oracle's ORC_MXFP8 decoder on the same
+    (device) cross K/V — a decoder-only comparison — and the device cache
+    against the MX oracle's cross K/V."""
+    path = make_model("micro-rich", mwx.GGML_BF16)
+    pcm = pcm_clip(0)
+    with mwx.Context.open(path, compute=mwx.COMPUTE_MXFP8) as ctx:
+        enc, k, v = ctx.test_encode(pcm)
+        omx = orc.Oracle(path, mxfp8=True)
+        toks = [omx.sot, 300, 1234, omx.beg, 777, 40000, 220, omx.beg + 37]
+        dev = ctx.test_decode(toks)
+    ref = omx.decode_seq(k, v, toks)
+    o16 = orc.Oracle(path)
+    ref16 = o16.decode_seq(k, v, toks)  # 16-bit decoder weights on the same K/V
+    err, err16 = np.abs(dev - ref).max(), np.abs(dev - ref16).max()
+    assert err < 0.15, err
+    assert err < 0.5 * err16, (err, err16)  # the device runs the fp8 weights
+    assert (dev.argmax(1) == ref.argmax(1)).all()
+    # cache: every value is an MX-fp8 value (code x 2^e, e per 32-block) and
+    # tracks the MX oracle's rounding of its own K/V
+    mel, _ = omx.mel(pcm)
+    k_ref, v_ref = omx.cross(omx.encode(mel))
+    for got, want in ((k, k_ref), (v, v_ref)):
+        d = np.abs(got - want)
+        assert d.mean() < 0.05 * np.abs(want).mean(), (d.mean(), np.abs(want).mean())
+
+
+def test_mxfp8_batch_equals_single(make_model):
+    """fp8 mode (fp8 decoder weights, fp8 cross cache read by the grouped
+    kernel at one row per clip): a batch decodes each clip as alone."""
+    path = make_model("micro-rich", mwx.GGML_BF16)
+    with mwx.Context.open(path, compute=mwx.COMPUTE_MXFP8) as ctx:
+        p = service_params(ctx, temperature_inc=0.0, language=b"en")
+        pcms = [pcm_clip(50 + k, 10.0 + 4 * k) for k in range(5)]
+        assert ctx.full_batch_states(pcms, p, range(5)) == 0
+        batched = [mwx.token_ids(ctx.segments(i)) for i in range(5)]
+        singles = [mwx.token_ids(run_fresh(ctx, pcm, p)) for pcm in pcms]
+    assert batched == singles and all(len(t) > 0 for t in batched)

@@ -195,3 +195,23 @@ def test_base_f16_batch1_full_depth_matches_oracle(make_model, arch):
             assert_same(segs, osegs, tid_tie_tol=2e-3 if arch == "base" else 0.0)
             n_tok += sum(len(s.tokens) for s in osegs)
         assert n_tok >= (400 if arch == "base" else 4)
+
+
+def test_v3_geometry_mxfp8_greedy_tracks_mx_oracle(v3):
+    """fp8 mode at large-v3 geometry, greedy (one row per clip: the fp8 cross
+    cache through the grouped kernel with NQ = 1, fp8 decoder GEMMs at KS 5 /
+    8): the token stream follows the MX oracle's until fp8 re-rounding noise
+    first reorders two close logits, and a 4-clip batch == each clip alone."""
+    _, _, path = v3
+    omx = orc.Oracle(path, mxfp8=True)
+    with mwx.Context.open(path, compute=mwx.COMPUTE_MXFP8) as ctx:
+        p = service_params(ctx, temperature_inc=0.0, language=b"en")
+        pcms = [pcm_clip(k) for k in range(4)]
+        assert ctx.full_batch_states(pcms, p, range(4)) == 0
+        batched = [mwx.token_ids(ctx.segments(i)) for i in range(4)]
+        for i, pcm in enumerate(pcms):
+            assert ctx.full(pcm, p, state_index=4 + i) == 0
+            assert mwx.token_ids(ctx.segments(4 + i)) == batched[i], i
+    _, osegs, _, _ = omx.full(pcms[0], greedy_opt())
+    oids = [t.id for s in osegs for t in s.tokens]
+    assert batched[0][:8] == oids[:8]

@@ -147,17 +147,30 @@ def np_mx_round(x):
     return (q * X).reshape(-1)
 
 
+MX_DEC_WEIGHTS = ("decoder.blocks.0.attn.query.weight", "decoder.blocks.1.attn.out.weight",
+                  "decoder.blocks.2.cross_attn.query.weight", "decoder.blocks.0.cross_attn.out.weight",
+                  "decoder.blocks.1.mlp.0.weight", "decoder.blocks.2.mlp.2.weight",
+                  "decoder.token_embedding.weight")
+
+
 def test_mxfp8_weights_follow_the_mx_rule(make_model):
-    """Oracle MX-fp8 mode: encoder and cross-K/V weights are the MX rounding of
-    the file's 16-bit weights (numpy restatement); other weights untouched."""
+    """Oracle MX-fp8 mode: encoder and cross-K/V weights — and, for a bf16
+    model, every decoder projection and the tied token embedding — are the MX
+    rounding of the file's 16-bit weights (numpy restatement); the rest (conv
+    stem, positional embeddings, LayerNorms, biases) is untouched. An f16
+    model keeps 16-bit decoder weights."""
     path = make_model("micro", mwx.GGML_BF16)
     plain, mx = orc.Oracle(path), orc.Oracle(path, mxfp8=True)
     for name in ("encoder.blocks.0.attn.query.weight", "encoder.blocks.1.mlp.2.weight",
-                 "decoder.blocks.2.cross_attn.value.weight"):
+                 "decoder.blocks.2.cross_attn.value.weight") + MX_DEC_WEIGHTS:
         np.testing.assert_array_equal(mx.tensor(name), np_mx_round(plain.tensor(name)))
-    for name in ("decoder.blocks.0.attn.query.weight", "decoder.token_embedding.weight",
-                 "encoder.conv1.weight"):
+    for name in ("encoder.conv1.weight", "decoder.positional_embedding",
+                 "decoder.blocks.0.attn_ln.weight", "decoder.blocks.0.mlp.0.bias"):
         np.testing.assert_array_equal(mx.tensor(name), plain.tensor(name))
+    path16 = make_model("micro", mwx.GGML_F16)
+    plain16, mx16 = orc.Oracle(path16), orc.Oracle(path16, mxfp8=True)
+    for name in MX_DEC_WEIGHTS:
+        np.testing.assert_array_equal(mx16.tensor(name), plain16.tensor(name))
 
 
 def np_quantize_q8_0_exact(x):
