@@ -17,7 +17,8 @@ from typing import List, Optional
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liborc.so")
+# ORC_LIB: the sanitizer build (tests/san/Makefile) for tests/test_sanitizers.py
+LIB_PATH = os.environ.get("ORC_LIB") or os.path.join(HERE, "liborc.so")
 ORC_EXACT = 1
 ORC_MXFP8 = 2  # encoder / cross-K/V matmuls on MX-fp8 operands (engine MWX_COMPUTE_MXFP8)
 
