@@ -42,17 +42,21 @@ ARCH = {  # n_mels, d, heads, enc layers, dec layers, vocab
 }
 
 
-def kernel_model(arch, kclass, clips, rows, launches, prompt_len, steps, windows=1):
+def kernel_model(arch, kclass, clips, rows, launches, prompt_len, steps, windows=1, kv8=False):
     """Algorithmic work of one launch of `kclass`, averaged over the launches of
-    one step: (bound, per-launch bytes or flops, description)."""
+    one step: (bound, per-launch bytes or flops, description). kv8: the cross
+    K/V cache is MX-fp8 (--fp8: one e4m3 byte per element + one E8M0 scale
+    byte per 32)."""
     n_mels, d, H, Le, Ld, V = ARCH[arch]
     L, T = 1500, 3000
     if kclass == "dec_attn_cross":
-        # every clip's cross K and V for one layer (f16) is read once per launch
+        # every clip's cross K and V for one layer is read once per launch
         # (greedy: one row per clip; beam / best-of: the clip's decoders share
         # it), plus q in / o out per row
-        b = clips * L * d * 2 * 2 + rows * d * 2 * 2
-        return "hbm", b, f"{clips:g} clips x K+V 1500x{d} f16 + {rows:g} rows x q/o per launch"
+        per = (1 + 1 / 32) if kv8 else 2
+        b = clips * L * d * 2 * per + rows * d * 2 * 2
+        kind = "MX-fp8 (e4m3 + E8M0 per 32)" if kv8 else "f16"
+        return "hbm", b, f"{clips:g} clips x K+V 1500x{d} {kind} + {rows:g} rows x q/o per launch"
     if kclass == "dec_attn_self":
         # every row reads its history K and V (f16, 64 per head) for one
         # layer: positions 1..(prompt_len + steps - 1) averaged over the steps,
@@ -441,7 +445,7 @@ def main():
     ap.add_argument("--perf-class", default="dec_attn_cross")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fp8", action="store_true",
-                    help="MX-fp8 compute for the encoder / cross-K/V GEMMs (C5)")
+                    help="MX-fp8 compute (C5): encoder, cross-K/V and decoder weight GEMMs, cross K/V cache")
     ap.add_argument("--host-input", action="store_true",
                     help="PCM in host memory, uploaded inside each step (PCIe-inclusive rate)")
     ap.add_argument("--pcm16", action="store_true",
@@ -561,12 +565,13 @@ def main():
         clips_per_launch = args.clips * (rows / (args.clips * max(1, args.beam)))
         bound, work, desc = kernel_model(args.arch, args.perf_class, clips_per_launch, rows,
                                          launches // max(1, args.steps), prompt_len,
-                                         args.decode_steps, n_windows)
+                                         args.decode_steps, n_windows, kv8=args.fp8)
         traffic = None
         tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(tf):
             try:
-                traffic = json.load(open(tf)).get(f"{args.arch}:{args.perf_class}:{args.clips}")
+                key = f"{args.arch}:{args.perf_class}:{args.clips}" + (":fp8" if args.fp8 else "")
+                traffic = json.load(open(tf)).get(key) if args.beam <= 1 else None
             except Exception:
                 traffic = None
         if bound == "hbm":
@@ -614,7 +619,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": (f"mxfp8 encoder/cross GEMMs + {args.wtype}" if args.fp8 else args.wtype),
+            "dtype": (f"mxfp8 (encoder/cross/decoder weight GEMMs, cross K/V cache) + {args.wtype}"
+                      if args.fp8 else args.wtype),
             "data": ("synthetic (seeded 16 kHz PCM16 clips, "
                      + (("host int16, uploaded and converted per step" if args.pcm16 else
                          "host memory, uploaded per step") if args.host_input else "resident in HBM")
