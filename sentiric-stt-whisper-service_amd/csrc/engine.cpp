@@ -157,6 +157,24 @@ struct State {
     }
     return pin;
   }
+  // run-ahead greedy decode: device row states [R] + step counter, prompts
+  // [R][Tctx], and a pinned ring of per-step reports the advance kernel
+  // writes (RUN_SLOTS slots of R rows), one event per slot
+  static constexpr int RUN_SLOTS = 4;
+  DBuf rrun, rprompt;
+  void* rep_pin = nullptr;
+  size_t rep_n = 0;
+  hipEvent_t ev_step[RUN_SLOTS] = {};
+  RunReport* report_ring(size_t bytes) {
+    if (bytes > rep_n) {
+      if (rep_pin) (void)hipHostFree(rep_pin);
+      rep_pin = nullptr;
+      rep_n = 0;
+      HIPC(hipHostMalloc(&rep_pin, bytes, hipHostMallocMapped | hipHostMallocCoherent));
+      rep_n = bytes;
+    }
+    return (RunReport*)rep_pin;
+  }
   // decoder workspace (row-batched)
   DBuf xd, hd, qd, od, ffd, logits, kself, vself, stepin, ctl, tokout, probs, logprobs, smask;
   DBuf pqkv, pres, pq;  // split-K partial slabs of the decode GEMMs

@@ -257,7 +257,7 @@ __device__ __forceinline__ float dpp_sum8(float d) {
 // written to the cache and taken from LDS (its cache line may be stale in L1).
 // The loop body is straight-line (two batches per trip, no early exit), so the
 // compiler keeps exactly one batch in flight with counted vmcnt waits.
-template <typename T, bool SELF, int UBX = 8>
+template <typename T, bool SELF, int UBX = 8, bool NTL = !SELF>
 __global__ __launch_bounds__(256) void dec_attn_kernel(
     const float* __restrict__ P, int KS, int pcols, const float* __restrict__ bias, float qscale,
     float kscale, _Float16* __restrict__ kbase, _Float16* __restrict__ vbase,
@@ -319,7 +319,7 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
     const _Float16* src = base + (long)j * 64 + c * 8;                            \
     if (SELF && j < own0)                                                         \
       src += ((long)mrow[j] - map_row0 - slot) * rstride;                         \
-    buf[u] = *reinterpret_cast<const f16x8*>(src);                                \
+    buf[u] = ld_stream<NTL>(reinterpret_cast<const f16x8*>(src));                 \
   }
   // self (beam search): the history rows of batch 0 are resolved through the
   // position map once, before anything else is loaded, and the row deltas are
@@ -342,7 +342,7 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
       asm volatile("" : "+v"(md)); /* no hoisted 64-bit V addresses */            \
       src += (long)md * rstride;                                                  \
     }                                                                             \
-    buf[u] = *reinterpret_cast<const f16x8*>(src);                                \
+    buf[u] = ld_stream<NTL>(reinterpret_cast<const f16x8*>(src));                 \
   }
   // reduce the projections of this head from the split-K slabs (KS <= 8):
   // the slab loads are issued first, then the first key batch, so the
@@ -513,7 +513,7 @@ __device__ __forceinline__ f16x8 dequant_h8(uint2 raw, uint32_t e) {
   return f16x8{a[0], a[1], b[0], b[1], c[0], c[1], d[0], d[1]};
 }
 
-template <typename T, int NQ, bool KV8 = false>
+template <typename T, int NQ, bool KV8 = false, bool NTL = true>
 __global__ __launch_bounds__(256) void dec_xattn_kernel(
     const float* __restrict__ P, int KS, int pcols, const float* __restrict__ bias,
     const void* __restrict__ kbase, const void* __restrict__ vbase,
@@ -560,12 +560,13 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
 #define LOADROWS16(buf, base, bidx, half)                                      \
   _Pragma("unroll") for (int uu = 0; uu < UH; ++uu) {                         \
     const int j = min((bidx) * 256 + wid * 64 + ((half) * UH + uu) * 8 + kg, jmax); \
-    buf[uu] = *reinterpret_cast<const f16x8*>(base + (long)j * 64 + c * 8);   \
+    buf[uu] = ld_stream<NTL>(reinterpret_cast<const f16x8*>(base + (long)j * 64 + c * 8)); \
   }
 #define LOADROWS8(qbuf, sreg, base8, sbase, bidx, half)                              \
   _Pragma("unroll") for (int uu = 0; uu < UH; ++uu) {                               \
     const int j = min((bidx) * 256 + wid * 64 + ((half) * UH + uu) * 8 + kg, jmax);   \
-    qbuf[uu] = *reinterpret_cast<const uint2*>(base8 + (long)j * 64 + c * 8);         \
+    const u32x2 q2_ = ld_stream<NTL>(reinterpret_cast<const u32x2*>(base8 + (long)j * 64 + c * 8)); \
+    qbuf[uu] = uint2{q2_[0], q2_[1]};                                                 \
   }                                                                                 \
   sreg = *reinterpret_cast<const uint16_t*>(                                        \
       sbase + (long)min((bidx) * 256 + wid * 64 + lane, jmax) * 2);
@@ -761,15 +762,25 @@ bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float*
   const dim3 g(H, (R + nq - 1) / nq);
   const bool kv8 = kscale8 != nullptr;
   if (!kv8 && nq == 1) return false;  // (f16 single rows: dec_attention)
+  // MWX_XATTN_NT=0: default-policy K/V loads (A/B of the non-temporal stream)
+  static const bool nt = !(getenv("MWX_XATTN_NT") && atoi(getenv("MWX_XATTN_NT")) == 0);
   switch (nq) {
 #define XQ(N)                                                                                   \
   case N:                                                                                       \
-    if (kv8)                                                                                    \
-      dec_xattn_kernel<T, N, true><<<g, 256, 0, st>>>(P, KS, pcols, bias, kbase, vbase,        \
+    if (kv8 && nt)                                                                              \
+      dec_xattn_kernel<T, N, true, true><<<g, 256, 0, st>>>(P, KS, pcols, bias, kbase, vbase,  \
                                                       kscale8, vscale8, kv_index, active,       \
                                                       n_keys, cap, R, o, H, scale);             \
+    else if (kv8)                                                                               \
+      dec_xattn_kernel<T, N, true, false><<<g, 256, 0, st>>>(P, KS, pcols, bias, kbase, vbase, \
+                                                      kscale8, vscale8, kv_index, active,       \
+                                                      n_keys, cap, R, o, H, scale);             \
+    else if (nt)                                                                                \
+      dec_xattn_kernel<T, N, false, true><<<g, 256, 0, st>>>(P, KS, pcols, bias, kbase, vbase, \
+                                                       nullptr, nullptr, kv_index, active,      \
+                                                       n_keys, cap, R, o, H, scale);            \
     else                                                                                        \
-      dec_xattn_kernel<T, N, false><<<g, 256, 0, st>>>(P, KS, pcols, bias, kbase, vbase,       \
+      dec_xattn_kernel<T, N, false, false><<<g, 256, 0, st>>>(P, KS, pcols, bias, kbase, vbase, \
                                                        nullptr, nullptr, kv_index, active,      \
                                                        n_keys, cap, R, o, H, scale);            \
     return true;
@@ -806,6 +817,8 @@ void dec_attention(const float* P, int KS, int pcols, const float* bias, float q
   // (self rows per lane group per batch: 4 -- 66 VGPRs, 7 waves/SIMD: beam 5
   // 659 -> 687 audio-s/s; 8 with MWX_SELF_UB=8 for A/B)
   static const bool self_ub4 = !(getenv("MWX_SELF_UB") && atoi(getenv("MWX_SELF_UB")) == 8);
+  // cross K/V streamed with non-temporal loads (MWX_XATTN_NT=0: default policy)
+  static const bool xattn_nt = !(getenv("MWX_XATTN_NT") && atoi(getenv("MWX_XATTN_NT")) == 0);
   if (fixed_len == 0 && self_ub4)
     dec_attn_kernel<T, true, 4><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale, kbase,
                                                    vbase, kv_index, pos, active, fixed_len,
@@ -815,11 +828,16 @@ void dec_attention(const float* P, int KS, int pcols, const float* bias, float q
     dec_attn_kernel<T, true><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale, kbase, vbase,
                                                 kv_index, pos, active, fixed_len, kv_len_cap, o,
                                                 H, scale, kvmap, own_from, map_row0, nq, R);
+  else if (xattn_nt)
+    dec_attn_kernel<T, false, 8, true><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale,
+                                                          kbase, vbase, kv_index, pos, active,
+                                                          fixed_len, kv_len_cap, o, H, scale,
+                                                          nullptr, nullptr, 0, nq, R);
   else
-    dec_attn_kernel<T, false><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale, kbase,
-                                                 vbase, kv_index, pos, active, fixed_len,
-                                                 kv_len_cap, o, H, scale, nullptr, nullptr, 0, nq,
-                                                 R);
+    dec_attn_kernel<T, false, 8, false><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale,
+                                                           kbase, vbase, kv_index, pos, active,
+                                                           fixed_len, kv_len_cap, o, H, scale,
+                                                           nullptr, nullptr, 0, nq, R);
 }
 
 template void enc_attention<_Float16>(const _Float16*, const _Float16*, const _Float16*, _Float16*,

@@ -146,6 +146,11 @@ __global__ __launch_bounds__(256) void ln_dec_kernel(float* __restrict__ x,
     pb0 = *reinterpret_cast<const f32x4*>(pbias + i0);
     pb1 = *reinterpret_cast<const f32x4*>(pbias + i0 + 4);
   }
+  // the LayerNorm weights too: no load is left behind the two reductions
+  const f32x4 w0 = *reinterpret_cast<const f32x4*>(w + i0);
+  const f32x4 w1 = *reinterpret_cast<const f32x4*>(w + i0 + 4);
+  const f32x4 b0 = *reinterpret_cast<const f32x4*>(b + i0);
+  const f32x4 b1 = *reinterpret_cast<const f32x4*>(b + i0 + 4);
   __builtin_amdgcn_sched_barrier(0);
   const int act_r = active ? active[row] : 1;
   if (!act_r) {
@@ -199,7 +204,8 @@ __global__ __launch_bounds__(256) void ln_dec_kernel(float* __restrict__ x,
   const float scale = 1.0f / sqrtf(variance + 1e-5f);
   typename Elt<T>::v8 o;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) o[e] = to_t<T>(((v[e] - mean) * scale) * w[i0 + e] + b[i0 + e]);
+  for (int e = 0; e < 8; ++e)
+    o[e] = to_t<T>(((v[e] - mean) * scale) * (e < 4 ? w0[e] : w1[e - 4]) + (e < 4 ? b0[e] : b1[e - 4]));
   *reinterpret_cast<typename Elt<T>::v8*>(y + pack_index(row, i0, N)) = o;
 }
 
@@ -527,6 +533,92 @@ void logits_process(float* logits, const float* static_mask, const RowCtl* ctl, 
   lp_filter_kernel<<<g, LP_T, 0, st>>>(logits, static_mask, ctl, ws.flt, ws.parts, C);
   lp_probs_kernel<<<g, LP_T, 0, st>>>(ws.flt, ws.parts, ctl, ws.res, probs, logprobs, C);
   lp_pick_kernel<<<R, 64, 0, st>>>(logits, ws.flt, ws.parts, ws.res, ctl, out, C);
+}
+
+// Run-ahead greedy decoding: applies the token loop's per-row rules to the
+// step just run (whisper.cpp v1.8.2 whisper_full_with_state, the greedy
+// branch of its decoder loop; host restatement driver.inc, same order of
+// tests) and writes the next step's inputs. One workgroup; every row is
+// independent. The step's token records and the inputs chosen for the next
+// step go straight to the pinned host ring slot `*run_step % nslot`.
+__global__ __launch_bounds__(256) void row_advance_kernel(RowRun* __restrict__ run,
+                                                          int* __restrict__ run_step,
+                                                          const int* __restrict__ prompt,
+                                                          int* __restrict__ si,
+                                                          RowCtl* __restrict__ ctl,
+                                                          const TokOut* __restrict__ out,
+                                                          RunReport* __restrict__ rep, RunConst C) {
+  const int step = *run_step;
+  const int R = C.R;
+  RunReport* slot = rep + (long)(step % C.nslot) * R;
+  for (int r = threadIdx.x; r < R; r += blockDim.x) {
+    RowRun w = run[r];
+    const RowCtl k = ctl[r];
+    const TokOut t = out[r];
+    if (!w.stopped) {
+      if (k.sample) {
+        const int id = t.id;
+        const int i = w.ntok;
+        w.penult_id = w.last_id;
+        w.last_id = id;
+        w.ntok = i + 1;
+        bool stop = false;
+        if (id > C.beg) {
+          const int sd_new = 2 * (id - C.beg);
+          if (w.has_ts && w.seek_delta > sd_new && w.result_len < i) {
+            stop = true;  // (failed)
+          } else {
+            w.seek_delta = sd_new;
+            w.result_len = i + 1;
+            w.has_ts = 1;
+          }
+        }
+        if (!stop) {
+          if (id == C.eot || (C.max_tokens > 0 && i >= C.max_tokens) ||
+              (w.has_ts && w.seek + w.seek_delta + C.delta_min >= w.seek_end))
+            stop = true;
+          else if (i == C.n_max - 1)
+            stop = true;
+        }
+        if (stop) w.stopped = 1;
+      }
+      if (!w.stopped) w.fed++;
+    }
+    const int tok = w.fed < w.p_len ? prompt[(long)r * C.prompt_stride + w.fed]
+                                    : (w.ntok > 0 ? w.last_id : 0);
+    RowCtl n;
+    n.active = w.stopped ? 0 : 1;
+    n.sample = (!w.stopped && w.fed >= w.p_len - 1) ? 1 : 0;
+    n.is_initial = w.ntok == 0 ? 1 : 0;
+    n.last_ts = (w.ntok > 0 && w.last_id >= C.beg) ? 1 : 0;
+    n.penult_ts = (w.ntok < 2 || w.penult_id >= C.beg) ? 1 : 0;
+    n.has_ts = w.has_ts;
+    n.seek_delta = w.seek_delta;
+    n.want_probs = 0;
+    n.temperature = C.temperature;
+    n.want_nosp = (n.sample && n.is_initial) ? 1 : 0;
+    n.pad[0] = n.pad[1] = 0;
+    si[r] = tok;
+    si[R + r] = w.fed;
+    si[2 * R + r] = n.active;
+    ctl[r] = n;
+    run[r] = w;
+    RunReport o;
+    o.out = t;
+    o.tok = tok;
+    o.pos = w.fed;
+    o.act = n.active;
+    o.pad = 0;
+    o.next = n;
+    slot[r] = o;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) *run_step = step + 1;
+}
+
+void row_advance(RowRun* run, int* run_step, const int* prompt, int* stepin, RowCtl* ctl,
+                 const TokOut* out, RunReport* rep, const RunConst& C, hipStream_t st) {
+  row_advance_kernel<<<1, 256, 0, st>>>(run, run_step, prompt, stepin, ctl, out, rep, C);
 }
 
 

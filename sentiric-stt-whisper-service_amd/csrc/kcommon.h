@@ -12,6 +12,19 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// 16-/8-byte loads of bytes one CU reads once per launch (the decode cross K/V
+// streams): NT = non-temporal (`nt` cache policy), which keeps them from
+// displacing reusable lines; measured 43.3 -> 38.5 us for the large-v3 cross
+// K/V byte pattern at 32 rows (scripts/probe/stream_probe.hip)
+template <bool NT, typename V>
+__device__ __forceinline__ V ld_stream(const V* p) {
+  if constexpr (NT)
+    return __builtin_nontemporal_load(p);
+  else
+    return *p;
+}
 
 // Element type traits: T is _Float16 (ggml f16 files) or __bf16.
 template <typename T>

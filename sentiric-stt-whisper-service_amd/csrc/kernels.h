@@ -200,6 +200,39 @@ struct TokOut {
   float nosp;
   int pad;
 };
+// Run-ahead greedy decoding: the per-row stop / next-input rules of the
+// whisper_full token loop (driver.inc, the host restatement of whisper.cpp
+// v1.8.2's decoder loop) applied on the device after every step, so the next
+// step's inputs (stepin, RowCtl) are ready without a host round trip and the
+// host processes step k while step k+1 runs.
+struct RowRun {
+  int fed;          // positions fed so far (the next step feeds position `fed`)
+  int p_len;        // prompt length
+  int ntok;         // tokens generated
+  int last_id;      // last / penultimate generated token ids
+  int penult_id;
+  int has_ts;       // decoder.has_ts / seek_delta / result_len
+  int seek_delta;
+  int result_len;
+  int stopped;
+  int seek, seek_end;  // the clip's window position and end (centiseconds)
+  int pad;
+};
+struct RunConst {
+  int beg, eot, max_tokens, n_max, delta_min, R, nslot, prompt_stride;
+  float temperature;
+  int pad[3];
+};
+// what the host reads back per row and step (written straight into pinned
+// host memory by the advance kernel: no copy launch per step)
+struct RunReport {
+  TokOut out;        // the step's token record
+  int tok, pos, act, pad;  // the next step's inputs as the device set them
+  RowCtl next;
+};
+void row_advance(RowRun* run, int* run_step, const int* prompt, int* stepin, RowCtl* ctl,
+                 const TokOut* out, RunReport* rep, const RunConst& C, hipStream_t st);
+
 struct LogitsConst {
   int n_vocab;
   int eot;

@@ -606,3 +606,53 @@ def test_mxfp8_batch_equals_single(make_model):
         batched = [mwx.token_ids(ctx.segments(i)) for i in range(5)]
         singles = [mwx.token_ids(run_fresh(ctx, pcm, p)) for pcm in pcms]
     assert batched == singles and all(len(t) > 0 for t in batched)
+
+
+_RUN_MODES = r'''
+import json, sys
+sys.path.insert(0, "sentiric-stt-whisper-service_amd")
+import mwx
+path, max_tokens, inc = sys.argv[1], int(sys.argv[2]), float(sys.argv[3])
+ctx = mwx.Context.open(path)
+p = ctx.default_params(mwx.SAMPLING_GREEDY)
+p.token_timestamps = True
+p.suppress_nst = True
+p.no_speech_thold = 0.85
+p.entropy_thold = 2.40
+p.logprob_thold = -0.7
+p.temperature_inc = inc
+p.greedy.best_of = 5
+p.language = b"en"
+p.max_tokens = max_tokens
+secs = [30.0, 75.3, 12.5, 48.0, 3.0, 30.0]
+pcms = [mwx.pcm16_to_f32(mwx.synth_pcm16(k, int(s * 16000))) for k, s in enumerate(secs)]
+assert ctx.full_batch(pcms, p) == 0
+out = [[[s.t0, s.t1, s.text, [(t.id, t.tid, t.p, t.t0, t.t1) for t in s.tokens]]
+        for s in ctx.segments(i)] for i in range(len(pcms))]
+print(json.dumps(out))
+'''
+
+
+@pytest.mark.parametrize("max_tokens,inc", [(0, 0.0), (0, 0.2), (7, 0.0)])
+def test_runahead_decode_equals_synchronous_loop(make_model, max_tokens, inc):
+    """Run-ahead greedy decoding (the device applies the token loop's stop and
+    next-input rules after each step, the host reads step k while step k+1
+    runs) gives exactly the host-driven loop's results (MWX_NO_RUNAHEAD=1):
+    six clips of 3-75 s (long-form seeks, timestamps, EOT), the fallback
+    re-decodes (temperature > 0 runs the host loop), and the max_tokens stop."""
+    import json
+    import os
+    import subprocess
+    import sys
+    path = make_model("micro-rich")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = []
+    for extra in ({}, {"MWX_NO_RUNAHEAD": "1"}):
+        env = dict(os.environ)
+        env.update(extra)
+        r = subprocess.run([sys.executable, "-c", _RUN_MODES, path, str(max_tokens), str(inc)],
+                           cwd=root, env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    assert res[0] == res[1]
+    assert sum(len(s[3]) for c in res[0] for s in c) > 40
