@@ -64,6 +64,19 @@ __global__ __launch_bounds__(256) void stream_kv_kernel(const uint4* __restrict_
   if (acc == 0x12345u) out[threadIdx.x] = (float)acc;
 }
 
+// reads [p, p + n16 * 16) once (brings it into the Infinity Cache / L2)
+__global__ __launch_bounds__(256) void touch_kernel(const uint4* __restrict__ p, long n16, float* out) {
+  uint32_t acc = 0;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n16; i += (long)gridDim.x * 256 * 4) {
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = p[min(i + u * (long)gridDim.x * 256, n16 - 1)];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc += v[u].x ^ v[u].w;
+  }
+  if (acc == 0x12345u) out[threadIdx.x] = (float)acc;
+}
+
 int main(int argc, char** argv) {
   const int R = argc > 1 ? atoi(argv[1]) : 32;
   const int reps = argc > 2 ? atoi(argv[2]) : 10;
@@ -183,6 +196,42 @@ int main(int argc, char** argv) {
     e.pack_out = true;
     return e;
   };
+  hipStream_t s2;
+  CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+  hipEvent_t fk, jn;
+  CK(hipEventCreateWithFlags(&fk, hipEventDisableTiming));
+  CK(hipEventCreateWithFlags(&jn, hipEventDisableTiming));
+  // one whole decoder layer (11 launches); pf: a side-stream kernel reads
+  // layer l+1's weights while layer l runs (0 none, 1 at layer start, 2 after
+  // the cross-attention's launch)
+  auto full_layer = [&](int l, int pf) {
+    auto prefetch = [&]() {
+      CK(hipEventRecord(fk, s));
+      CK(hipStreamWaitEvent(s2, fk, 0));
+      const int ln = (l + 1) % L;
+      touch_kernel<<<512, 256, 0, s2>>>((const uint4*)wl(ln, 0), (long)(per_layer * 2 / 16), x + 4 * d);
+    };
+    if (pf == 1) prefetch();
+    layer_norm_dec<T>(x, lnw, lnb, hd, R, d, act, s, slab, 8, bias);
+    gemm_splitk_partials<T>(hd, wl(l, 0), R, 3 * d, d, slab, s);
+    dec_attention<T>(slab, 5, 3 * d, bias, kqs, kqs, (_Float16*)kself + (l & 1) * self_elems,
+                     (_Float16*)vself + (l & 1) * self_elems, nullptr, pos, act, 0, Tctx, od, R, H,
+                     1.0f, s, kvmap, kvown, 0, 1);
+    gemm_splitk_partials<T>(od, wl(l, 1), R, d, d, slab, s);
+    layer_norm_dec<T>(x, lnw, lnb, hd, R, d, act, s, slab, 5, bias);
+    gemm_splitk_partials<T>(hd, wl(l, 2), R, d, d, slab, s);
+    dec_attention<T>(slab, 5, d, bias, 1.0f, 1.0f, (_Float16*)ck + (l & 1) * cross_elems,
+                     (_Float16*)cv + (l & 1) * cross_elems, xidx, pos, act, Lc, Lc, od, R, H, kqs, s);
+    if (pf == 2) prefetch();
+    gemm_splitk_partials<T>(od, wl(l, 3), R, d, d, slab, s);
+    layer_norm_dec<T>(x, lnw, lnb, hd, R, d, act, s, slab, 5, bias);
+    gemm_decode<T>(EPI_GELU, hd, wl(l, 4), R, 4 * d, d, ep_gelu(), s);
+    gemm_splitk_partials<T>(ffd, wl(l, 5), R, d, 4 * d, slab, s);
+    if (pf && l == L - 1) {  // join the side stream
+      CK(hipEventRecord(jn, s2));
+      CK(hipStreamWaitEvent(s, jn, 0));
+    }
+  };
   struct Op {
     std::string name;
     int launches_per_layer;
@@ -235,6 +284,11 @@ int main(int argc, char** argv) {
        [&](int) {
          logits_process(logits, smask, ctl, tout, nullptr, nullptr, LCo, R, LPScratch{flt, parts, lres}, s);
        }},
+      {"FULL layer (11 launches)", 11, [&](int l) { full_layer(l, 0); }},
+      {"FULL layer + prefetch next at start", 11, [&](int l) { full_layer(l, 1); }},
+      {"FULL layer + prefetch next after xattn", 11, [&](int l) { full_layer(l, 2); }},
+      {"touch one layer's weights", 1,
+       [&](int l) { touch_kernel<<<512, 256, 0, s>>>((const uint4*)wl(l, 0), (long)(per_layer * 2 / 16), x + 4 * d); }},
       {"LEGACY layer GEMMs+LN (9 launches)", 9,
        [&](int l) {
          layer_norm_dec<T>(x, lnw, lnb, hd, R, d, act, s, slab, 8, bias);

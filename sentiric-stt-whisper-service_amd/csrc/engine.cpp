@@ -139,6 +139,7 @@ struct State {
   DBuf cross_ks, cross_vs;  // MX-fp8 cross cache: E8M0 scales (kv8)
   bool cross_kv8 = false;   // layout of cross_k / cross_v
   DBuf energy, pcm16;
+  DBuf meld, melpart;  // batched log-mel: per-clip descriptors, partial maxima
   DBuf aq, as;  // MX-fp8 activations (codes [rows][K], scales [rows][K/32])
   DBuf ibuf;  // small int arrays (slot maps)
   DBuf pro_pcm, pro_desc, pro_fs, pro_ft, pro_fc, pro_out;  // segment prosody

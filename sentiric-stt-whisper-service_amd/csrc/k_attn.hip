@@ -17,6 +17,7 @@
 //   sum, multiply by (float)(1/sum), round P to f16, then P.V in f32. K and V
 //   rows are streamed with 8 lanes per 128-B row (fully coalesced).
 #include <cstdlib>
+#include <type_traits>
 
 #include "kcommon.h"
 #include "kernels.h"
@@ -61,7 +62,6 @@ __global__ __launch_bounds__(256) void enc_attn_kernel(const _Float16* __restric
   const int srow = tid >> 3, sch = tid & 7;
   const int kso0 = srow * 64 + ((sch ^ (srow & 7)) << 3);  // (row+32)&7 == row&7
   const int vso0 = srow * VSTR + sch * 8;
-  uint4 rk0, rk1, rv0, rv1;
 #define GLOAD(kb)                                                                    \
   do {                                                                               \
     const int kr0 = min((kb) * 64 + srow, L - 1), kr1 = min((kb) * 64 + srow + 32, L - 1); \
@@ -84,11 +84,18 @@ __global__ __launch_bounds__(256) void enc_attn_kernel(const _Float16* __restric
   } while (0)
 
   const int nkb = (L + 63) / 64;
-  GLOAD(0);
-  SSTORE(0);
+  {
+    uint4 rk0, rk1, rv0, rv1;
+    GLOAD(0);
+    SSTORE(0);
+  }
   __syncthreads();
-  for (int kb = 0; kb < nkb; ++kb) {
+  // one 64-key tile; MASKED: the last tile of a length that is not a multiple
+  // of 64 (keys >= L get -inf); the full tiles run without the key test
+  auto tile = [&](const int kb, auto masked) {
+    constexpr bool MASKED = decltype(masked)::value;
     const int cur = kb & 1;
+    uint4 rk0, rk1, rv0, rv1;  // tile kb+1 in flight (global -> registers -> LDS)
     if (kb + 1 < nkb) GLOAD(kb + 1);
     // S^T = K Q^T : sacc[t][u] rows = keys 16t + 4g + r, col = query c16
     f32x4 sacc[4][2];
@@ -110,7 +117,7 @@ __global__ __launch_bounds__(256) void enc_attn_kernel(const _Float16* __restric
       }
     }
     // mask keys beyond L
-    if (kb * 64 + 64 > L) {
+    if constexpr (MASKED) {
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -134,16 +141,25 @@ __global__ __launch_bounds__(256) void enc_attn_kernel(const _Float16* __restric
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mnew = fmaxf(mrow[u], mx * scale_log2);
-      const float alpha = exp2f(mrow[u] - mnew);
+      // v_exp_f32 directly (exponents here are <= 0; the libm wrapper only
+      // adds the denormal-range rescale, for results far below f16 resolution)
+      const float alpha = __builtin_amdgcn_exp2f(mrow[u] - mnew);
       float ps[4][4];
       float rs = 0.0f;
+      // s * scale - m rounded twice as before (packed: v_pk_mul_f32 +
+      // v_pk_add_f32 on element pairs), then the sum in the same order
+      typedef float f32x2 __attribute__((ext_vector_type(2)));
+      const f32x2 sc2 = f32x2{scale_log2, scale_log2}, mn2 = f32x2{-mnew, -mnew};
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = exp2f(sacc[t][u][r] * scale_log2 - mnew);
-          ps[t][r] = p;
-          rs += p;
+        for (int r = 0; r < 4; r += 2) {
+          const f32x2 sv = f32x2{sacc[t][u][r], sacc[t][u][r + 1]};
+          const f32x2 xv = sv * sc2 + mn2;
+          ps[t][r] = __builtin_amdgcn_exp2f(xv[0]);
+          ps[t][r + 1] = __builtin_amdgcn_exp2f(xv[1]);
+          rs += ps[t][r];
+          rs += ps[t][r + 1];
         }
       rs += __shfl_xor(rs, 16, 64);
       rs += __shfl_xor(rs, 32, 64);
@@ -179,7 +195,12 @@ __global__ __launch_bounds__(256) void enc_attn_kernel(const _Float16* __restric
     }
     if (kb + 1 < nkb) SSTORE(cur ^ 1);
     __syncthreads();
-  }
+  };
+  for (int kb = 0; kb < nkb - 1; ++kb) tile(kb, std::false_type{});
+  if (L % 64)
+    tile(nkb - 1, std::true_type{});
+  else
+    tile(nkb - 1, std::false_type{});
 #undef GLOAD
 #undef SSTORE
   const int D = H * 64;

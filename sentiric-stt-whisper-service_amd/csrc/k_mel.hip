@@ -16,21 +16,29 @@
 // as upstream), plus the encoder's f16 time-major input window
 // melT[clip][1 + 3000 + 1][CPAD] (zero rows for the conv's t = -1 / 3000 taps).
 #include "kcommon.h"
+#include "kernels.h"
 
 namespace mwx {
 
 constexpr int MEL_FRAMES_PER_WG = 16;
 
-// tables: hann[400], cosT[400], sinT[400] (whisper.cpp global cache values)
+// tables: hann[400], cosT[400], sinT[400] (whisper.cpp global cache values).
+// All clips of a batch in one launch: grid (frame tiles of the longest clip,
+// clips); clip c's samples / mel rows are at the offsets of desc[c].
 __global__ __launch_bounds__(256) void mel_frames_kernel(
-    const float* __restrict__ pcm, int n, int n_len, int n_fft_frames,
+    const float* __restrict__ pcm_base, const MelClip* __restrict__ desc,
     const float* __restrict__ filters, int n_mels, const float* __restrict__ tables,
-    float* __restrict__ out) {
+    float* __restrict__ out_base) {
   __shared__ float xs[MEL_FRAMES_PER_WG][400];
   __shared__ float tc[400], ts[400];
   __shared__ float pw[MEL_FRAMES_PER_WG][204];
+  const MelClip dc = desc[blockIdx.y];
+  const int n = dc.n, n_len = dc.n_len, n_fft_frames = dc.n_fft;
+  const float* __restrict__ pcm = pcm_base + dc.pcm_off;
+  float* __restrict__ out = out_base + dc.mel_off;
   const int tid = threadIdx.x;
   const int i0 = blockIdx.x * MEL_FRAMES_PER_WG;
+  if (i0 >= n_len) return;
   const float floor_v = -10.0f;  // log10(1e-10)
   if (i0 >= n_fft_frames) {
     // constant frames (no signal): whole tile is log10(1e-10)
@@ -101,13 +109,20 @@ __global__ __launch_bounds__(256) void mel_frames_kernel(
   }
 }
 
-// per-clip global max of the raw log-mel (one workgroup per clip)
-__global__ __launch_bounds__(1024) void mel_max_kernel(const float* __restrict__ mel,
-                                                       long clip_stride, long count,
-                                                       float* __restrict__ mx) {
-  const float* p = mel + blockIdx.x * clip_stride;
+// per-clip global max of the raw log-mel: MEL_MAX_PARTS workgroups per clip
+// each reduce a slice into part[clip][p]; the normalisation takes the max of
+// the parts (max is exact, so the result does not depend on the split)
+constexpr int MEL_MAX_PARTS = 16;
+__global__ __launch_bounds__(1024) void mel_max_kernel(const float* __restrict__ mel_base,
+                                                       const MelClip* __restrict__ desc, int n_mels,
+                                                       float* __restrict__ part) {
+  const MelClip dc = desc[blockIdx.y];
+  const long count = (long)n_mels * dc.n_len;
+  const float* p = mel_base + dc.mel_off;
+  const long per = (count + MEL_MAX_PARTS - 1) / MEL_MAX_PARTS;
+  const long b = blockIdx.x * per, e = min(count, b + per);
   float v = -INFINITY;
-  for (long i = threadIdx.x; i < count; i += 1024) v = fmaxf(v, p[i]);
+  for (long i = b + threadIdx.x; i < e; i += 1024) v = fmaxf(v, p[i]);
   v = wave_max(v);
   __shared__ float red[16];
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
@@ -115,17 +130,26 @@ __global__ __launch_bounds__(1024) void mel_max_kernel(const float* __restrict__
   if (threadIdx.x < 64) {
     float w = threadIdx.x < 16 ? red[threadIdx.x] : -INFINITY;
     w = wave_max(w);
-    if (threadIdx.x == 0) mx[blockIdx.x] = w;
+    if (threadIdx.x == 0) part[blockIdx.y * MEL_MAX_PARTS + blockIdx.x] = w;
   }
 }
 
-// clamp at max - 8 and rescale: x = (max(x, mx - 8) + 4) / 4
-__global__ __launch_bounds__(256) void mel_norm_kernel(float* __restrict__ mel, long clip_stride,
-                                                       long count, const float* __restrict__ mx) {
+// clamp at max - 8 and rescale: x = (max(x, mx - 8) + 4) / 4; mx[clip] keeps
+// the clip's max
+__global__ __launch_bounds__(256) void mel_norm_kernel(float* __restrict__ mel_base,
+                                                       const MelClip* __restrict__ desc, int n_mels,
+                                                       const float* __restrict__ part,
+                                                       float* __restrict__ mx) {
+  const MelClip dc = desc[blockIdx.y];
+  const long count = (long)n_mels * dc.n_len;
+  float m = part[blockIdx.y * MEL_MAX_PARTS];
+#pragma unroll
+  for (int q = 1; q < MEL_MAX_PARTS; ++q) m = fmaxf(m, part[blockIdx.y * MEL_MAX_PARTS + q]);
+  if (blockIdx.x == 0 && threadIdx.x == 0) mx[blockIdx.y] = m;
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= count) return;
-  float* p = mel + blockIdx.y * clip_stride;
-  const float lo = mx[blockIdx.y] - 8.0f;
+  float* p = mel_base + dc.mel_off;
+  const float lo = m - 8.0f;
   float x = p[i];
   if (x < lo) x = lo;
   p[i] = (x + 4.0f) / 4.0f;
@@ -175,16 +199,16 @@ __global__ __launch_bounds__(256) void signal_energy_kernel(const float* __restr
 // ---------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------
-void launch_mel(const float* pcm, int n, int n_len, int n_fft_frames, const float* filters,
-                int n_mels, const float* tables, float* out, hipStream_t st) {
-  const int nwg = (n_len + MEL_FRAMES_PER_WG - 1) / MEL_FRAMES_PER_WG;
-  mel_frames_kernel<<<nwg, 256, 0, st>>>(pcm, n, n_len, n_fft_frames, filters, n_mels, tables, out);
-}
-void launch_mel_norm(float* mel, long clip_stride, long count, int n_clips, float* mx,
-                     hipStream_t st) {
-  mel_max_kernel<<<n_clips, 1024, 0, st>>>(mel, clip_stride, count, mx);
-  dim3 g((unsigned)((count + 255) / 256), n_clips);
-  mel_norm_kernel<<<g, 256, 0, st>>>(mel, clip_stride, count, mx);
+void launch_mel_batch(const float* pcm_base, const MelClip* desc, int n_clips, int max_n_len,
+                      const float* filters, int n_mels, const float* tables, float* mel_base,
+                      float* part, float* mx, hipStream_t st) {
+  if (n_clips <= 0 || max_n_len <= 0) return;
+  const dim3 gf((max_n_len + MEL_FRAMES_PER_WG - 1) / MEL_FRAMES_PER_WG, n_clips);
+  mel_frames_kernel<<<gf, 256, 0, st>>>(pcm_base, desc, filters, n_mels, tables, mel_base);
+  mel_max_kernel<<<dim3(MEL_MAX_PARTS, n_clips), 1024, 0, st>>>(mel_base, desc, n_mels, part);
+  const long count = (long)n_mels * max_n_len;
+  const dim3 gn((unsigned)((count + 255) / 256), n_clips);
+  mel_norm_kernel<<<gn, 256, 0, st>>>(mel_base, desc, n_mels, part, mx);
 }
 void launch_mel_window(const float* mel, long mel_clip_stride, const int* clip_of_slot,
                        const int* seek_of_slot, const int* n_len_of_slot, int n_mels, int T,

@@ -110,10 +110,17 @@ int gemm_splitk_partials(const T* Ap, const DecW<T>& W, int M, int N, int K, flo
 template <typename T>
 bool gemm_decode(int epi, const T* Ap, const DecW<T>& W, int M, int N, int K, const EpiParams& P,
                  hipStream_t st);
-void launch_mel(const float* pcm, int n, int n_len, int n_fft_frames, const float* filters,
-                int n_mels, const float* tables, float* out, hipStream_t st);
-void launch_mel_norm(float* mel, long clip_stride, long count, int n_clips, float* mx,
-                     hipStream_t st);
+// Log-mel of a batch of clips in one pass (three launches): clip c's samples
+// at pcm_base + desc[c].pcm_off (n), its mel [n_mels][n_len] at mel_base +
+// desc[c].mel_off, normalised in place; mx[c] = the clip's raw max; part:
+// n_clips * 16 floats of scratch.
+struct MelClip {
+  long pcm_off, mel_off;
+  int n, n_len, n_fft, pad;
+};
+void launch_mel_batch(const float* pcm_base, const MelClip* desc, int n_clips, int max_n_len,
+                      const float* filters, int n_mels, const float* tables, float* mel_base,
+                      float* part, float* mx, hipStream_t st);
 void launch_mel_window(const float* mel, long mel_clip_stride, const int* clip_of_slot,
                        const int* seek_of_slot, const int* n_len_of_slot, int n_mels, int T,
                        int cpad, _Float16* melT, int n_slots, hipStream_t st);
