@@ -425,6 +425,73 @@ def dry_run(args, world, rank, local):
     return 0
 
 
+def stream_bench(args):
+    """Streaming re-transcription latency: one live stream
+    through the service path (SttEngine + StreamSession over libmwx_stt.so,
+    the reference's gRPC loop without the transport) fed 0.5-s chunks of a
+    synthetic 16 kHz PCM16 stream; every chunk triggers a re-transcription of
+    the whole growing buffer (up to the 30-s cap), as the reference does.
+    Reports the wall time of each partial (chunk in -> events out).
+    MWX_NO_MEL_CACHE=1 disables the incremental log-mel for an A/B."""
+    import ctypes as C
+    import mwx
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    wt = mwx.GGML_BF16 if args.wtype == "bf16" else mwx.GGML_F16
+    d = os.environ.get("TMPDIR", "/tmp")
+    name = f"mwx_bench_{args.arch}_{args.wtype}.bin"
+    path = os.path.join(d, name)
+    if not os.path.exists(path):
+        tmp = path + f".tmp{os.getpid()}"
+        mwx.write_synthetic_model(tmp, args.arch, wt, 0)
+        os.replace(tmp, path)
+    L = C.CDLL(os.path.join(ROOT, "sentiric-stt-whisper-service_amd", "libmwx_stt.so"))
+    L.mwx_stt_new_ex.restype = C.c_void_p
+    L.mwx_stt_new_ex.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_char_p,
+                                 C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
+    L.mwx_stt_stream_new.restype = C.c_void_p
+    L.mwx_stt_stream_new.argtypes = [C.c_void_p]
+    L.mwx_stt_stream_free.argtypes = [C.c_void_p]
+    L.mwx_stt_stream_feed.restype = C.c_int
+    L.mwx_stt_stream_feed.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_char_p, C.c_int]
+    L.mwx_stt_free.argtypes = [C.c_void_p]
+    beam = max(1, args.beam)
+    eng = L.mwx_stt_new_ex(d.encode(), name.encode(), 1, 20000, beam, b"en", 500, local, 1, 2000,
+                           8000)
+    if not eng:
+        raise RuntimeError("SttEngine init failed")
+    cap = 1 << 22
+    out = C.create_string_buffer(cap)
+    lat = []
+    for rep in range(args.warmup + args.steps):
+        raw = mwx.synth_pcm16(100 + rep, 30 * 16000).tobytes()
+        s = L.mwx_stt_stream_new(eng)
+        for p in range(0, len(raw), 16000):  # 0.5-s chunks = stream_buffer_samples
+            t0 = time.perf_counter()
+            r = L.mwx_stt_stream_feed(s, raw[p:p + 16000], len(raw[p:p + 16000]), out, cap)
+            t1 = time.perf_counter()
+            if r < 0:
+                raise RuntimeError(f"stream feed rc={r}")
+            if rep >= args.warmup:
+                lat.append((t1 - t0) * 1e3)
+        L.mwx_stt_stream_feed(s, b"", 0, out, cap)  # end of speech (final, not timed)
+        L.mwx_stt_stream_free(s)
+    L.mwx_stt_free(eng)
+    lat = np.array(lat)
+    line = {"metric": "streaming partial latency (0.5-s cadence, re-transcription of the growing "
+                      "buffer)", "value": round(float(np.percentile(lat, 50)), 2), "unit": "ms",
+            "higher_is_better": False, "p95_ms": round(float(np.percentile(lat, 95)), 2),
+            "max_ms": round(float(lat.max()), 2), "mean_ms": round(float(lat.mean()), 2),
+            "partials": int(len(lat)), "streams": args.steps, "n_gpus": 1,
+            "dtype": args.wtype, "data": "synthetic (seeded 16 kHz PCM16 stream, seeded weights)",
+            "mel_cache": os.environ.get("MWX_NO_MEL_CACHE") is None,
+            "config": {"workload": f"whisper-{args.arch} {args.wtype}: one 30-s stream in 0.5-s "
+                                   f"chunks through SttEngine/StreamSession, "
+                                   f"{'beam-%d' % beam if beam > 1 else 'greedy'} decode until "
+                                   f"the model stops"}}
+    print(json.dumps(line), flush=True)
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1,
@@ -450,6 +517,8 @@ def main():
                     help="PCM in host memory, uploaded inside each step (PCIe-inclusive rate)")
     ap.add_argument("--pcm16", action="store_true",
                     help="with --host-input: upload int16 PCM, converted on the device")
+    ap.add_argument("--stream", action="store_true",
+                    help="streaming partial-latency leg (SURVEY.md §8 f3) instead of transcription")
     ap.add_argument("--prosody", action="store_true",
                     help="segment-prosody leg (SURVEY.md §8 f4) instead of transcription")
     args = ap.parse_args()
@@ -465,6 +534,8 @@ def main():
         return dry_run(args, world, rank, local)
     if args.prosody:
         return prosody_bench(args)
+    if args.stream:
+        return stream_bench(args)
 
     import torch
     dist = init_dist(world, local)

@@ -140,6 +140,12 @@ struct State {
   bool cross_kv8 = false;   // layout of cross_k / cross_v
   DBuf energy, pcm16;
   DBuf meld, melpart;  // batched log-mel: per-clip descriptors, partial maxima
+  // incremental log-mel (streaming re-transcription of a growing buffer):
+  // ping-pong slots of this state's previous samples and raw log-mel
+  DBuf melc_pcm[2], melc_raw[2];
+  int melc_slot = 0;  // slot holding the previous call's data
+  int melc_n = 0;     // its samples (0: nothing cached)
+  int melc_len = 0;   // its n_len
   DBuf aq, as;  // MX-fp8 activations (codes [rows][K], scales [rows][K/32])
   DBuf ibuf;  // small int arrays (slot maps)
   DBuf pro_pcm, pro_desc, pro_fs, pro_ft, pro_fc, pro_out;  // segment prosody

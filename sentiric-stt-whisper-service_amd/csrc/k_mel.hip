@@ -36,18 +36,59 @@ __global__ __launch_bounds__(256) void mel_frames_kernel(
   const int n = dc.n, n_len = dc.n_len, n_fft_frames = dc.n_fft;
   const float* __restrict__ pcm = pcm_base + dc.pcm_off;
   float* __restrict__ out = out_base + dc.mel_off;
+  float* __restrict__ save_raw = dc.save_raw;
   const int tid = threadIdx.x;
   const int i0 = blockIdx.x * MEL_FRAMES_PER_WG;
   if (i0 >= n_len) return;
+  if (dc.save_pcm) {  // this tile's hop range of samples, for the next call
+    const int j1 = min(n, (i0 + MEL_FRAMES_PER_WG) * 160);
+    for (int j = i0 * 160 + tid; j < j1; j += 256) dc.save_pcm[j] = pcm[j];
+  }
   const float floor_v = -10.0f;  // log10(1e-10)
   if (i0 >= n_fft_frames) {
     // constant frames (no signal): whole tile is log10(1e-10)
     for (int idx = tid; idx < MEL_FRAMES_PER_WG * n_mels; idx += 256) {
       const int f = idx % MEL_FRAMES_PER_WG, m = idx / MEL_FRAMES_PER_WG;
       const int i = i0 + f;
-      if (i < n_len) out[(size_t)m * n_len + i] = floor_v;
+      if (i < n_len) {
+        out[(size_t)m * n_len + i] = floor_v;
+        if (save_raw) save_raw[(size_t)m * n_len + i] = floor_v;
+      }
     }
     return;
+  }
+  // incremental: frame i reads padded samples [160 i, 160 i + 400), i.e.
+  // samples [160 i - 200, 160 i + 200) (and samples 1..200 reflected for the
+  // first frames). If every sample the tile reads is bit-identical to the
+  // previous call's and lay inside that call's clip, the tile's raw log-mel
+  // is the previous call's (same inputs, same arithmetic).
+  if (dc.n_prev > 0) {
+    const int last = min(i0 + MEL_FRAMES_PER_WG, n_fft_frames) - 1;
+    const int lo = max(0, i0 * 160 - 200), hi = last * 160 + 200;
+    bool same = hi <= n && hi <= dc.n_prev && last < dc.len_prev;
+    if (same) {
+      for (int j = lo + tid; j < hi; j += 256)
+        same &= __float_as_uint(pcm[j]) == __float_as_uint(dc.prev_pcm[j]);
+    }
+    if (__syncthreads_and(same)) {
+      for (int idx = tid; idx < MEL_FRAMES_PER_WG * n_mels; idx += 256) {
+        const int f = idx % MEL_FRAMES_PER_WG, m = idx / MEL_FRAMES_PER_WG;
+        const int i = i0 + f;
+        if (i > last) continue;
+        const float r = dc.prev_raw[(size_t)m * dc.len_prev + i];
+        out[(size_t)m * n_len + i] = r;
+        if (save_raw) save_raw[(size_t)m * n_len + i] = r;
+      }
+      // frames of the tile past n_fft_frames (the last tile): log10(1e-10)
+      for (int idx = tid; idx < MEL_FRAMES_PER_WG * n_mels; idx += 256) {
+        const int f = idx % MEL_FRAMES_PER_WG, m = idx / MEL_FRAMES_PER_WG;
+        const int i = i0 + f;
+        if (i <= last || i >= n_len) continue;
+        out[(size_t)m * n_len + i] = floor_v;
+        if (save_raw) save_raw[(size_t)m * n_len + i] = floor_v;
+      }
+      return;
+    }
   }
   for (int j = tid; j < 400; j += 256) {
     tc[j] = tables[400 + j];
@@ -106,6 +147,7 @@ __global__ __launch_bounds__(256) void mel_frames_kernel(
       r = floor_v;
     }
     out[(size_t)m * n_len + i] = r;
+    if (save_raw) save_raw[(size_t)m * n_len + i] = r;
   }
 }
 

@@ -114,9 +114,21 @@ bool gemm_decode(int epi, const T* Ap, const DecW<T>& W, int M, int N, int K, co
 // at pcm_base + desc[c].pcm_off (n), its mel [n_mels][n_len] at mel_base +
 // desc[c].mel_off, normalised in place; mx[c] = the clip's raw max; part:
 // n_clips * 16 floats of scratch.
+// Incremental log-mel (streaming re-transcription): with prev_pcm set, a tile
+// of frames whose input samples equal the previous call's (and were real
+// samples then) copies its raw log-mel from prev_raw instead of recomputing
+// it; save_pcm / save_raw (the other slot of the state's ping-pong cache)
+// receive this call's samples and raw log-mel for the next call.
 struct MelClip {
   long pcm_off, mel_off;
-  int n, n_len, n_fft, pad;
+  int n, n_len, n_fft;
+  int n_prev;    // samples of the previous call on this state (0: no cache)
+  int len_prev;  // its n_len (stride of prev_raw)
+  int pad;
+  const float* prev_pcm;  // [n_prev]
+  const float* prev_raw;  // [n_mels][len_prev], before normalisation
+  float* save_pcm;        // [n] or nullptr
+  float* save_raw;        // [n_mels][n_len] or nullptr
 };
 void launch_mel_batch(const float* pcm_base, const MelClip* desc, int n_clips, int max_n_len,
                       const float* filters, int n_mels, const float* tables, float* mel_base,

@@ -407,12 +407,13 @@ class Context:
     def hparam(self, name: str) -> int:
         return getattr(lib(), f"mwx_{name}")(self.ctx)
 
-    def test_mel(self, pcm: np.ndarray) -> np.ndarray:
+    def test_mel(self, pcm: np.ndarray, state_index: int = 0) -> np.ndarray:
         pcm = np.ascontiguousarray(pcm, dtype=np.float32)
         n_mels = self.hparam("n_mels")
         n_len = (len(pcm) + 480000) // 160
         out = np.empty((n_mels, n_len), dtype=np.float32)
-        r = lib().mwx_test_mel(self.ctx, self.state(), fptr(pcm), len(pcm), fptr(out), out.size)
+        r = lib().mwx_test_mel(self.ctx, self.state(state_index), fptr(pcm), len(pcm), fptr(out),
+                               out.size)
         if r != n_len:
             raise RuntimeError(f"mwx_test_mel returned {r}")
         return out

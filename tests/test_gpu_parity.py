@@ -36,6 +36,31 @@ def test_mel_parity(make_model, arch, seconds):
     np.testing.assert_allclose(dev, ref, atol=1e-4, rtol=0)  # north-star tolerance
 
 
+def test_incremental_mel_equals_fresh(make_model):
+    """Streaming re-transcription: a state that saw a
+    buffer reuses the raw log-mel of every frame tile whose samples are
+    unchanged. A growing 0.5-s-cadence buffer, an edit in the middle, a
+    shorter buffer (new stream) and a long one, each bit-identical to the
+    log-mel computed on a fresh state, and to the oracle within 1e-4."""
+    path = make_model("micro-v3")
+    full = pcm_clip(6, 36.0)
+    edited = full[:9 * 16000].copy()
+    edited[4 * 16000 + 77] += 0.25
+    seq = [full[:k * 8000] for k in (1, 2, 3, 4, 9, 10, 11)] + [edited, full[:9 * 16000],
+                                                                full[:30 * 16000],
+                                                                full[:30 * 16000 + 160 * 7 + 3],
+                                                                full[:2 * 16000], full]
+    o = orc.Oracle(path)
+    with mwx.Context.open(path) as ctx:
+        for j, pcm in enumerate(seq):
+            inc = ctx.test_mel(pcm, state_index=0)
+            fresh = ctx.test_mel(pcm, state_index=1 + j)
+            assert np.array_equal(inc, fresh), (j, len(pcm))
+            if j in (3, 7, 11):
+                ref, _ = o.mel(pcm)
+                np.testing.assert_allclose(inc, ref, atol=1e-4, rtol=0)
+
+
 # ---------------------------------------------------------------- encoder
 def test_encoder_and_cross_kv_parity(micro):
     ctx, o, _ = micro
