@@ -231,7 +231,7 @@ void enc_attention(const _Float16* q, const _Float16* k, const _Float16* vt, T* 
 constexpr int DEC_MAX_KEYS = 1536;
 
 __device__ __forceinline__ float block_max_256(float v, float* red) {
-  v = wave_max(v);
+  v = wave_max_dpp(v);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   __syncthreads();
   if (lane == 0) red[wid] = v;
@@ -239,7 +239,7 @@ __device__ __forceinline__ float block_max_256(float v, float* red) {
   return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 }
 __device__ __forceinline__ double block_sum_256d(double v, double* red) {
-  v = wave_sum_d(v);
+  v = wave_sum_d_dpp(v);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   __syncthreads();
   if (lane == 0) red[wid] = v;
@@ -675,7 +675,7 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
   for (int q = 0; q < NQ; ++q) {
     float m = -INFINITY;
     for (int j = tid; j < n; j += 256) m = fmaxf(m, sc[q][j]);
-    mx[q] = wave_max(m);
+    mx[q] = wave_max_dpp(m);
   }
   if (lane == 0)
 #pragma unroll
@@ -693,7 +693,7 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
       sc[q][j] = e;
       sm += (double)e;
     }
-    sum[q] = wave_sum_d(sm);
+    sum[q] = wave_sum_d_dpp(sm);
   }
   if (lane == 0)
 #pragma unroll

@@ -182,7 +182,7 @@ __global__ __launch_bounds__(256) void ln_dec_kernel(float* __restrict__ x,
 #pragma unroll
     for (int e = 0; e < 8; ++e) s += (double)v[e];
   }
-  s = wave_sum_d(s);
+  s = wave_sum_d_dpp(s);
   if (lane == 0) red[0][wid] = s;
   __syncthreads();
   s = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
@@ -195,7 +195,7 @@ __global__ __launch_bounds__(256) void ln_dec_kernel(float* __restrict__ x,
       s2 += (double)(d * d);
     }
   }
-  s2 = wave_sum_d(s2);
+  s2 = wave_sum_d_dpp(s2);
   if (lane == 0) red[1][wid] = s2;
   __syncthreads();
   if (!own) return;
@@ -274,7 +274,7 @@ __device__ __forceinline__ void sfor(F&& f) {
 }
 
 __device__ __forceinline__ float bmax256(float v, float* red) {
-  v = wave_max(v);
+  v = wave_max_dpp(v);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   __syncthreads();
   if (lane == 0) red[wid] = v;
@@ -290,7 +290,7 @@ __device__ __forceinline__ float bsum256(float v, float* red) {
   return (red[0] + red[1]) + (red[2] + red[3]);
 }
 __device__ __forceinline__ double bsum256d(double v, double* red) {
-  v = wave_sum_d(v);
+  v = wave_sum_d_dpp(v);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   __syncthreads();
   if (lane == 0) red[wid] = v;

@@ -111,4 +111,44 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   return v;
 }
 
+// Wave reductions without LDS round trips: DPP steps inside each 16-lane row
+// (xor 1, xor 2 by quad_perm, then row_half_mirror and row_mirror pair lanes
+// i and 7-i / 15-i), then the four row results read with v_readlane and
+// combined as (r0 + r1) + (r2 + r3); every lane gets the result. A
+// ds_bpermute shuffle costs an LDS round trip per step (six per reduction,
+// twelve for a double); these cost a few cycles each.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const uint64_t u = __double_as_longlong(v);
+  const uint64_t lo = dpp_u32<CTRL>((uint32_t)u), hi = dpp_u32<CTRL>((uint32_t)(u >> 32));
+  return __longlong_as_double((long long)((hi << 32) | lo));
+}
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+  const uint64_t u = __double_as_longlong(v);
+  const uint64_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, lane);
+  const uint64_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), lane);
+  return __longlong_as_double((long long)((hi << 32) | lo));
+}
+__device__ __forceinline__ double wave_sum_d_dpp(double v) {
+  v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f64<0x141>(v);  // row_half_mirror
+  v += dpp_f64<0x140>(v);  // row_mirror
+  return (readlane_f64(v, 0) + readlane_f64(v, 16)) + (readlane_f64(v, 32) + readlane_f64(v, 48));
+}
+__device__ __forceinline__ float wave_max_dpp(float v) {
+  v = fmaxf(v, __uint_as_float(dpp_u32<0xB1>(__float_as_uint(v))));
+  v = fmaxf(v, __uint_as_float(dpp_u32<0x4E>(__float_as_uint(v))));
+  v = fmaxf(v, __uint_as_float(dpp_u32<0x141>(__float_as_uint(v))));
+  v = fmaxf(v, __uint_as_float(dpp_u32<0x140>(__float_as_uint(v))));
+  return fmaxf(fmaxf(__uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(v), 0)),
+                     __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(v), 16))),
+               fmaxf(__uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(v), 32)),
+                     __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(v), 48))));
+}
+
 }  // namespace mwx
