@@ -510,6 +510,9 @@ def main():
     ap.add_argument("--clip-seconds", type=float, default=30.0,
                     help="clip length (> 30: long-form, windows decoded one after another)")
     ap.add_argument("--perf-class", default="dec_attn_cross")
+    ap.add_argument("--lanes", type=int, default=1,
+                    help="concurrent batches (host threads, each with its own states and HIP "
+                         "stream), as the SttEngine's parallel_requests batchers run them")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fp8", action="store_true",
                     help="MX-fp8 compute (C5): encoder, cross-K/V and decoder weight GEMMs, cross K/V cache")
@@ -573,50 +576,95 @@ def main():
 
     # inputs resident in HBM before the timed region (the PCIe-inclusive rate,
     # host buffers uploaded inside the step, is --host-input)
+    lanes = max(1, args.lanes)
+    if lanes > 1 and args.host_input:
+        raise SystemExit("bench.py: --lanes > 1 needs HBM-resident input (no --host-input)")
+    for i in range(lanes * args.clips):  # all states exist before any lane thread runs
+        ctx.state(i)
     if args.host_input and args.pcm16:
         p16s = [mwx.synth_pcm16(k, n_samp) for k in shard.clip_ids(rank, args.clips)]
-        run_batch = lambda: ctx.full_batch_pcm16(p16s, p)  # noqa: E731
+        run_batch = lambda lane: ctx.full_batch_pcm16(p16s, p)  # noqa: E731
     elif args.host_input:
-        run_batch = lambda: ctx.full_batch(pcms, p)  # noqa: E731
+        run_batch = lambda lane: ctx.full_batch(pcms, p)  # noqa: E731
     else:
         dev = [ctx.upload(x) for x in pcms]
-        run_batch = lambda: ctx.full_batch_device(dev, p)  # noqa: E731
+        run_batch = lambda lane: ctx.full_batch_device(dev, p, lane * args.clips)  # noqa: E731
 
-    def step():
-        rc = run_batch()
+    def step(lane):
+        """One batch of `clips` clips on lane `lane` (states lane*clips ..):
+        mel -> encoder -> cross K/V -> decode; returns the packed token records."""
+        rc = run_batch(lane)
         if rc != 0:
             raise RuntimeError(f"mwx_full_batch rc={rc}")
-        block = shard.pack_records([[(t.id, t.t0, t.t1, t.p) for s in ctx.segments(c)
-                                     for t in s.tokens] for c in range(args.clips)], max_tok)
+        s0 = lane * args.clips
+        return shard.pack_records([[(t.id, t.t0, t.t1, t.p) for s in ctx.segments(s0 + c)
+                                    for t in s.tokens] for c in range(args.clips)], max_tok)
+
+    def gather(block):
         # RCCL over xGMI: every rank's token records (id, t0, t1, p) to rank 0
         g = shard.gather_to_rank0(dist, block, device="cuda")
         if g is not None:
             gathered["tokens"] = g
 
-    for _ in range(args.warmup):
-        step()
+    def run_steps(n):
+        """n batches spread round-robin over the lanes; each lane is a host
+        thread driving its own states and HIP stream (the SttEngine's
+        parallel_requests batchers), so one lane's encoder / host work overlaps
+        another lane's decode. Gathers run afterwards in batch order."""
+        if lanes == 1:
+            for _ in range(n):
+                gather(step(0))
+            return
+        import threading
+        out = [[] for _ in range(lanes)]
+        errs = []
+
+        def lane_loop(lane):
+            try:
+                for _ in range(len(range(lane, n, lanes))):
+                    out[lane].append(step(lane))
+            except Exception as ex:  # re-raised in the main thread
+                errs.append(ex)
+
+        th = [threading.Thread(target=lane_loop, args=(i,)) for i in range(lanes)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if errs:
+            raise errs[0]
+        for i in range(n):
+            gather(out[i % lanes][i // lanes])
+
+    for lane in range(lanes):
+        for _ in range(args.warmup):
+            gather(step(lane))
     L = mwx.lib()
-    st0 = ctx.state(0)  # workspace / stream owner of the batch
-    L.mwx_perf_read(st0, None, None)
+    owners = [ctx.state(lane * args.clips) for lane in range(lanes)]  # workspace / stream owners
     # the dominant kernel's class, plus the encoder GEMMs (MFMA fraction,
     # SURVEY.md §8 d asks for both bounds), timed in the same steps
     classes = [args.perf_class] + (["enc_gemm"] if args.perf_class != "enc_gemm" else [])
-    L.mwx_perf_enable(st0, ",".join(classes).encode())
+    for so in owners:
+        L.mwx_perf_read(so, None, None)
+        L.mwx_perf_enable(so, ",".join(classes).encode())
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    run_steps(args.steps)
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
     import ctypes
     timed = {}
     for cls in classes:
-        tms, nlc = ctypes.c_double(), ctypes.c_int()
-        L.mwx_perf_read_class(st0, cls.encode(), ctypes.byref(tms), ctypes.byref(nlc))
-        timed[cls] = (tms.value, nlc.value)
-    L.mwx_perf_enable(st0, None)
+        tot, cnt = 0.0, 0
+        for so in owners:  # summed over the lanes' states
+            tms, nlc = ctypes.c_double(), ctypes.c_int()
+            L.mwx_perf_read_class(so, cls.encode(), ctypes.byref(tms), ctypes.byref(nlc))
+            tot, cnt = tot + tms.value, cnt + nlc.value
+        timed[cls] = (tot, cnt)
+    for so in owners:
+        L.mwx_perf_enable(so, None)
     tot_ms, nl = ctypes.c_double(timed[args.perf_class][0]), ctypes.c_int(timed[args.perf_class][1])
     if dist is not None:
         e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -704,6 +752,7 @@ def main():
                 "global_batch": world * args.clips,
                 "seq_len": 1500,
                 "parallelism": f"dp{world}",
+                "lanes": lanes,
             },
             "audio_sec_per_s_per_gpu": round(value / world, 2),
             "rtf": round(elapsed / audio_s * world, 6),

@@ -278,7 +278,7 @@ __device__ __forceinline__ float dpp_sum8(float d) {
 // written to the cache and taken from LDS (its cache line may be stale in L1).
 // The loop body is straight-line (two batches per trip, no early exit), so the
 // compiler keeps exactly one batch in flight with counted vmcnt waits.
-template <typename T, bool SELF, int UBX = 8, bool NTL = !SELF>
+template <typename T, bool SELF, int UBX = 8, bool NTL = !SELF, int NBC = 0>
 __global__ __launch_bounds__(256) void dec_attn_kernel(
     const float* __restrict__ P, int KS, int pcols, const float* __restrict__ bias, float qscale,
     float kscale, _Float16* __restrict__ kbase, _Float16* __restrict__ vbase,
@@ -328,7 +328,9 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
   const long rstride = (long)H * cap * 64;
   // rows per 8-lane group per batch (cross: UBX, tunable), BR rows per batch
   constexpr int UB = UBX, BR = 32 * UB;
-  const int nb = (n + BR - 1) / BR;
+  // NBC > 0 (cross over the 1500 encoder frames): the batch count is a
+  // compile-time constant, so the K / V stream below is fully unrolled
+  const int nb = NBC > 0 ? NBC : (n + BR - 1) / BR;
   // rows past the end are clamped to the last OLD row (self: the new row is
   // being written by this workgroup and is taken from LDS instead)
   const int jmax = SELF ? max(n - 2, 0) : n - 1;
@@ -420,37 +422,24 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
       if (c == 0 && j < n) sc[j] = d * scale;
     }
   };
-  if constexpr (SELF) {
-    // <= 4 batches of 128 rows at UB = 4 (n <= 448): latency-bound, one batch
-    // per trip (loading V batch 0 together with K batch 0 measured 10% slower
-    // at UB = 8: occupancy 4 -> 3)
-    for (int b = 0; wave_busy && b < nb; ++b) {
-      if (b > 0) LOADROWS(ka, K, b)
-      score_batch(ka, b);
+  // softmax over the n scores in LDS (ggml order: f32 max, exp, double sum,
+  // P = f16(e * (float)(1/sum)))
+  auto softmax = [&]() {
+    __syncthreads();
+    float mx = -INFINITY;
+    for (int j = tid; j < n; j += 256) mx = fmaxf(mx, sc[j]);
+    mx = block_max_256(mx, redf);
+    double sum = 0.0;
+    for (int j = tid; j < n; j += 256) {
+      const float e = expf(sc[j] - mx);
+      sc[j] = e;
+      sum += (double)e;
     }
-  } else {
-    for (int b = 0; b < nb; b += 2) {  // (odd nb: one clamped batch extra)
-      LOADROWS(kb2, K, b + 1)
-      score_batch(ka, b);
-      LOADROWS(ka, K, b + 2)
-      score_batch(kb2, b + 1);
-    }
-  }
-  LOADROWS0(ka, V)
-  __syncthreads();
-  float mx = -INFINITY;
-  for (int j = tid; j < n; j += 256) mx = fmaxf(mx, sc[j]);
-  mx = block_max_256(mx, redf);
-  double sum = 0.0;
-  for (int j = tid; j < n; j += 256) {
-    const float e = expf(sc[j] - mx);
-    sc[j] = e;
-    sum += (double)e;
-  }
-  sum = block_sum_256d(sum, redd);
-  const float inv = (float)(1.0 / sum);
-  for (int j = tid; j < n; j += 256) sc[j] = (float)(_Float16)(sc[j] * inv);
-  __syncthreads();
+    sum = block_sum_256d(sum, redd);
+    const float inv = (float)(1.0 / sum);
+    for (int j = tid; j < n; j += 256) sc[j] = (float)(_Float16)(sc[j] * inv);
+    __syncthreads();
+  };
   float acc[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) acc[e] = 0.0f;
@@ -479,11 +468,58 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
     }
   };
   if constexpr (SELF) {
+    // <= 4 batches of 128 rows at UB = 4 (n <= 448): latency-bound, one batch
+    // per trip (loading V batch 0 together with K batch 0 measured 10% slower
+    // at UB = 8: occupancy 4 -> 3)
+    for (int b = 0; wave_busy && b < nb; ++b) {
+      if (b > 0) LOADROWS(ka, K, b)
+      score_batch(ka, b);
+    }
+    LOADROWS0(ka, V)
+    softmax();
     for (int b = 0; wave_busy && b < nb; ++b) {
       if (b > 0) LOADROWS(ka, V, b)
       pv_batch(ka, b);
     }
+  } else if constexpr (NBC > 0) {
+    // cross with a compile-time even batch count (n = 1500: 6): the K batches
+    // and then the V batches form one load stream through the two register
+    // buffers (loops of constant trip count, last trips peeled), no batch is loaded past the last one (the
+    // runtime loop below loads a clamped K and V batch past the end, and its
+    // K -> V hand-over drains every load), and V batches 0 and 1 are in
+    // flight across the softmax
+    static_assert(NBC % 2 == 0 && NBC >= 4, "even batch count");
+#pragma unroll 1
+    for (int b = 0; b < NBC - 2; b += 2) {
+      LOADROWS(kb2, K, b + 1)
+      score_batch(ka, b);
+      LOADROWS(ka, K, b + 2)
+      score_batch(kb2, b + 1);
+    }
+    LOADROWS(kb2, K, NBC - 1)
+    score_batch(ka, NBC - 2);
+    LOADROWS(ka, V, 0)
+    score_batch(kb2, NBC - 1);
+    LOADROWS(kb2, V, 1)
+    softmax();
+#pragma unroll 1
+    for (int b = 0; b < NBC - 2; b += 2) {
+      pv_batch(ka, b);
+      LOADROWS(ka, V, b + 2)
+      pv_batch(kb2, b + 1);
+      LOADROWS(kb2, V, b + 3)
+    }
+    pv_batch(ka, NBC - 2);
+    pv_batch(kb2, NBC - 1);
   } else {
+    for (int b = 0; b < nb; b += 2) {  // (odd nb: one clamped batch extra)
+      LOADROWS(kb2, K, b + 1)
+      score_batch(ka, b);
+      LOADROWS(ka, K, b + 2)
+      score_batch(kb2, b + 1);
+    }
+    LOADROWS0(ka, V)
+    softmax();
     for (int b = 0; b < nb; b += 2) {
       LOADROWS(kb2, V, b + 1)
       pv_batch(ka, b);
@@ -534,7 +570,7 @@ __device__ __forceinline__ f16x8 dequant_h8(uint2 raw, uint32_t e) {
   return f16x8{a[0], a[1], b[0], b[1], c[0], c[1], d[0], d[1]};
 }
 
-template <typename T, int NQ, bool KV8 = false, bool NTL = true>
+template <typename T, int NQ, bool KV8 = false, bool NTL = true, int NBC = 0>
 __global__ __launch_bounds__(256) void dec_xattn_kernel(
     const float* __restrict__ P, int KS, int pcols, const float* __restrict__ bias,
     const void* __restrict__ kbase, const void* __restrict__ vbase,
@@ -573,7 +609,7 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
   // bidx*256 + wid*64 + u*8 + kg, u < 8) but are streamed in halves of 4 rows
   // per lane group (u = 4*half + uu), so fewer registers hold loads in flight
   constexpr int UH = 4;
-  const int nb = (n + 255) >> 8;
+  const int nb = NBC > 0 ? NBC : (n + 255) >> 8;
   const int jmax = n - 1;
   f16x8 ka[UH], kb2[UH];
   uint2 qa[KV8 ? UH : 1], qb[KV8 ? UH : 1];  // fp8 rows in flight
@@ -648,25 +684,43 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
       __builtin_amdgcn_sched_barrier(0);  // one key row's conversions live at a time
     }
   };
-  for (int b = 0; b < nb; ++b) {
+  // NBC > 0 (n = 1500: 6 batches, a compile-time count): the last K trip
+  // loads V batch 0 instead of a clamped K batch past the end (whose loads the
+  // K -> V hand-over would otherwise drain), and the last V trip loads nothing
+  auto k_trip = [&](int b, bool last) {
     if constexpr (KV8) {
       LOADROWS8(qb, sb, K8, KS8, b, 1)
       WIDEN8(ka, qa, sa, 0)
       score_batch(ka, b, 0);
-      LOADROWS8(qa, sa, K8, KS8, b + 1, 0)
+      if (NBC > 0 && last) {
+        LOADROWS8(qa, sa, V8, VS8, 0, 0)
+      } else {
+        LOADROWS8(qa, sa, K8, KS8, b + 1, 0)
+      }
       WIDEN8(kb2, qb, sb, 1)
       score_batch(kb2, b, 1);
     } else {
       LOADROWS16(kb2, K, b, 1)
       score_batch(ka, b, 0);
-      LOADROWS16(ka, K, b + 1, 0)
+      if (NBC > 0 && last) {
+        LOADROWS16(ka, V, 0, 0)
+      } else {
+        LOADROWS16(ka, K, b + 1, 0)
+      }
       score_batch(kb2, b, 1);
     }
-  }
-  if constexpr (KV8) {
-    LOADROWS8(qa, sa, V8, VS8, 0, 0)
+  };
+  if constexpr (NBC > 0) {
+#pragma unroll 1
+    for (int b = 0; b < NBC - 1; ++b) k_trip(b, false);
+    k_trip(NBC - 1, true);
   } else {
-    LOADROWS16(ka, V, 0, 0)
+    for (int b = 0; b < nb; ++b) k_trip(b, false);
+    if constexpr (KV8) {
+      LOADROWS8(qa, sa, V8, VS8, 0, 0)
+    } else {
+      LOADROWS16(ka, V, 0, 0)
+    }
   }
   __syncthreads();
   // softmax per query (block_max_256 / block_sum_256d order)
@@ -731,20 +785,31 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
       __builtin_amdgcn_sched_barrier(0);
     }
   };
-  for (int b = 0; b < nb; ++b) {
+  auto v_trip = [&](int b, bool last) {
     if constexpr (KV8) {
       LOADROWS8(qb, sb, V8, VS8, b, 1)
       WIDEN8(ka, qa, sa, 0)
       pv_batch(ka, b, 0);
-      LOADROWS8(qa, sa, V8, VS8, b + 1, 0)
+      if (!(NBC > 0 && last)) {
+        LOADROWS8(qa, sa, V8, VS8, b + 1, 0)
+      }
       WIDEN8(kb2, qb, sb, 1)
       pv_batch(kb2, b, 1);
     } else {
       LOADROWS16(kb2, V, b, 1)
       pv_batch(ka, b, 0);
-      LOADROWS16(ka, V, b + 1, 0)
+      if (!(NBC > 0 && last)) {
+        LOADROWS16(ka, V, b + 1, 0)
+      }
       pv_batch(kb2, b, 1);
     }
+  };
+  if constexpr (NBC > 0) {
+#pragma unroll 1
+    for (int b = 0; b < NBC - 1; ++b) v_trip(b, false);
+    v_trip(NBC - 1, true);
+  } else {
+    for (int b = 0; b < nb; ++b) v_trip(b, false);
   }
 #undef LOADROWS16
 #undef LOADROWS8
@@ -785,28 +850,36 @@ bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float*
   if (!kv8 && nq == 1) return false;  // (f16 single rows: dec_attention)
   // MWX_XATTN_NT=0: default-policy K/V loads (A/B of the non-temporal stream)
   static const bool nt = !(getenv("MWX_XATTN_NT") && atoi(getenv("MWX_XATTN_NT")) == 0);
+  // 1500 keys (every Whisper model): the constant-batch-count load stream
+  // (MWX_XATTN_NBC=0: the runtime count, for A/B)
+  static const bool nbc = !(getenv("MWX_XATTN_NBC") && atoi(getenv("MWX_XATTN_NBC")) == 0);
+  const bool c6 = nbc && !kv8 && n_keys > 1280 && n_keys <= 1536;
+#define XL(N, K8, NT)                                                                          \
+  do {                                                                                         \
+    if (c6)                                                                                    \
+      dec_xattn_kernel<T, N, K8, NT, 6><<<g, 256, 0, st>>>(P, KS, pcols, bias, kbase, vbase,   \
+                                                           kscale8, vscale8, kv_index, active, \
+                                                           n_keys, cap, R, o, H, scale);       \
+    else                                                                                       \
+      dec_xattn_kernel<T, N, K8, NT><<<g, 256, 0, st>>>(P, KS, pcols, bias, kbase, vbase,      \
+                                                        kscale8, vscale8, kv_index, active,    \
+                                                        n_keys, cap, R, o, H, scale);          \
+  } while (0)
   switch (nq) {
-#define XQ(N)                                                                                   \
-  case N:                                                                                       \
-    if (kv8 && nt)                                                                              \
-      dec_xattn_kernel<T, N, true, true><<<g, 256, 0, st>>>(P, KS, pcols, bias, kbase, vbase,  \
-                                                      kscale8, vscale8, kv_index, active,       \
-                                                      n_keys, cap, R, o, H, scale);             \
-    else if (kv8)                                                                               \
-      dec_xattn_kernel<T, N, true, false><<<g, 256, 0, st>>>(P, KS, pcols, bias, kbase, vbase, \
-                                                      kscale8, vscale8, kv_index, active,       \
-                                                      n_keys, cap, R, o, H, scale);             \
-    else if (nt)                                                                                \
-      dec_xattn_kernel<T, N, false, true><<<g, 256, 0, st>>>(P, KS, pcols, bias, kbase, vbase, \
-                                                       nullptr, nullptr, kv_index, active,      \
-                                                       n_keys, cap, R, o, H, scale);            \
-    else                                                                                        \
-      dec_xattn_kernel<T, N, false, false><<<g, 256, 0, st>>>(P, KS, pcols, bias, kbase, vbase, \
-                                                       nullptr, nullptr, kv_index, active,      \
-                                                       n_keys, cap, R, o, H, scale);            \
+#define XQ(N)                                  \
+  case N:                                      \
+    if (kv8 && nt)                             \
+      XL(N, true, true);                       \
+    else if (kv8)                              \
+      XL(N, true, false);                      \
+    else if (nt)                               \
+      XL(N, false, true);                      \
+    else                                       \
+      XL(N, false, false);                     \
     return true;
     XQ(1) XQ(2) XQ(3) XQ(4) XQ(5) XQ(6) XQ(8)
 #undef XQ
+#undef XL
     default: return false;
   }
 }
@@ -840,6 +913,9 @@ void dec_attention(const float* P, int KS, int pcols, const float* bias, float q
   static const bool self_ub4 = !(getenv("MWX_SELF_UB") && atoi(getenv("MWX_SELF_UB")) == 8);
   // cross K/V streamed with non-temporal loads (MWX_XATTN_NT=0: default policy)
   static const bool xattn_nt = !(getenv("MWX_XATTN_NT") && atoi(getenv("MWX_XATTN_NT")) == 0);
+  // MWX_XATTN_NBC=0: the runtime-batch-count cross kernel (A/B of the
+  // constant-count load stream)
+  static const bool xattn_nbc = !(getenv("MWX_XATTN_NBC") && atoi(getenv("MWX_XATTN_NBC")) == 0);
   if (fixed_len == 0 && self_ub4)
     dec_attn_kernel<T, true, 4><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale, kbase,
                                                    vbase, kv_index, pos, active, fixed_len,
@@ -849,6 +925,11 @@ void dec_attention(const float* P, int KS, int pcols, const float* bias, float q
     dec_attn_kernel<T, true><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale, kbase, vbase,
                                                 kv_index, pos, active, fixed_len, kv_len_cap, o,
                                                 H, scale, kvmap, own_from, map_row0, nq, R);
+  else if (xattn_nt && fixed_len == 1500 && xattn_nbc)  // (every Whisper model: 1500 frames)
+    dec_attn_kernel<T, false, 8, true, 6><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale,
+                                                             kbase, vbase, kv_index, pos, active,
+                                                             fixed_len, kv_len_cap, o, H, scale,
+                                                             nullptr, nullptr, 0, nq, R);
   else if (xattn_nt)
     dec_attn_kernel<T, false, 8, true><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale,
                                                           kbase, vbase, kv_index, pos, active,

@@ -372,10 +372,13 @@ class Context:
         """Copies PCM into a buffer on this context's GPU (HBM-resident input)."""
         return DevicePCM(self, pcm)
 
-    def full_batch_device(self, bufs: Sequence["DevicePCM"], params: FullParams) -> int:
-        """Batch over PCM already resident in this GPU's memory: no PCIe transfer."""
+    def full_batch_device(self, bufs: Sequence["DevicePCM"], params: FullParams,
+                          state0: int = 0) -> int:
+        """Batch over PCM already resident in this GPU's memory: no PCIe transfer.
+        Clip i runs on state state0 + i (state0 owns the batch's workspace and
+        stream, so batches on disjoint state ranges may run concurrently)."""
         n = len(bufs)
-        states = (C.c_void_p * n)(*[self.state(i) for i in range(n)])
+        states = (C.c_void_p * n)(*[self.state(state0 + i) for i in range(n)])
         ptrs = (C.POINTER(C.c_float) * n)(*[b.ptr for b in bufs])
         ln = (C.c_int * n)(*[b.n for b in bufs])
         return lib().mwx_full_batch(self.ctx, states, params, ptrs, ln, n)
