@@ -9,6 +9,13 @@ Whisper-large-v3 shapes, bf16 weights (synthetic, seeded), 32 clips x 30 s per
 GPU, decode length fixed at the upstream cap of 220 steps per clip (EOT and
 timestamps suppressed via bench_fixed_steps so every clip costs the same).
 
+Lanes (default 2 = the reference's parallel_requests default, src/config.h:41):
+two batches are in flight per GPU, each driven by its own host thread on its
+own states and HIP stream, as the SttEngine's batchers run them; batch k of the
+K timed batches runs on lane k % 2. Every batch is still 32 clips; one lane's
+encoder / host work overlaps the other's decode. --lanes 1 times one batch at
+a time (the PCIe-inclusive --host-input legs always do).
+
 Multi-GPU: launched with torch.distributed.run, one process per GPU; clips are
 sharded (weak scaling, 32 per GPU); RCCL is used only for the final token-stream
 gather. value = audio seconds processed by all ranks / max-over-ranks time.
@@ -510,9 +517,11 @@ def main():
     ap.add_argument("--clip-seconds", type=float, default=30.0,
                     help="clip length (> 30: long-form, windows decoded one after another)")
     ap.add_argument("--perf-class", default="dec_attn_cross")
-    ap.add_argument("--lanes", type=int, default=1,
+    ap.add_argument("--lanes", type=int, default=2,
                     help="concurrent batches (host threads, each with its own states and HIP "
                          "stream), as the SttEngine's parallel_requests batchers run them")
+    ap.add_argument("--lane-stagger", type=float, default=0.0,
+                    help="seconds lane i waits (x i) before its first timed batch")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fp8", action="store_true",
                     help="MX-fp8 compute (C5): encoder, cross-K/V and decoder weight GEMMs, cross K/V cache")
@@ -577,8 +586,8 @@ def main():
     # inputs resident in HBM before the timed region (the PCIe-inclusive rate,
     # host buffers uploaded inside the step, is --host-input)
     lanes = max(1, args.lanes)
-    if lanes > 1 and args.host_input:
-        raise SystemExit("bench.py: --lanes > 1 needs HBM-resident input (no --host-input)")
+    if args.host_input:
+        lanes = 1  # (the PCIe-inclusive legs time one batch at a time)
     for i in range(lanes * args.clips):  # all states exist before any lane thread runs
         ctx.state(i)
     if args.host_input and args.pcm16:
@@ -621,6 +630,8 @@ def main():
 
         def lane_loop(lane):
             try:
+                if args.lane_stagger > 0:  # (inside the timed region)
+                    time.sleep(lane * args.lane_stagger)
                 for _ in range(len(range(lane, n, lanes))):
                     out[lane].append(step(lane))
             except Exception as ex:  # re-raised in the main thread
@@ -655,26 +666,44 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     import ctypes
-    timed = {}
-    for cls in classes:
-        tot, cnt = 0.0, 0
-        for so in owners:  # summed over the lanes' states
-            tms, nlc = ctypes.c_double(), ctypes.c_int()
-            L.mwx_perf_read_class(so, cls.encode(), ctypes.byref(tms), ctypes.byref(nlc))
-            tot, cnt = tot + tms.value, cnt + nlc.value
-        timed[cls] = (tot, cnt)
-    for so in owners:
-        L.mwx_perf_enable(so, None)
-    tot_ms, nl = ctypes.c_double(timed[args.perf_class][0]), ctypes.c_int(timed[args.perf_class][1])
+
+    def read_timed(states):
+        out = {}
+        for cls in classes:
+            tot, cnt = 0.0, 0
+            for so in states:  # summed over the lanes' states
+                tms, nlc = ctypes.c_double(), ctypes.c_int()
+                L.mwx_perf_read_class(so, cls.encode(), ctypes.byref(tms), ctypes.byref(nlc))
+                tot, cnt = tot + tms.value, cnt + nlc.value
+            out[cls] = (tot, cnt)
+        for so in states:
+            L.mwx_perf_enable(so, None)
+        return out
+
+    timed = read_timed(owners)
+    timed_1lane, steps_1lane = None, 0
+    if lanes > 1:
+        # after the timed region (not part of `value`): the same batches on one
+        # lane, so the kernels' rooflines are also reported without another
+        # lane's kernels sharing HBM and CUs with them
+        steps_1lane = min(2, args.steps)
+        L.mwx_perf_read(owners[0], None, None)
+        L.mwx_perf_enable(owners[0], ",".join(classes).encode())
+        for _ in range(steps_1lane):
+            gather(step(0))
+        torch.cuda.synchronize()
+        timed_1lane = read_timed(owners[:1])
     if dist is not None:
         e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     audio_s = world * args.clips * args.clip_seconds * args.steps
     value = audio_s / elapsed
-    if rank == 0:
-        launches = max(1, nl.value)
-        avg_s = tot_ms.value / 1e3 / launches
+
+    def make_roofs(tm, nsteps):
+        """(dominant-kernel roofline, encoder-GEMM roofline) from live timings"""
+        launches = max(1, tm[args.perf_class][1])
+        avg_s = tm[args.perf_class][0] / 1e3 / launches
         # decode kernels run per row group (MWX_DECODE_GROUPS chains on their
         # own streams, default 1); the engine times every 8th decode step's
         # launches (MWX_PERF_PERIOD), all inside the timed region
@@ -683,7 +712,7 @@ def main():
             rows = rows / max(1, int(os.environ.get("MWX_DECODE_GROUPS", "1")))
         clips_per_launch = args.clips * (rows / (args.clips * max(1, args.beam)))
         bound, work, desc = kernel_model(args.arch, args.perf_class, clips_per_launch, rows,
-                                         launches // max(1, args.steps), prompt_len,
+                                         launches // max(1, nsteps), prompt_len,
                                          args.decode_steps, n_windows, kv8=args.fp8)
         traffic = None
         tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -704,12 +733,13 @@ def main():
                     "unit": "TFLOP/s", "frac": round(achieved / MFMA_PEAK_TFLOPS, 4),
                     "traffic": traffic}
         roof.update({"kernel": args.perf_class, "avg_launch_us": round(avg_s * 1e6, 2),
-                     "launches": nl.value, "work_per_launch": work, "work_desc": desc})
+                     "launches": tm[args.perf_class][1], "work_per_launch": work,
+                     "work_desc": desc})
         roof_enc = None
-        if "enc_gemm" in timed and args.perf_class != "enc_gemm" and timed["enc_gemm"][1] > 0:
-            ems, en = timed["enc_gemm"]
+        if "enc_gemm" in tm and args.perf_class != "enc_gemm" and tm["enc_gemm"][1] > 0:
+            ems, en = tm["enc_gemm"]
             _, ework, edesc = kernel_model(args.arch, "enc_gemm", args.clips, rows,
-                                           en // max(1, args.steps), prompt_len, args.decode_steps,
+                                           en // max(1, nsteps), prompt_len, args.decode_steps,
                                            n_windows)
             eavg = ems / 1e3 / en
             epeak = 2 * MFMA_PEAK_TFLOPS if args.fp8 else MFMA_PEAK_TFLOPS
@@ -718,6 +748,15 @@ def main():
                         "unit": "TFLOP/s", "frac": round(each / epeak, 4), "kernel": "enc_gemm",
                         "avg_launch_us": round(eavg * 1e6, 2), "launches": en,
                         "work_per_launch": ework, "work_desc": edesc}
+        return roof, roof_enc
+
+    if rank == 0:
+        roof, roof_enc = make_roofs(timed, args.steps)
+        roof_1lane = None
+        if timed_1lane is not None:
+            r1, e1 = make_roofs(timed_1lane, steps_1lane)
+            roof_1lane = {"note": f"{steps_1lane} batches on one lane after the timed region",
+                          "roofline": r1, "roofline_encoder": e1}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             # all cores granted to this job (OMP_NUM_THREADS on the GPU box)
@@ -760,6 +799,7 @@ def main():
             "gathered": gather_summary(gathered.get("tokens"), world * args.clips, max_tok),
             "roofline": roof,
             "roofline_encoder": roof_enc,
+            "one_lane": roof_1lane,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -134,6 +134,11 @@ struct State {
   // ev_in orders the groups after the step inputs, ev_done joins them
   hipStream_t gstream[MWX_MAX_GROUPS] = {};
   hipEvent_t ev_in = nullptr, ev_done[MWX_MAX_GROUPS] = {};
+  // encoder stream (MWX_STREAM_PRIO=enc_low / both): the encoder of a batch runs
+  // on a low-priority stream, ordered after / before `stream` by two events,
+  // so a concurrent batch's latency-bound decode chain is dispatched first
+  hipStream_t estream = nullptr;
+  hipEvent_t ev_e0 = nullptr, ev_e1 = nullptr;
   // encoder workspace (clip-batched)
   DBuf pcm, mel, melmax, melT, h1p, x, h, q, k, vt, o, ff, enc, cross_k, cross_v;
   DBuf cross_ks, cross_vs;  // MX-fp8 cross cache: E8M0 scales (kv8)
@@ -734,7 +739,7 @@ struct Driver {
     T* o = (T*)S.o.get((size_t)M * d * sizeof(T));
     T* ff = (T*)S.ff.get((size_t)M * 4 * d * sizeof(T));
     T* enc = (T*)S.enc.get((size_t)M * d * sizeof(T));
-    { PerfScope ps(S, "mel");
+    { PerfScope ps(S, "mel", st);
     launch_mel_window((const float*)S.mel.p, mel_clip_stride, ib, ib + 4096, ib + 2 * 4096,
                       hp.n_mels, T2, cp, melT, nb, st); }
     EpiParams e;
@@ -743,7 +748,7 @@ struct Driver {
     e.c16 = h1p + d;
     e.ldc = d;
     e.c_bstride = (long)(T2 + 2) * d;
-    { PerfScope ps(S, "enc_gemm");
+    { PerfScope ps(S, "enc_gemm", st);
     gemm<_Float16>(EPI_GELU, true, melT, cp, (long)(T2 + 2) * cp, C.conv1_w, 3 * cp, T2, d,
                    3 * cp, nb, e, st); }
     // conv2 (k3 s2 p1) + GELU + positional embedding -> residual stream x
@@ -753,7 +758,7 @@ struct Driver {
     e.ldc = d;
     e.c_bstride = (long)Lc * d;
     e.pe = C.enc_pe;
-    { PerfScope ps(S, "enc_gemm");
+    { PerfScope ps(S, "enc_gemm", st);
     gemm<_Float16>(EPI_CONV2, false, h1p, 2 * d, (long)(T2 + 2) * d, C.conv2_w, 3 * d, Lc, d,
                    3 * d, nb, e, st); }
     const float kq_scale = 1.0f / sqrtf(64.0f);
@@ -784,30 +789,30 @@ struct Driver {
       e.H = H;
       e.d = d;
       e.ldv = Lp;  // V^T rows are padded to Lp (16-B aligned tile loads)
-      { PerfScope ps(S, "enc_gemm");
+      { PerfScope ps(S, "enc_gemm", st);
       mgemm(EPI_ENC_QKV, h, d, W.qkv_x, W.qkv_w, 3 * d, e); }
-      { PerfScope ps(S, "enc_attn");
+      { PerfScope ps(S, "enc_attn", st);
       enc_attention<T>(q, k, vt, o, nb, H, Lc, kq_scale, st); }
       e = EpiParams();
       e.bias = W.o_b;
       e.c32 = x;
       e.r32 = x;
       e.ldc = d;
-      { PerfScope ps(S, "enc_gemm");
+      { PerfScope ps(S, "enc_gemm", st);
       mgemm(EPI_RES, o, d, W.o_x, W.o_w, d, e); }
       layer_norm<T>(x, W.ln2_w, W.ln2_b, h, M, d, nullptr, st);
       e = EpiParams();
       e.bias = W.fc1_b;
       e.c16 = ff;
       e.ldc = 4 * d;
-      { PerfScope ps(S, "enc_gemm");
+      { PerfScope ps(S, "enc_gemm", st);
       mgemm(EPI_GELU, h, d, W.fc1_x, W.fc1_w, 4 * d, e); }
       e = EpiParams();
       e.bias = W.fc2_b;
       e.c32 = x;
       e.r32 = x;
       e.ldc = d;
-      { PerfScope ps(S, "enc_gemm");
+      { PerfScope ps(S, "enc_gemm", st);
       mgemm(EPI_RES, ff, 4 * d, W.fc2_x, W.fc2_w, d, e); }
     }
     layer_norm<T>(x, C.enc_ln_w, C.enc_ln_b, enc, M, d, nullptr, st);
@@ -826,7 +831,7 @@ struct Driver {
     e.ncap = S.cross_cap;
     e.slot = ib + 3 * 4096;
     e.kscale = powf(64.0f, -0.25f);
-    PerfScope ps(S, "cross_gemm");
+    PerfScope ps(S, "cross_gemm", st);
     mgemm(EPI_CROSS_KV, enc, d, C.cross_x, C.cross_w, L_dec * 2 * d, e);
   }
 

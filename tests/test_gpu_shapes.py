@@ -215,3 +215,57 @@ def test_v3_geometry_mxfp8_greedy_tracks_mx_oracle(v3):
     _, osegs, _, _ = omx.full(pcms[0], greedy_opt())
     oids = [t.id for s in osegs for t in s.tokens]
     assert batched[0][:8] == oids[:8]
+
+
+def test_v3_geometry_concurrent_lanes_equal_sequential(v3):
+    """Two batches at once (bench.py --lanes 2, the SttEngine's
+    parallel_requests batchers): one greedy and one beam-5 batch on disjoint
+    states, driven from two host threads on their own HIP streams, give
+    exactly the results each gives alone."""
+    import threading
+    ctx, _, _ = v3
+    pg = service_params(ctx, temperature_inc=0.0, language=b"en")
+    pb = ctx.default_params(mwx.SAMPLING_BEAM_SEARCH)
+    pb.beam_search.beam_size = 5
+    pb.language = b"en"
+    pb.temperature_inc = 0.0
+    lanes = [([pcm_clip(k, 30.0 - 1.5 * k) for k in range(4)], pg),
+             ([pcm_clip(k + 8, 24.0 + 2.0 * k) for k in range(3)], pb)]
+
+    def toks(base, n):
+        return [[(t.id, t.p, t.t0, t.t1) for s in ctx.segments(base + i) for t in s.tokens]
+                for i in range(n)]
+
+    alone = []
+    for pcms, p in lanes:
+        base = fresh(ctx)
+        assert ctx.full_batch_states(pcms, p, range(base, base + len(pcms))) == 0
+        alone.append(toks(base, len(pcms)))
+    bases = []
+    for pcms, _ in lanes:
+        bases.append(fresh(ctx))
+        for i in range(len(pcms)):
+            ctx.state(bases[-1] + i)
+    rcs = [None, None]
+
+    def run(j):
+        pcms, p = lanes[j]
+        arrs = [np.ascontiguousarray(x, dtype=np.float32) for x in pcms]
+        n = len(arrs)
+        L = mwx.lib()
+        states = (mwx.C.c_void_p * n)(*[ctx.state(bases[j] + i) for i in range(n)])
+        ptrs = (mwx.C.POINTER(mwx.C.c_float) * n)(*[mwx.fptr(a) for a in arrs])
+        lens = (mwx.C.c_int * n)(*[len(a) for a in arrs])
+        for _ in range(2):
+            rcs[j] = L.mwx_full_batch(ctx.ctx, states, p, ptrs, lens, n)
+            if rcs[j] != 0:
+                return
+
+    th = [threading.Thread(target=run, args=(j,)) for j in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert rcs == [0, 0]
+    for j, (pcms, _) in enumerate(lanes):
+        assert toks(bases[j], len(pcms)) == alone[j], j
