@@ -606,8 +606,7 @@ def main():
         if rc != 0:
             raise RuntimeError(f"mwx_full_batch rc={rc}")
         s0 = lane * args.clips
-        return shard.pack_records([[(t.id, t.t0, t.t1, t.p) for s in ctx.segments(s0 + c)
-                                    for t in s.tokens] for c in range(args.clips)], max_tok)
+        return shard.pack_records([ctx.token_records(s0 + c) for c in range(args.clips)], max_tok)
 
     def gather(block):
         # RCCL over xGMI: every rank's token records (id, t0, t1, p) to rank 0

@@ -18,6 +18,7 @@
 #include <cmath>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <random>
 #include <string>
 #include <vector>
@@ -39,12 +40,25 @@ namespace mwx {
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// Process-wide order between graph capture and (de)allocation: while any
+// thread captures a stream, HIP rejects legacy-stream operations such as
+// hipMemset ("would make the legacy stream depend on a capturing stream") and
+// hipFree / hipHostFree synchronize the device. Concurrent batches (the
+// SttEngine's parallel_requests batchers) capture their decode graphs while
+// another batch may be growing its buffers, so both hold this lock
+// (recursive: a capture may grow a buffer of its own).
+inline std::recursive_mutex& capture_mutex() {
+  static std::recursive_mutex m;
+  return m;
+}
+
 // grow-only device buffer
 struct DBuf {
   void* p = nullptr;
   size_t n = 0;
   void* get(size_t bytes, bool zero = false) {
     if (bytes > n) {
+      std::lock_guard<std::recursive_mutex> lock(capture_mutex());
       if (p) (void)hipFree(p);
       p = nullptr;
       n = 0;
@@ -55,6 +69,7 @@ struct DBuf {
     return p;
   }
   void release() {
+    std::lock_guard<std::recursive_mutex> lock(capture_mutex());
     if (p) (void)hipFree(p);
     p = nullptr;
     n = 0;
@@ -161,6 +176,7 @@ struct State {
   size_t pin_n = 0;
   void* pinned(size_t bytes) {
     if (bytes > pin_n) {
+      std::lock_guard<std::recursive_mutex> lock(capture_mutex());
       if (pin) (void)hipHostFree(pin);
       pin = nullptr;
       pin_n = 0;
@@ -179,6 +195,7 @@ struct State {
   hipEvent_t ev_step[RUN_SLOTS] = {};
   RunReport* report_ring(size_t bytes) {
     if (bytes > rep_n) {
+      std::lock_guard<std::recursive_mutex> lock(capture_mutex());
       if (rep_pin) (void)hipHostFree(rep_pin);
       rep_pin = nullptr;
       rep_n = 0;

@@ -403,6 +403,18 @@ class Context:
             out.append(seg)
         return out
 
+    def token_records(self, state_index: int = 0) -> List[tuple]:
+        """(id, t0, t1, p) of every token of every segment, in order: the
+        per-token whisper.h accessors only (no text), for the gather."""
+        L = lib()
+        s = self.state(state_index)
+        out = []
+        for i in range(L.mwx_full_n_segments_from_state(s)):
+            for j in range(L.mwx_full_n_tokens_from_state(s, i)):
+                td = L.mwx_full_get_token_data_from_state(s, i, j)
+                out.append((td.id, td.t0, td.t1, td.p))
+        return out
+
     def lang_id(self, state_index: int = 0) -> int:
         return lib().mwx_full_lang_id_from_state(self.state(state_index))
 

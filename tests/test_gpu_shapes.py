@@ -269,3 +269,8 @@ def test_v3_geometry_concurrent_lanes_equal_sequential(v3):
     assert rcs == [0, 0]
     for j, (pcms, _) in enumerate(lanes):
         assert toks(bases[j], len(pcms)) == alone[j], j
+    # the gather's text-free record accessor (bench.py) reads the same tokens
+    for j, (pcms, _) in enumerate(lanes):
+        for i in range(len(pcms)):
+            assert ctx.token_records(bases[j] + i) == [
+                (t.id, t.t0, t.t1, t.p) for s in ctx.segments(bases[j] + i) for t in s.tokens]
