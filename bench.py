@@ -506,7 +506,8 @@ def main():
                          "them itself")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher + record gather only, synthetic records (no GPU needed)")
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=6,
+                    help="timed batches (a multiple of --lanes keeps the lanes evenly loaded)")
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--arch", default="large-v3")
     ap.add_argument("--wtype", default="bf16", choices=["bf16", "f16"])
@@ -605,6 +606,7 @@ def main():
         rc = run_batch(lane)
         if rc != 0:
             raise RuntimeError(f"mwx_full_batch rc={rc}")
+        print(f"bench.py: lane {lane}: batch done", file=sys.stderr, flush=True)  # (progress)
         s0 = lane * args.clips
         return shard.pack_records([ctx.token_records(s0 + c) for c in range(args.clips)], max_tok)
 
@@ -685,7 +687,7 @@ def main():
         # after the timed region (not part of `value`): the same batches on one
         # lane, so the kernels' rooflines are also reported without another
         # lane's kernels sharing HBM and CUs with them
-        steps_1lane = min(2, args.steps)
+        steps_1lane = min(2 if args.clip_seconds <= 30 else 1, args.steps)
         L.mwx_perf_read(owners[0], None, None)
         L.mwx_perf_enable(owners[0], ",".join(classes).encode())
         for _ in range(steps_1lane):
