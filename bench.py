@@ -11,8 +11,8 @@ timestamps suppressed via bench_fixed_steps so every clip costs the same).
 
 Lanes (default 2 = the reference's parallel_requests default, src/config.h:41):
 two batches are in flight per GPU, each driven by its own host thread on its
-own states and HIP stream, as the SttEngine's batchers run them; batch k of the
-K timed batches runs on lane k % 2. Every batch is still 32 clips; one lane's
+own states and HIP stream, as the SttEngine's batchers run them; a lane takes
+the next of the K timed batches when its previous one is done. Every batch is still 32 clips; one lane's
 encoder / host work overlaps the other's decode. --lanes 1 times one batch at
 a time (the PCIe-inclusive --host-input legs always do).
 
@@ -521,6 +521,8 @@ def main():
     ap.add_argument("--lanes", type=int, default=2,
                     help="concurrent batches (host threads, each with its own states and HIP "
                          "stream), as the SttEngine's parallel_requests batchers run them")
+    ap.add_argument("--lane-prio", default="",
+                    help="per-lane stream priority of the lanes' states, e.g. 'high,normal'")
     ap.add_argument("--lane-stagger", type=float, default=0.0,
                     help="seconds lane i waits (x i) before its first timed batch")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -589,8 +591,12 @@ def main():
     lanes = max(1, args.lanes)
     if args.host_input:
         lanes = 1  # (the PCIe-inclusive legs time one batch at a time)
+    prios = args.lane_prio.split(",") if args.lane_prio else []
     for i in range(lanes * args.clips):  # all states exist before any lane thread runs
+        if i % args.clips == 0 and prios:  # (read by mwx_init_state: the stream's priority)
+            os.environ["MWX_STATE_PRIO"] = prios[min(i // args.clips, len(prios) - 1)]
         ctx.state(i)
+    os.environ.pop("MWX_STATE_PRIO", None)
     if args.host_input and args.pcm16:
         p16s = [mwx.synth_pcm16(k, n_samp) for k in shard.clip_ids(rank, args.clips)]
         run_batch = lambda lane: ctx.full_batch_pcm16(p16s, p)  # noqa: E731
@@ -617,24 +623,32 @@ def main():
             gathered["tokens"] = g
 
     def run_steps(n):
-        """n batches spread round-robin over the lanes; each lane is a host
-        thread driving its own states and HIP stream (the SttEngine's
-        parallel_requests batchers), so one lane's encoder / host work overlaps
-        another lane's decode. Gathers run afterwards in batch order."""
+        """n batches over the lanes; each lane is a host thread driving its own
+        states and HIP stream (the SttEngine's parallel_requests batchers) and
+        takes the next batch when its previous one is done, so one lane's
+        encoder / host work overlaps another lane's decode. Gathers run
+        afterwards in batch order."""
         if lanes == 1:
             for _ in range(n):
                 gather(step(0))
             return
         import threading
-        out = [[] for _ in range(lanes)]
+        out = {}
         errs = []
+        nxt = [0]
+        lock = threading.Lock()
 
         def lane_loop(lane):
             try:
                 if args.lane_stagger > 0:  # (inside the timed region)
                     time.sleep(lane * args.lane_stagger)
-                for _ in range(len(range(lane, n, lanes))):
-                    out[lane].append(step(lane))
+                while True:
+                    with lock:
+                        i = nxt[0]
+                        nxt[0] += 1
+                    if i >= n or errs:
+                        return
+                    out[i] = step(lane)
             except Exception as ex:  # re-raised in the main thread
                 errs.append(ex)
 
@@ -646,7 +660,7 @@ def main():
         if errs:
             raise errs[0]
         for i in range(n):
-            gather(out[i % lanes][i // lanes])
+            gather(out[i])
 
     for lane in range(lanes):
         for _ in range(args.warmup):

@@ -17,7 +17,12 @@ timeout -s KILL 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_B
 cd "$GRAFT_REPO_ROOT"
 python scripts/pmc_report.py $O $TAG --md $O/pmc_${TAG}.md > $O/pmc_${TAG}_report.txt 2>&1 || echo "report failed"
 run() { # env extra
-  env $1 timeout -k 10 300 python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline $2 > $O/b_$TAG.json 2>> $O/bench_$TAG.err || { tail -20 $O/bench_$TAG.err; exit 3; }
+  env $1 timeout -k 10 300 python -u bench.py --steps 6 --warmup 1 --no-cpu-baseline $2 > $O/b_$TAG.json 2>> $O/bench_$TAG.err || { tail -20 $O/bench_$TAG.err; exit 3; }
   python -c "import json,sys; d=json.loads(open('$O/b_$TAG.json').readlines()[-1]); print('$1 $2', d['value'], d['ms_per_step'], d['roofline']['avg_launch_us'], d['gathered']['complete'])"
 }
-run MWX_XATTN_NBC=0 "--beam 5 --lanes 1" && run MWX_XATTN_NBC=1 "--beam 5 --lanes 1" && run MWX_XATTN_NBC=0 "--beam 5 --lanes 1" && run MWX_XATTN_NBC=1 "--beam 5 --lanes 1" && run MWX_XATTN_NBC=1 "--beam 5 --lanes 2"
+run MWX_STREAM_PRIO=enc_low "--lanes 2" && run MWX_STREAM_PRIO=enc_low "--lanes 2 --lane-prio high,normal" && \
+run MWX_STREAM_PRIO=enc_low "--lanes 2 --lane-prio high,low" && run MWX_STREAM_PRIO=both "--lanes 2" && \
+run GPU_MAX_HW_QUEUES=8 "--lanes 2" && run GPU_MAX_HW_QUEUES=8 "--lanes 3" && \
+run MWX_STREAM_PRIO=enc_low "--lanes 3 --lane-prio high,normal,low" && run MWX_STREAM_PRIO=enc_low "--lanes 2" && \
+run MWX_XATTN_NBC=0 "--beam 5 --lanes 1 --steps 2" && run MWX_XATTN_NBC=1 "--beam 5 --lanes 1 --steps 2" && \
+run MWX_XATTN_NBC=0 "--beam 5 --lanes 1 --steps 2" && run MWX_XATTN_NBC=1 "--beam 5 --lanes 1 --steps 2"

@@ -12,4 +12,7 @@ timeout -k 10 600 python -u bench.py --fp8 --beam 5 --clip-seconds 600 --steps 2
 tail -1 $O/bench_${TAG}_c5.json | cut -c1-160
 cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_$TAG -o greedy -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/prof_$TAG.log 2>&1 || { echo "prof failed"; exit 4; }
+cd "$GRAFT_REPO_ROOT"
+# (the trace database exceeds what gpurun copies back: summarise it here)
+python scripts/prof_summary.py $O/prof_$TAG/greedy_results.db $O/prof_${TAG}_kernel_stats.md > /dev/null && rm -rf $O/prof_$TAG
 echo done
