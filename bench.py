@@ -521,8 +521,6 @@ def main():
     ap.add_argument("--lanes", type=int, default=2,
                     help="concurrent batches (host threads, each with its own states and HIP "
                          "stream), as the SttEngine's parallel_requests batchers run them")
-    ap.add_argument("--lane-prio", default="",
-                    help="per-lane stream priority of the lanes' states, e.g. 'high,normal'")
     ap.add_argument("--lane-stagger", type=float, default=0.0,
                     help="seconds lane i waits (x i) before its first timed batch")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -591,12 +589,8 @@ def main():
     lanes = max(1, args.lanes)
     if args.host_input:
         lanes = 1  # (the PCIe-inclusive legs time one batch at a time)
-    prios = args.lane_prio.split(",") if args.lane_prio else []
     for i in range(lanes * args.clips):  # all states exist before any lane thread runs
-        if i % args.clips == 0 and prios:  # (read by mwx_init_state: the stream's priority)
-            os.environ["MWX_STATE_PRIO"] = prios[min(i // args.clips, len(prios) - 1)]
         ctx.state(i)
-    os.environ.pop("MWX_STATE_PRIO", None)
     if args.host_input and args.pcm16:
         p16s = [mwx.synth_pcm16(k, n_samp) for k in shard.clip_ids(rank, args.clips)]
         run_batch = lambda lane: ctx.full_batch_pcm16(p16s, p)  # noqa: E731

@@ -850,9 +850,10 @@ bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float*
   if (!kv8 && nq == 1) return false;  // (f16 single rows: dec_attention)
   // MWX_XATTN_NT=0: default-policy K/V loads (A/B of the non-temporal stream)
   static const bool nt = !(getenv("MWX_XATTN_NT") && atoi(getenv("MWX_XATTN_NT")) == 0);
-  // 1500 keys (every Whisper model): the constant-batch-count load stream
-  // (MWX_XATTN_NBC=0: the runtime count, for A/B)
-  static const bool nbc = !(getenv("MWX_XATTN_NBC") && atoi(getenv("MWX_XATTN_NBC")) == 0);
+  // 1500 keys: the constant-batch-count load stream, opt-in (MWX_XATTN_NBC=1):
+  // beam 5, same box, 770.6 / 775.7 against 778.9 / 778.8 audio-s/s for the
+  // runtime count, so the grouped kernel keeps the runtime count by default
+  static const bool nbc = getenv("MWX_XATTN_NBC") && atoi(getenv("MWX_XATTN_NBC")) == 1;
   const bool c6 = nbc && !kv8 && n_keys > 1280 && n_keys <= 1536;
 #define XL(N, K8, NT)                                                                          \
   do {                                                                                         \
