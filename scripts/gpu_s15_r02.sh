@@ -14,5 +14,5 @@ run() { # env extra
   env $1 timeout -k 10 300 python -u bench.py --steps 6 --warmup 1 --no-cpu-baseline $2 > $O/b_$TAG.json 2>> $O/bench_$TAG.err || { tail -20 $O/bench_$TAG.err; exit 3; }
   python -c "import json,sys; d=json.loads(open('$O/b_$TAG.json').readlines()[-1]); e=d['roofline_encoder'] if d.get('one_lane') is None else d['one_lane']['roofline_encoder']; print('$1 $2', d['value'], d['ms_per_step'], d['roofline_encoder']['avg_launch_us'], d['roofline_encoder']['frac'], e['frac'], d['gathered']['complete'])"
 }
-run MWX_GEMM_PP=0 "--lanes 1 --steps 3" && run MWX_GEMM_PP=1 "--lanes 1 --steps 3" && run MWX_GEMM_PP=0 "--lanes 1 --steps 3" && run MWX_GEMM_PP=1 "--lanes 1 --steps 3" && \
+run MWX_GEMM_PP=1 "--lanes 1 --steps 3" && run MWX_GEMM_PP=0 "--lanes 1 --steps 3" && run MWX_GEMM_PP=1 "--lanes 1 --steps 3" && run MWX_GEMM_PP=0 "--lanes 1 --steps 3" && \
 run MWX_GEMM_PP=0 "--lanes 2" && run MWX_GEMM_PP=1 "--lanes 2"

@@ -160,19 +160,7 @@ constexpr int GFM = BM / GWM / 16, GFN = BN / GWN / 16;  // 8 x 4 fragments per 
 // 64 + 16*(l>>4) + [0,16) in bytes 16-31 -- exactly the 16-B chunks (l>>4)
 // and 4+(l>>4) of the row -- and its scale operand is that row's scale of
 // k block l>>4.
-// PP = true (16-bit operands): ping-pong schedule of the two wave groups that
-// share each SIMD (waves 0-3: rows 0-127 of the tile, waves 4-7: rows
-// 128-255). The K loop runs in phases separated by one workgroup barrier;
-// in each phase one group reads its fragments of a K tile from LDS while the
-// other group runs the MFMAs of the tile it read in the previous phase, so
-// the fragment reads of one wave overlap the MFMAs of its SIMD partner
-// instead of every wave stalling on its reads after each tile's barrier.
-// Group 0 reads tile t in phase 2t and multiplies it in phase 2t+1; group 1
-// one phase later. The DMA of tile t+1 is issued at phase 2t into the stage
-// tile t-1 held (read by both groups by then) and has landed by phase 2t+2.
-// Every output is the same MFMA chain over k as in the default schedule, so
-// results are bit-identical.
-template <typename T, int EPI, bool OUT16, bool MX = false, bool PP = false>
+template <typename T, int EPI, bool OUT16, bool MX = false>
 __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, long lda,
                                                    long a_bstride, const void* __restrict__ Wv,
                                                    long ldw, int M, int N, int K, EpiParams P) {
@@ -259,53 +247,6 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
 #pragma unroll
     for (int j = 0; j < GFN; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
   const int nk = K / BKE;
-  if constexpr (PP && !MX) {
-    static_assert(NSTG == 2 && CPR == 8, "ping-pong: 2-stage ring of 64-deep tiles");
-    constexpr int NSUB = CPR / 4;
-    const int grp = wid >> 2;  // == wm
-    V8 af[NSUB][GFM], bf[NSUB][GFN];
-    GLDS(0, 0);
-    for (int p = 0; p <= 2 * nk; ++p) {
-      // even phase 2t: tile t has landed (this wave's DMA; the barrier makes
-      // every wave's part visible)
-      if ((p & 1) == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      if ((p & 1) == 0 && p / 2 + 1 < nk) GLDS(p / 2 + 1, (p / 2 + 1) & 1);
-      const int q = p - grp;
-      if (q >= 0 && (q & 1) == 0 && (q >> 1) < nk) {
-        const int cur = (q >> 1) & 1;
-#pragma unroll
-        for (int s = 0; s < NSUB; ++s) {
-          const int kc = s * 4 + (lane >> 4);
-#pragma unroll
-          for (int i = 0; i < GFM; ++i) {
-            const int row = wm * (BM / GWM) + i * 16 + (lane & 15);
-            af[s][i] = *reinterpret_cast<const V8*>(&lds[cur][row * BKE + ((kc ^ swz(row)) << 3)]);
-          }
-#pragma unroll
-          for (int j = 0; j < GFN; ++j) {
-            const int row = BM + wn * (BN / GWN) + j * 16 + (lane & 15);
-            bf[s][j] = *reinterpret_cast<const V8*>(&lds[cur][row * BKE + ((kc ^ swz(row)) << 3)]);
-          }
-        }
-        // the fragments are in registers before the barrier that lets the
-        // stage be refilled
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      } else if (q >= 1 && (q & 1) == 1 && ((q - 1) >> 1) < nk) {
-        if (GEMM_PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int s = 0; s < NSUB; ++s)
-#pragma unroll
-          for (int i = 0; i < GFM; ++i)
-#pragma unroll
-            for (int j = 0; j < GFN; ++j) acc[i][j] = Elt<T>::mfma(af[s][i], bf[s][j], acc[i][j]);
-        if (GEMM_PRIO) __builtin_amdgcn_s_setprio(0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  } else {
 #pragma unroll
   for (int t = 0; t < NSTG - 1; ++t)
     if (t < nk) GLDS(t, t);
@@ -397,7 +338,6 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
     }
     // this wave's reads of `cur` have returned before its next barrier
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  }
   }
 #undef GLDS
   const int wr0 = m0 + wm * (BM / GWM), wc0 = n0 + wn * (BN / GWN);
@@ -861,12 +801,7 @@ static void gemm_dispatch(const T* A, long lda, long a_bstride, const T* W, long
   // (measured: -3..-5% on the encoder GEMMs, +5% on the all-layer cross K/V
   // GEMM whose 320 column tiles stream 210 MB of weights per row tile)
   P.xcd_remap = xcd_remap_enabled() && EPI != EPI_CROSS_KV;
-  // MWX_GEMM_PP=1: the ping-pong wave-group schedule (A/B)
-  static const bool pp = getenv("MWX_GEMM_PP") && atoi(getenv("MWX_GEMM_PP")) == 1;
-  if (pp)
-    gemm_big<T, EPI, OUT16, false, true><<<g, 512, 0, st>>>(A, lda, a_bstride, W, ldw, M, N, K, P);
-  else
-    gemm_big<T, EPI, OUT16><<<g, 512, 0, st>>>(A, lda, a_bstride, W, ldw, M, N, K, P);
+  gemm_big<T, EPI, OUT16><<<g, 512, 0, st>>>(A, lda, a_bstride, W, ldw, M, N, K, P);
 }
 
 template <typename T>
