@@ -793,8 +793,9 @@ def main():
                          "host memory, uploaded per step") if args.host_input else "resident in HBM")
                      + "; seeded weights in the ggml .bin layout)"),
             "config": {
-                "workload": (f"whisper-{args.arch} {args.wtype}: {args.clips} x {args.clip_seconds:g} s "
-                             f"clips per GPU, mel + encoder + cross-KV + {args.decode_steps} "
+                "workload": (f"whisper-{args.arch} {args.wtype}: batches of {args.clips} x "
+                             f"{args.clip_seconds:g} s clips per GPU ({lanes} in flight), mel + "
+                             f"encoder + cross-KV + {args.decode_steps} "
                              f"{'beam-%d' % args.beam if args.beam > 1 else 'greedy'} KV-cached "
                              f"decode steps per 30-s window, RCCL token gather to rank 0"),
                 "global_batch": world * args.clips,
