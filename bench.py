@@ -499,6 +499,45 @@ def stream_bench(args):
     return 0
 
 
+def run_lanes(n, lanes, step, stagger=0.0):
+    """Runs n batches over `lanes` host threads and returns their results in
+    batch order. Each lane drives its own states and HIP stream (the
+    SttEngine's parallel_requests batchers) and takes the next batch when its
+    previous one is done, so one lane's encoder / host work overlaps another
+    lane's decode; step(lane) runs one batch on that lane. The first error
+    stops every lane and is re-raised."""
+    if lanes <= 1:
+        return [step(0) for _ in range(n)]
+    import threading
+    out = {}
+    errs = []
+    nxt = [0]
+    lock = threading.Lock()
+
+    def lane_loop(lane):
+        try:
+            if stagger > 0:  # (inside the caller's timed region)
+                time.sleep(lane * stagger)
+            while True:
+                with lock:
+                    i = nxt[0]
+                    nxt[0] += 1
+                if i >= n or errs:
+                    return
+                out[i] = step(lane)
+        except Exception as ex:  # re-raised in the calling thread
+            errs.append(ex)
+
+    th = [threading.Thread(target=lane_loop, args=(i,)) for i in range(lanes)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if errs:
+        raise errs[0]
+    return [out[i] for i in range(n)]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1,
@@ -617,44 +656,8 @@ def main():
             gathered["tokens"] = g
 
     def run_steps(n):
-        """n batches over the lanes; each lane is a host thread driving its own
-        states and HIP stream (the SttEngine's parallel_requests batchers) and
-        takes the next batch when its previous one is done, so one lane's
-        encoder / host work overlaps another lane's decode. Gathers run
-        afterwards in batch order."""
-        if lanes == 1:
-            for _ in range(n):
-                gather(step(0))
-            return
-        import threading
-        out = {}
-        errs = []
-        nxt = [0]
-        lock = threading.Lock()
-
-        def lane_loop(lane):
-            try:
-                if args.lane_stagger > 0:  # (inside the timed region)
-                    time.sleep(lane * args.lane_stagger)
-                while True:
-                    with lock:
-                        i = nxt[0]
-                        nxt[0] += 1
-                    if i >= n or errs:
-                        return
-                    out[i] = step(lane)
-            except Exception as ex:  # re-raised in the main thread
-                errs.append(ex)
-
-        th = [threading.Thread(target=lane_loop, args=(i,)) for i in range(lanes)]
-        for t in th:
-            t.start()
-        for t in th:
-            t.join()
-        if errs:
-            raise errs[0]
-        for i in range(n):
-            gather(out[i])
+        for block in run_lanes(n, lanes, step, args.lane_stagger):
+            gather(block)
 
     for lane in range(lanes):
         for _ in range(args.warmup):
