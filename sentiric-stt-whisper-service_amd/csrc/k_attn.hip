@@ -375,24 +375,31 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
   const int part = tid >> 6, e = tid & 63;
   const int col = part * D + h * 64 + e;
   float pk[8];
+  float bcol = 0.0f;
   if (red) {
     const float* pp = P + (long)row * pcols + col;
 #pragma unroll
     for (int k = 0; k < 8; ++k) pk[k] = pp[min(k, KS - 1) * pstride];
+    // (requested with the slabs: a bias load issued after the key batches
+    // would make the query wait for all of them)
+    if (part != 1) bcol = bias[col];
   }
   LOADROWS0(ka, K)
+  // NBC: the second key batch is requested before the query is formed too,
+  // so two batches are in flight from the start
+  if constexpr (NBC > 0) LOADROWS(kb2, K, 1)
   if (red) {
     float acc = pk[0];
 #pragma unroll
     for (int k = 1; k < 8; ++k) acc += k < KS ? pk[k] : 0.0f;
     if (part == 0) {
-      sq[e] = (float)(_Float16)((acc + bias[col]) * qscale);
+      sq[e] = (float)(_Float16)((acc + bcol) * qscale);
     } else if (part == 1) {
       const _Float16 kv = (_Float16)(acc * kscale);
       snk[e] = (float)kv;
       K[(long)p_row * 64 + e] = kv;
     } else {
-      const _Float16 vv = (_Float16)(acc + bias[col]);
+      const _Float16 vv = (_Float16)(acc + bcol);
       snv[e] = (float)vv;
       V[(long)p_row * 64 + e] = vv;
     }
@@ -491,12 +498,11 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
     static_assert(NBC % 2 == 0 && NBC >= 4, "even batch count");
 #pragma unroll 1
     for (int b = 0; b < NBC - 2; b += 2) {
-      LOADROWS(kb2, K, b + 1)
       score_batch(ka, b);
       LOADROWS(ka, K, b + 2)
       score_batch(kb2, b + 1);
+      LOADROWS(kb2, K, b + 3)
     }
-    LOADROWS(kb2, K, NBC - 1)
     score_batch(ka, NBC - 2);
     LOADROWS(ka, V, 0)
     score_batch(kb2, NBC - 1);
@@ -646,6 +652,9 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
 #pragma unroll
     for (int k = 0; k < 8; ++k) pq[i][k] = pp[min(k, KS - 1) * pstride];
   }
+  // the bias is requested with the slabs (after the key loads, the query
+  // would wait for them)
+  const float bq = bias[h * 64 + (tid & 63)];
   if constexpr (KV8) {
     LOADROWS8(qa, sa, K8, KS8, 0, 0)
   } else {
@@ -659,7 +668,7 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
       float acc = pq[i][0];
 #pragma unroll
       for (int k = 1; k < 8; ++k) acc += k < KS ? pq[i][k] : 0.0f;
-      sq[q][e] = (float)(_Float16)(acc + bias[h * 64 + e]);
+      sq[q][e] = (float)(_Float16)(acc + bq);  // (e == tid & 63)
     }
   }
   __syncthreads();
