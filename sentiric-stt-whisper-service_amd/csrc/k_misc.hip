@@ -297,6 +297,38 @@ __device__ __forceinline__ double bsum256d(double v, double* red) {
   __syncthreads();
   return (red[0] + red[1]) + (red[2] + red[3]);
 }
+// several workgroup reductions through one barrier pair: each value is
+// reduced exactly as by its single-value form (wave reduction, then the four
+// wave results in the same order), so results are bit-identical
+__device__ __forceinline__ void bmax3_256(float& a, float& b, float& c, float (*red)[4]) {
+  a = wave_max_dpp(a);
+  b = wave_max_dpp(b);
+  c = wave_max_dpp(c);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) {
+    red[0][wid] = a;
+    red[1][wid] = b;
+    red[2][wid] = c;
+  }
+  __syncthreads();
+  a = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+  b = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
+  c = fmaxf(fmaxf(red[2][0], red[2][1]), fmaxf(red[2][2], red[2][3]));
+}
+__device__ __forceinline__ void bsum2_256(float& a, float& b, float (*red)[4]) {
+  a = wave_sum(a);
+  b = wave_sum(b);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) {
+    red[0][wid] = a;
+    red[1][wid] = b;
+  }
+  __syncthreads();
+  a = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+  b = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+}
 // argmax with lowest-index tie break
 __device__ __forceinline__ void better(float& v, int& idx, float ov, int oi) {
   if (ov > v || (ov == v && oi < idx)) {
@@ -327,6 +359,7 @@ __global__ __launch_bounds__(LP_T) void lp_filter_kernel(const float* __restrict
                                                          LPPart* __restrict__ parts,
                                                          LogitsConst C) {
   __shared__ float red[4];
+  __shared__ float red3[3][4];
   const int row = blockIdx.y, ch = blockIdx.x;
   const RowCtl c = ctl[row];
   if (!c.active || !c.sample) return;
@@ -366,9 +399,7 @@ __global__ __launch_bounds__(LP_T) void lp_filter_kernel(const float* __restrict
     else
       mtext = fmaxf(mtext, v[k]);
   });
-  m = bmax256(m, red);
-  mts = bmax256(mts, red);
-  mtext = bmax256(mtext, red);
+  bmax3_256(m, mts, mtext, red3);
   float s = 0.0f, sts = 0.0f, rs = 0.0f;
   sfor<0, LP_NPT>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
@@ -378,8 +409,7 @@ __global__ __launch_bounds__(LP_T) void lp_filter_kernel(const float* __restrict
       if (i >= C.beg) sts += expf(v[k] - mts);
     }
   });
-  s = bsum256(s, red);
-  sts = bsum256(sts, red);
+  bsum2_256(s, sts, red3);
   if (c.want_nosp) {
     rmax = bmax256(rmax, red);
     sfor<0, LP_NPT>([&](auto kc) {
@@ -438,8 +468,8 @@ __global__ __launch_bounds__(LP_T) void lp_probs_kernel(float* __restrict__ flt,
                                                         float* __restrict__ probs_out,
                                                         float* __restrict__ logprobs_out,
                                                         LogitsConst C) {
-  __shared__ float redf[4];
-  __shared__ int redi[4];
+  __shared__ float redf2[2][4];
+  __shared__ int redi2[2][4];
   __shared__ double redd[4];
   const int row = blockIdx.y, ch = blockIdx.x;
   const RowCtl c = ctl[row];
@@ -476,9 +506,34 @@ __global__ __launch_bounds__(LP_T) void lp_probs_kernel(float* __restrict__ flt,
       }
     }
   });
-  bargmax256(best, best_i, redf, redi);
-  bargmax256(tbest, tbest_i, redf, redi);
-  sum_ts = bsum256d(sum_ts, redd);
+  {  // (bargmax256 x 2 + bsum256d through one barrier pair, same orders)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      better(best, best_i, __shfl_xor(best, o, 64), __shfl_xor(best_i, o, 64));
+      better(tbest, tbest_i, __shfl_xor(tbest, o, 64), __shfl_xor(tbest_i, o, 64));
+    }
+    sum_ts = wave_sum_d_dpp(sum_ts);
+    const int lane = tid & 63, wid = tid >> 6;
+    __syncthreads();
+    if (lane == 0) {
+      redf2[0][wid] = best;
+      redi2[0][wid] = best_i;
+      redf2[1][wid] = tbest;
+      redi2[1][wid] = tbest_i;
+      redd[wid] = sum_ts;
+    }
+    __syncthreads();
+    best = redf2[0][0];
+    best_i = redi2[0][0];
+    tbest = redf2[1][0];
+    tbest_i = redi2[1][0];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      better(best, best_i, redf2[0][k], redi2[0][k]);
+      better(tbest, tbest_i, redf2[1][k], redi2[1][k]);
+    }
+    sum_ts = (redd[0] + redd[1]) + (redd[2] + redd[3]);
+  }
   if (tid == 0) {
     LPRes r;
     r.best = best;
