@@ -117,39 +117,51 @@ def oracle_stt_transcribe(o, pcm16, steps):
                            for s in segs], o.eot, o.token_bytes)
 
 
+CPU_DEC_STEPS = 8  # decode steps the large-model CPU leg measures (the rest are extrapolated)
+
+
 def cpu_large_sample(model_path, arch, threads, prompt_len, steps):
     """The oracle (scalar C++ + OpenMP) on a bounded sample of ONE clip of the
-    benched model: full log-mel, conv stem + 1 of the encoder layers, and 4
-    decode steps measured; the per-clip time is extrapolated to all layers,
-    the cross K/V and prompt + `steps` decode steps (a full large-v3 clip
-    takes minutes on the CPU)."""
+    benched model: full log-mel, conv stem + ALL encoder layers, the all-layer
+    cross K/V and the prompt + CPU_DEC_STEPS decode positions (KV-cached, on
+    the clip's own cross K/V) measured; only the remaining decode steps are
+    extrapolated, at the measured mean time per step."""
     import mwx
     import orc
-    L = orc.lib()
     o = orc.Oracle(model_path, threads=threads)
-    n_mels, d, H, Le, Ld, V = ARCH[arch]
     pcm = mwx.pcm16_to_f32(mwx.synth_pcm16(0))
     t0 = time.perf_counter()
     mel, _ = o.mel(pcm)
     t_mel = time.perf_counter() - t0
-    L.orc_set_enc_layer_limit(0)
     t0 = time.perf_counter()
-    o.encode(mel)
-    t_conv = time.perf_counter() - t0
-    L.orc_set_enc_layer_limit(1)
+    enc = o.encode(mel)
+    t_enc = time.perf_counter() - t0
     t0 = time.perf_counter()
-    o.encode(mel)
-    t_layer = time.perf_counter() - t0 - t_conv
-    L.orc_set_enc_layer_limit(-1)
-    k = np.zeros((Ld, 1500, d), np.float32)
+    k, v = o.cross(enc)
+    t_cross = time.perf_counter() - t0
+    n_meas = prompt_len + CPU_DEC_STEPS
+    toks = [o.sot] + [300 + i for i in range(n_meas - 1)]
     t0 = time.perf_counter()
-    o.decode_seq(k, k, [o.sot, 300, 301, 302])
-    t_dec = (time.perf_counter() - t0) / 4
-    layer_flops = 2 * 1500 * d * 12 * d + 4 * 1500 * 1500 * d
-    t_cross = t_layer * (2 * 1500 * d * 2 * d * Ld) / layer_flops
-    t_clip = t_mel + t_conv + Le * t_layer + t_cross + (prompt_len + steps) * t_dec
+    o.decode_seq(k, v, toks)
+    t_dec_meas = time.perf_counter() - t0
+    t_step = t_dec_meas / n_meas
+    n_total = prompt_len + steps
+    t_clip = t_mel + t_enc + t_cross + t_dec_meas + (n_total - n_meas) * t_step
     o.close()
-    return 30.0 / t_clip, t_mel + t_conv + t_layer + 4 * t_dec, t_clip
+    measured = t_mel + t_enc + t_cross + t_dec_meas
+    return 30.0 / t_clip, measured, t_clip, n_meas, n_total
+
+
+def granted_cpus():
+    """CPUs this job may use: the affinity mask, capped by OMP_NUM_THREADS when
+    the host sets it (the GPU box grants 16 CPUs per GPU and exports
+    OMP_NUM_THREADS=16 while os.cpu_count() reports the whole machine)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return min(aff, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else aff, aff
 
 
 def cpu_baseline(model_path, arch, threads, prompt_len, steps):
@@ -161,17 +173,20 @@ def cpu_baseline(model_path, arch, threads, prompt_len, steps):
     end to end through the SttEngine steps (oracle_stt_transcribe)."""
     import mwx
     import orc
+    granted, aff = granted_cpus()
     out = {"unit": "audio-sec/s", "kind": "port", "cpu_model": cpu_model(),
-           "host_cpus": os.cpu_count(), "label": "CPU restatement of the reference path "
-                                                 "(whisper.cpp v1.8.2 semantics)"}
+           "host_cpus": os.cpu_count(), "affinity_cpus": aff, "granted_cpus": granted,
+           "label": "CPU restatement of the reference path (whisper.cpp v1.8.2 semantics)"}
     legs = {}
     for th in sorted({4, threads}):
-        v, sampled, t_clip = cpu_large_sample(model_path, arch, th, prompt_len, steps)
+        v, measured, t_clip, n_meas, n_total = cpu_large_sample(model_path, arch, th, prompt_len,
+                                                                steps)
         legs[th] = {"value": round(v, 4), "cores": th,
-                    "sample": (f"1 clip of 30 s, {arch}: full log-mel + conv + 1/{ARCH[arch][3]} "
-                               f"encoder layers + 4 decode steps measured ({sampled:.1f} s), "
-                               f"extrapolated to all layers, cross K/V and {prompt_len + steps} "
-                               f"decode steps: {t_clip:.1f} s/clip")}
+                    "sample": (f"1 clip of 30 s, {arch}: log-mel + conv + all {ARCH[arch][3]} "
+                               f"encoder layers + all-layer cross K/V + {n_meas} of {n_total} "
+                               f"decode positions measured ({measured:.1f} s); the other "
+                               f"{n_total - n_meas} decode steps extrapolated at the measured "
+                               f"mean: {t_clip:.1f} s/clip")}
     out.update(legs[threads])
     out["threads4"] = legs[4]
     tiny = os.path.join(os.environ.get("TMPDIR", "/tmp"), "mwx_bench_tiny.en_f16.bin")
@@ -615,7 +630,7 @@ def main():
     p.language = b"en"
     p.temperature = 0.0
     p.temperature_inc = 0.0
-    p.token_timestamps = False
+    p.token_timestamps = True  # as the service sets it (src/stt_engine.cpp:225)
     p.suppress_nst = True
     p.bench_fixed_steps = args.decode_steps
     prompt_len = 3 if ARCH[args.arch][5] >= 51865 else 1
@@ -666,7 +681,11 @@ def main():
     owners = [ctx.state(lane * args.clips) for lane in range(lanes)]  # workspace / stream owners
     # the dominant kernel's class, plus the encoder GEMMs (MFMA fraction,
     # SURVEY.md §8 d asks for both bounds), timed in the same steps
+    # (+ event_bracket: the timing events around an empty kernel at the same
+    # point of the decode chain, whose average is the events' own cost)
     classes = [args.perf_class] + (["enc_gemm"] if args.perf_class != "enc_gemm" else [])
+    if args.perf_class.startswith("dec_attn"):
+        classes.append("event_bracket")
     for so in owners:
         L.mwx_perf_read(so, None, None)
         L.mwx_perf_enable(so, ",".join(classes).encode())
@@ -693,17 +712,21 @@ def main():
         return out
 
     timed = read_timed(owners)
-    timed_1lane, steps_1lane = None, 0
+    timed_1lane, steps_1lane, elapsed_1lane = None, 0, None
     if lanes > 1:
         # after the timed region (not part of `value`): the same batches on one
-        # lane, so the kernels' rooflines are also reported without another
-        # lane's kernels sharing HBM and CUs with them
+        # lane (B = 32 strictly one batch at a time), timed and with the
+        # kernels' rooflines measured without another lane's kernels sharing
+        # HBM and CUs with them
         steps_1lane = min(2 if args.clip_seconds <= 30 else 1, args.steps)
         L.mwx_perf_read(owners[0], None, None)
         L.mwx_perf_enable(owners[0], ",".join(classes).encode())
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
         for _ in range(steps_1lane):
             gather(step(0))
         torch.cuda.synchronize()
+        elapsed_1lane = time.perf_counter() - t1
         timed_1lane = read_timed(owners[:1])
     if dist is not None:
         e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -715,7 +738,14 @@ def main():
     def make_roofs(tm, nsteps):
         """(dominant-kernel roofline, encoder-GEMM roofline) from live timings"""
         launches = max(1, tm[args.perf_class][1])
-        avg_s = tm[args.perf_class][0] / 1e3 / launches
+        avg_raw = tm[args.perf_class][0] / 1e3 / launches
+        # the bracket of an empty kernel at the same point of the chain: the
+        # two event nodes' own cost (+ the empty kernel), removed from the
+        # kernel's bracket so the duration compares with rocprofv3's
+        ev_s = None
+        if tm.get("event_bracket", (0, 0))[1] > 0:
+            ev_s = tm["event_bracket"][0] / 1e3 / tm["event_bracket"][1]
+        avg_s = avg_raw - ev_s if ev_s is not None and ev_s < 0.5 * avg_raw else avg_raw
         # decode kernels run per row group (MWX_DECODE_GROUPS chains on their
         # own streams, default 1); the engine times every 8th decode step's
         # launches (MWX_PERF_PERIOD), all inside the timed region
@@ -745,6 +775,8 @@ def main():
                     "unit": "TFLOP/s", "frac": round(achieved / MFMA_PEAK_TFLOPS, 4),
                     "traffic": traffic}
         roof.update({"kernel": args.perf_class, "avg_launch_us": round(avg_s * 1e6, 2),
+                     "avg_bracket_us": round(avg_raw * 1e6, 2),
+                     "event_bracket_us": round(ev_s * 1e6, 2) if ev_s is not None else None,
                      "launches": tm[args.perf_class][1], "work_per_launch": work,
                      "work_desc": desc})
         roof_enc = None
@@ -767,12 +799,16 @@ def main():
         roof_1lane = None
         if timed_1lane is not None:
             r1, e1 = make_roofs(timed_1lane, steps_1lane)
-            roof_1lane = {"note": f"{steps_1lane} batches on one lane after the timed region",
+            v1 = args.clips * args.clip_seconds * steps_1lane / elapsed_1lane
+            roof_1lane = {"note": f"{steps_1lane} batches on one lane after the timed region "
+                                  f"(one batch of {args.clips} clips at a time)",
+                          "value": round(v1, 2), "unit": "audio-sec/s",
+                          "ms_per_step": round(elapsed_1lane / steps_1lane * 1e3, 2),
                           "roofline": r1, "roofline_encoder": e1}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            # all cores granted to this job (OMP_NUM_THREADS on the GPU box)
-            threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
+            # all cores granted to this job (the GPU box: 16 per GPU, OMP_NUM_THREADS)
+            threads = granted_cpus()[0]
             try:
                 sys.path.insert(0, os.path.join(ROOT, "oracle"))
                 cpu = cpu_baseline(path, args.arch, threads, prompt_len, args.decode_steps)
@@ -800,7 +836,8 @@ def main():
                              f"{args.clip_seconds:g} s clips per GPU ({lanes} in flight), mel + "
                              f"encoder + cross-KV + {args.decode_steps} "
                              f"{'beam-%d' % args.beam if args.beam > 1 else 'greedy'} KV-cached "
-                             f"decode steps per 30-s window, RCCL token gather to rank 0"),
+                             f"decode steps per 30-s window, token timestamps on (as the service), RCCL "
+                             f"token gather to rank 0"),
                 "global_batch": world * args.clips,
                 "seq_len": 1500,
                 "parallelism": f"dp{world}",

@@ -1,0 +1,62 @@
+#!/bin/bash
+# One parameterised GPU run recipe (gpurun). Usage, on the box:
+#   bash scripts/gpu_run.sh TAG STEP [STEP ...]
+# steps (each under its own time limit; the first failure ends the run):
+#   tests      pytest -m gpu (one process)
+#   smoke      __graft_entry__.smoke()
+#   bench      default bench line (C3: 2 lanes + one-lane value + CPU baseline)
+#   benchq     default bench without the CPU baseline (quick)
+#   bench1     C3 on one lane
+#   c2         C2: base f16, one clip per request
+#   b5         beam 5 (service default decode), C3 shape
+#   c5         C5: MX-fp8, beam 5, 600-s long-form clips
+#   prompt     long-form leg with previous-window text carried as the prompt
+#   prof       rocprofv3 --kernel-trace --stats of the exact default bench command
+#   prof1      the same for --lanes 1
+#   profc2     kernel trace of the C2 leg
+#   pmc        FETCH_SIZE / WRITE_SIZE / MFMA-busy passes (each its own run) on a short decode
+# Outputs go to gpurun_out/<TAG>_*; copy the summaries to be judged into profiles/.
+set -o pipefail
+export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT" || exit 1
+O=$GRAFT_REPO_ROOT/gpurun_out
+mkdir -p "$O"
+TAG=$1
+shift
+B="python3 $GRAFT_REPO_ROOT/bench.py"
+run() {  # name, seconds, command...
+  local name=$1 secs=$2
+  shift 2
+  echo "[$(date +%T)] $name"
+  timeout -k 10 "$secs" "$@" > "$O/${TAG}_${name}.out" 2> "$O/${TAG}_${name}.err"
+  local rc=$?
+  if [ $rc -ne 0 ]; then
+    echo "$name failed rc=$rc"
+    tail -30 "$O/${TAG}_${name}.out" "$O/${TAG}_${name}.err"
+    exit $rc
+  fi
+  tail -1 "$O/${TAG}_${name}.out" | cut -c1-400
+}
+for s in "$@"; do
+  case $s in
+    tests) run tests 1150 python -u -m pytest tests -m gpu -x -v -s -rf --timeout 300 --timeout-method thread ;;
+    smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python -u bench.py --steps 20 --warmup 5 ;;
+    benchq) run benchq 400 python -u bench.py --steps 8 --warmup 2 --no-cpu-baseline ;;
+    bench1) run bench1 400 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
+    c2) run c2 300 python -u bench.py --arch base --wtype f16 --clips 1 --lanes 1 --steps 20 --warmup 3 --no-cpu-baseline ;;
+    b5) run b5 500 python -u bench.py --beam 5 --steps 4 --warmup 1 --no-cpu-baseline ;;
+    c5) run c5 700 python -u bench.py --fp8 --beam 5 --clip-seconds 600 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    prompt) run prompt 700 python -u bench.py --prompt-leg --steps 2 --warmup 1 --no-cpu-baseline ;;
+    prof) (cd /tmp && run prof 600 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_prof" -o prof -- $B --steps 4 --warmup 2 --no-cpu-baseline) || exit 4 ;;
+    prof1) (cd /tmp && run prof1 600 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_prof1" -o prof -- $B --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline) || exit 4 ;;
+    profc2) (cd /tmp && run profc2 400 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_profc2" -o prof -- $B --arch base --wtype f16 --clips 1 --lanes 1 --steps 5 --warmup 2 --no-cpu-baseline) || exit 4 ;;
+    pmc)
+      for C in FETCH_SIZE WRITE_SIZE; do
+        (cd /tmp && run pmc_$C 400 rocprofv3 --pmc $C --output-format csv -d "$O/${TAG}_pmc_$C" -o pmc -- $B --lanes 1 --steps 1 --warmup 0 --decode-steps 8 --no-cpu-baseline) || exit 5
+      done
+      (cd /tmp && run pmc_MFMA 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$O/${TAG}_pmc_MFMA" -o pmc -- $B --lanes 1 --steps 1 --warmup 0 --decode-steps 8 --no-cpu-baseline) || exit 5 ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "all steps done"

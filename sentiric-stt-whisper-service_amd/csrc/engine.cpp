@@ -254,6 +254,12 @@ static int perf_class_index(const State& S, const char* cls) {
   return -1;
 }
 
+// True when a PerfScope of class `cls` would record events right now.
+static bool perf_on(const State& s, const char* cls) {
+  if (s.perf_class.empty() || (s.capturing && !s.capture_perf)) return false;
+  return perf_class_index(s, cls) >= 0;
+}
+
 // Records a start/stop HIP event pair around a launch when `cls` is the
 // state's enabled perf class.
 struct PerfScope {
@@ -1015,6 +1021,13 @@ struct Driver {
       int k3;
       { PerfScope ps(S, "dec_gemm", s);
         k3 = gemm_splitk_partials<T>(hd, Dw(W.cq), n, d, d, Pq, s); }
+      if (perf_on(S, "event_bracket")) {
+        // calibration: the same event pair around an empty kernel at the same
+        // point of the chain (bench.py subtracts its average from the
+        // cross-attention brackets: the two event nodes' own cost)
+        PerfScope ps(S, "event_bracket", s);
+        launch_perf_empty(s);
+      }
       { PerfScope ps(S, "dec_attn_cross", s);
         // the decoders of a beam / best-of group share their clip's cross K/V:
         // stream it once per group; an MX-fp8 cache is read by the grouped

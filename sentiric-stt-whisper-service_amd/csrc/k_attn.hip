@@ -887,7 +887,7 @@ bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float*
     else                                       \
       XL(N, false, false);                     \
     return true;
-    XQ(1) XQ(2) XQ(3) XQ(4) XQ(5) XQ(6) XQ(8)
+    XQ(1) XQ(2) XQ(3) XQ(4) XQ(5) XQ(6) XQ(7) XQ(8)
 #undef XQ
 #undef XL
     default: return false;

@@ -185,7 +185,7 @@ void dec_attention(const float* P, int KS, int pcols, const float* bias, float q
 // Cross-attention for groups of nq consecutive rows that share one cross
 // slot (beam-search / best-of decoders of a clip; kv_index[row] equal within a
 // group): K/V of the slot are streamed once per group. Same per-row results as
-// dec_attention. Returns false if nq is not supported (2, 3, 4, 5, 6, 8).
+// dec_attention. Returns false if nq is not supported (1..8; f16 caches: 2..8).
 // kscale8 / vscale8 != nullptr: the cache is MX-fp8 (kbase / vbase hold e4m3
 // codes [slot][H][cap][64], the scales [slot][H][cap][2] E8M0), any nq >= 1.
 template <typename T>
@@ -249,6 +249,8 @@ struct RunReport {
   int tok, pos, act, pad;  // the next step's inputs as the device set them
   RowCtl next;
 };
+// empty one-wave kernel (timing-event overhead calibration, bench.py)
+void launch_perf_empty(hipStream_t st);
 void row_advance(RowRun* run, int* run_step, const int* prompt, int* stepin, RowCtl* ctl,
                  const TokOut* out, RunReport* rep, const RunConst& C, hipStream_t st);
 

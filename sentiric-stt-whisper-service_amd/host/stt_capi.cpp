@@ -157,7 +157,9 @@ void* mwx_stt_new_ex(const char* model_dir, const char* model_filename, int para
 // returns the events as JSON (strings hex-encoded) like mwx_stt_transcribe_pcm16.
 // If `cap` is too small the chunk is still consumed: the events are kept and
 // -(needed + 2) is returned; mwx_stt_stream_drain then delivers them (never
-// feed the chunk again).
+// feed the chunk again). While such events are undelivered, a feed returns
+// -3 (MWX_STT_PENDING) WITHOUT consuming its chunk: drain, then feed the same
+// chunk again. -1 = error, -2 = EngineBusyException.
 struct StreamHandle {
   explicit StreamHandle(SttEngine& e) : session(e) {}
   StreamSession session;
@@ -175,7 +177,7 @@ int mwx_stt_stream_drain(void* s, char* out, int cap) {
 
 int mwx_stt_stream_feed(void* s, const uint8_t* data, int len, char* out, int cap) {
   StreamHandle* h = static_cast<StreamHandle*>(s);
-  if (!h->pending.empty()) return -1;  // undelivered events: drain first
+  if (!h->pending.empty()) return -3;  // MWX_STT_PENDING: drain first, chunk not consumed
   try {
     const auto evs = h->session.feed(data, len > 0 ? (size_t)len : 0);
     std::string o = "[";

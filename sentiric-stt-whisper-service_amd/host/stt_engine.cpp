@@ -400,25 +400,27 @@ std::vector<TranscriptionResult> SttEngine::transcribe(const std::vector<float>&
   if (!ctx_) return {};
   if (options.should_abort && options.should_abort()) return {};
   // src/stt_engine.cpp:136-145: non-16 kHz input is resampled; an empty
-  // result (failure) keeps the original buffer
+  // result (failure) keeps the original buffer. One pass, as the reference
+  // swaps its pcm pointer: the abort callback is polled once above and
+  // processing_time_ms includes the resampling.
   std::vector<float> resampled;
   if (input_sample_rate != 16000)
     resampled = resample_audio(pcmf32.data(), pcmf32.size(), input_sample_rate, 16000);
-  if (!resampled.empty()) return transcribe(resampled, 16000, options, out_metrics);
-  const size_t pcm_size = pcmf32.size();
+  const std::vector<float>& pcm = resampled.empty() ? pcmf32 : resampled;
+  const size_t pcm_size = pcm.size();
   const size_t min_samples = static_cast<size_t>((settings_.vad_ms_min_duration * 16000) / 1000);
   if (pcm_size < min_samples) {
     if (out_metrics) *out_metrics = {0.0, 0.0, 0};
     return {};
   }
-  if (settings_.max_batch > 1) return transcribe_batched(pcmf32, options, out_metrics);
+  if (settings_.max_batch > 1) return transcribe_batched(pcm, options, out_metrics);
   StateGuard guard(*this);
   mwx_state* state = guard.get();
   const auto t_acq = std::chrono::steady_clock::now();
   std::string lang;
   std::function<bool()> abort_fn = options.should_abort;
   const mwx_full_params p = make_params(options, lang, abort_fn);
-  const int ret = mwx_full_with_state(ctx_, state, p, pcmf32.data(), static_cast<int>(pcm_size));
+  const int ret = mwx_full_with_state(ctx_, state, p, pcm.data(), static_cast<int>(pcm_size));
   const auto t_end = std::chrono::steady_clock::now();
   if (out_metrics) *out_metrics = {ms_between(t_start, t_acq), ms_between(t_acq, t_end), 0};
   if (ret != 0) {
@@ -428,7 +430,7 @@ std::vector<TranscriptionResult> SttEngine::transcribe(const std::vector<float>&
                  ret);
     return {};
   }
-  return collect(state, lang, pcmf32.data(), pcm_size, options.prosody_opts,
+  return collect(state, lang, pcm.data(), pcm_size, options.prosody_opts,
                  out_metrics ? &out_metrics->token_count : nullptr);
 }
 

@@ -10,7 +10,10 @@ Whisper on the same seeded weights instead:
     reflect-pads the clip end where whisper.cpp zero-pads, so only frames
     0..2997 are comparable.
   * encoder / decoder: WhisperForConditionalGeneration built from a local
-    config with the weights of the seeded `micro` ggml file, activation forced
+    config with the weights of the seeded `micro` ggml file and of the two
+    benchmarked geometries (large-v3 d 1280 / 20 heads / 128 mels / vocab
+    51866 with 2 + 2 layers in bf16; base d 512 at full 6 + 6 depth in f16),
+    activation forced
     to the tanh GELU ggml uses (conv GELU patched too), run on the oracle's own
     mel so only the network math is compared. The oracle is run in its "exact"
     (fp32, no 16-bit rounding) mode for this comparison.
@@ -128,6 +131,59 @@ def hf_model(hp, t):
     return m
 
 
+def network_golden(arch, wtype, tf_tokens, pcm, prefix, out):
+    """HF fp32 encoder rows / stats and teacher-forced logits for the seeded
+    `arch` model (weight type `wtype`), on the oracle's own mel."""
+    path = os.path.join("/tmp", f"golden_{arch}_{wtype}.bin")
+    mwx.write_synthetic_model(path, arch, wtype, 0)
+    hp, t = read_ggml(path)
+    o = orc.Oracle(path, exact=True)
+    mel, _ = o.mel(pcm)
+    feats = torch.from_numpy(np.ascontiguousarray(mel[:, :3000]))[None]
+    orig_gelu = torch.nn.functional.gelu
+    torch.nn.functional.gelu = lambda x, approximate="none": orig_gelu(x, approximate="tanh")
+    try:
+        m = hf_model(hp, t)
+        with torch.no_grad():
+            enc = m.model.encoder(feats).last_hidden_state
+            dec = m(encoder_outputs=(enc,), decoder_input_ids=torch.tensor([tf_tokens])).logits[0]
+    finally:
+        torch.nn.functional.gelu = orig_gelu
+    enc = enc[0].numpy()
+    dec = dec.numpy()
+    out[prefix + "enc_rows"] = np.array([0, 1, 2, 500, 1000, 1499], np.int32)
+    out[prefix + "enc_hf"] = enc[out[prefix + "enc_rows"]].astype(np.float32)
+    out[prefix + "enc_hf_mean"] = np.float64(enc.mean())
+    out[prefix + "enc_hf_std"] = np.float64(enc.std())
+    out[prefix + "tf_tokens"] = np.array(tf_tokens, np.int32)
+    top = np.argsort(-dec, axis=1)[:, :10]
+    out[prefix + "dec_top_ids"] = top.astype(np.int32)
+    out[prefix + "dec_top_vals"] = np.take_along_axis(dec, top, axis=1).astype(np.float32)
+    out[prefix + "dec_lse"] = np.log(np.exp(dec - dec.max(1, keepdims=True)).sum(1)) + dec.max(1)
+    out[prefix + "dec_sample_ids"] = np.arange(0, dec.shape[1], 997, dtype=np.int32)
+    out[prefix + "dec_sample_vals"] = dec[:, out[prefix + "dec_sample_ids"]].astype(np.float32)
+    # quick self-check
+    enc_o = o.encode(mel)
+    print(arch, "enc max|diff| vs oracle-exact:", np.abs(enc_o - enc).max(), "std", enc.std())
+    k, v = o.cross(enc_o)
+    lg = o.decode_seq(k, v, tf_tokens)
+    print(arch, "logits max|diff|:", np.abs(lg - dec).max(), "std", dec.std())
+    o.close()
+    os.remove(path)
+
+
+# the benchmarked geometries (BASELINE.json configs[1..4]): large-v3 (d 1280,
+# 20 heads, 128 mels, vocab 51866; 2 + 2 layers so HF and the oracle stay
+# cheap, bf16 = C3's weight type) and base at full depth (d 512, 6 + 6 layers,
+# f16 = C2's weight type)
+GEOMETRIES = [
+    ("micro", mwx.GGML_F16, TF_TOKENS, ""),
+    ("large-v3-l2", mwx.GGML_BF16, [50258, 50259, 50360, 300, 1234, 40000, 220, 50400, 50364],
+     "v3_"),
+    ("base", mwx.GGML_F16, [50258, 50259, 50359, 300, 1234, 40000, 220, 50400, 50363], "base_"),
+]
+
+
 def main():
     from transformers import WhisperFeatureExtractor
     pcm = mwx.pcm16_to_f32(mwx.synth_pcm16(0))
@@ -139,43 +195,11 @@ def main():
         out[f"{key}_rows"] = np.array(rows, np.int32)
         out[f"{key}_hf"] = feats[rows, :2998].astype(np.float32)
         out[f"{key}_hf_mean"] = np.float64(feats[:, :2998].mean())
-    # ---- micro network (exact oracle mode vs HF fp32) ----
-    path = os.path.join("/tmp", "golden_micro.bin")
-    mwx.write_synthetic_model(path, "micro", mwx.GGML_F16, 0)
-    hp, t = read_ggml(path)
-    o = orc.Oracle(path, exact=True)
-    mel, _ = o.mel(pcm)
-    feats = torch.from_numpy(np.ascontiguousarray(mel[:, :3000]))[None]
-    orig_gelu = torch.nn.functional.gelu
-    torch.nn.functional.gelu = lambda x, approximate="none": orig_gelu(x, approximate="tanh")
-    try:
-        m = hf_model(hp, t)
-        with torch.no_grad():
-            enc = m.model.encoder(feats).last_hidden_state
-            dec = m(encoder_outputs=(enc,), decoder_input_ids=torch.tensor([TF_TOKENS])).logits[0]
-    finally:
-        torch.nn.functional.gelu = orig_gelu
-    enc = enc[0].numpy()
-    dec = dec.numpy()
-    out["enc_rows"] = np.array([0, 1, 2, 500, 1000, 1499], np.int32)
-    out["enc_hf"] = enc[out["enc_rows"]].astype(np.float32)
-    out["enc_hf_mean"] = np.float64(enc.mean())
-    out["enc_hf_std"] = np.float64(enc.std())
-    out["tf_tokens"] = np.array(TF_TOKENS, np.int32)
-    top = np.argsort(-dec, axis=1)[:, :10]
-    out["dec_top_ids"] = top.astype(np.int32)
-    out["dec_top_vals"] = np.take_along_axis(dec, top, axis=1).astype(np.float32)
-    out["dec_lse"] = np.log(np.exp(dec - dec.max(1, keepdims=True)).sum(1)) + dec.max(1)
-    out["dec_sample_ids"] = np.arange(0, dec.shape[1], 997, dtype=np.int32)
-    out["dec_sample_vals"] = dec[:, out["dec_sample_ids"]].astype(np.float32)
+    # ---- networks (exact oracle mode vs HF fp32) ----
+    for arch, wtype, toks, prefix in GEOMETRIES:
+        network_golden(arch, wtype, toks, pcm, prefix, out)
     np.savez_compressed(os.path.join(OUT, "hf_golden.npz"), **out)
     print("wrote", os.path.join(OUT, "hf_golden.npz"))
-    # quick self-check
-    enc_o = o.encode(mel)
-    print("enc max|diff| vs oracle-exact:", np.abs(enc_o - enc).max(), "std", enc.std())
-    k, v = o.cross(enc_o)
-    lg = o.decode_seq(k, v, TF_TOKENS)
-    print("logits max|diff|:", np.abs(lg - dec).max(), "std", dec.std())
 
 
 if __name__ == "__main__":
