@@ -352,13 +352,15 @@ def prosody_cpu_baseline(pcm, desc, budget_s=10.0):
 
 def gather_summary(block, clips, per_clip):
     """Rank 0's view of the last step's record gather: clips received and
-    whether every clip carries its full fixed-length token record."""
+    whether every clip carries its full fixed-length token record (per_clip
+    None: decoding until the model stops, every clip has some tokens)."""
     import shard
     if block is None:
         return None
     recs = shard.unpack_records(block)
+    full = (lambda r: len(r) == per_clip) if per_clip else (lambda r: len(r) > 0)
     return {"clips": len(recs), "tokens": sum(len(r) for r in recs),
-            "complete": len(recs) == clips and all(len(r) == per_clip for r in recs)}
+            "complete": len(recs) == clips and all(full(r) for r in recs)}
 
 
 def launch_ranks(n):
@@ -566,7 +568,16 @@ def main():
     ap.add_argument("--arch", default="large-v3")
     ap.add_argument("--wtype", default="bf16", choices=["bf16", "f16"])
     ap.add_argument("--clips", type=int, default=32, help="30-s clips per GPU")
-    ap.add_argument("--decode-steps", type=int, default=220)
+    ap.add_argument("--decode-steps", type=int, default=220,
+                    help="fixed decode steps per 30-s window (bench_fixed_steps); 0 = decode "
+                         "until the model stops (EOT / timestamps), carrying each window's text "
+                         "into the next window's prompt")
+    ap.add_argument("--rich", action="store_true",
+                    help="'-rich' synthetic weights (timestamps, EOT and segment splits in the "
+                         "token stream; use with --decode-steps 0)")
+    ap.add_argument("--prompt-leg", action="store_true",
+                    help="long-form leg with real previous-window text in every prompt: "
+                         "--rich --decode-steps 0 --clip-seconds 600")
     ap.add_argument("--beam", type=int, default=0,
                     help="beam size (0: greedy; the service default is 5)")
     ap.add_argument("--clip-seconds", type=float, default=30.0,
@@ -589,6 +600,8 @@ def main():
     ap.add_argument("--prosody", action="store_true",
                     help="segment-prosody leg (SURVEY.md §8 f4) instead of transcription")
     args = ap.parse_args()
+    if args.prompt_leg:
+        args.rich, args.decode_steps, args.clip_seconds = True, 0, 600.0
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return launch_ranks(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -613,10 +626,11 @@ def main():
 
     import mwx
     wt = mwx.GGML_BF16 if args.wtype == "bf16" else mwx.GGML_F16
-    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"mwx_bench_{args.arch}_{args.wtype}.bin")
+    march = args.arch + ("-rich" if args.rich else "")
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"mwx_bench_{march}_{args.wtype}.bin")
     if local == 0 and not os.path.exists(path):
         tmp = path + f".tmp{os.getpid()}"
-        mwx.write_synthetic_model(tmp, args.arch, wt, 0)
+        mwx.write_synthetic_model(tmp, march, wt, 0)
         os.replace(tmp, path)
     barrier()
     ctx = mwx.Context.open(path, device=local,
@@ -635,7 +649,7 @@ def main():
     p.bench_fixed_steps = args.decode_steps
     prompt_len = 3 if ARCH[args.arch][5] >= 51865 else 1
     n_windows = max(1, int(np.ceil(args.clip_seconds / 30.0 - 1e-9)))
-    max_tok = args.decode_steps * n_windows
+    max_tok = (args.decode_steps or 448) * n_windows
     gathered = {}
 
     # inputs resident in HBM before the timed region (the PCIe-inclusive rate,
@@ -662,7 +676,11 @@ def main():
             raise RuntimeError(f"mwx_full_batch rc={rc}")
         print(f"bench.py: lane {lane}: batch done", file=sys.stderr, flush=True)  # (progress)
         s0 = lane * args.clips
-        return shard.pack_records([ctx.token_records(s0 + c) for c in range(args.clips)], max_tok)
+        recs = [ctx.token_records(s0 + c) for c in range(args.clips)]
+        tok_count.append(sum(len(r) for r in recs))
+        return shard.pack_records(recs, max_tok)
+
+    tok_count = []  # tokens generated per batch (list.append: thread-safe)
 
     def gather(block):
         # RCCL over xGMI: every rank's token records (id, t0, t1, p) to rank 0
@@ -689,6 +707,9 @@ def main():
     for so in owners:
         L.mwx_perf_read(so, None, None)
         L.mwx_perf_enable(so, ",".join(classes).encode())
+    for lane in range(lanes):
+        ctx.decode_counters(lane * args.clips, reset=True)
+    del tok_count[:]
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -712,6 +733,16 @@ def main():
         return out
 
     timed = read_timed(owners)
+    # decode work of the timed batches: steps launched (one per token position
+    # of the longest row), prompt positions run by the batched prefill, tokens
+    dsteps = dpre = 0
+    for lane in range(lanes):
+        a, b = ctx.decode_counters(lane * args.clips, reset=True)
+        dsteps, dpre = dsteps + a, dpre + b
+    decode_work = {"decode_steps_per_batch": round(dsteps / args.steps, 1),
+                   "prefill_positions_per_batch": round(dpre / args.steps, 1),
+                   "tokens_per_clip": round(sum(tok_count) / args.steps / args.clips, 1),
+                   "windows_per_clip": n_windows if args.decode_steps else None}
     timed_1lane, steps_1lane, elapsed_1lane = None, 0, None
     if lanes > 1:
         # after the timed region (not part of `value`): the same batches on one
@@ -832,9 +863,10 @@ def main():
                          "host memory, uploaded per step") if args.host_input else "resident in HBM")
                      + "; seeded weights in the ggml .bin layout)"),
             "config": {
-                "workload": (f"whisper-{args.arch} {args.wtype}: batches of {args.clips} x "
+                "workload": (f"whisper-{args.arch}{' (-rich weights)' if args.rich else ''} "
+                             f"{args.wtype}: batches of {args.clips} x "
                              f"{args.clip_seconds:g} s clips per GPU ({lanes} in flight), mel + "
-                             f"encoder + cross-KV + {args.decode_steps} "
+                             f"encoder + cross-KV + {args.decode_steps or 'until-EOT'} "
                              f"{'beam-%d' % args.beam if args.beam > 1 else 'greedy'} KV-cached "
                              f"decode steps per 30-s window, token timestamps on (as the service), RCCL "
                              f"token gather to rank 0"),
@@ -846,7 +878,9 @@ def main():
             "audio_sec_per_s_per_gpu": round(value / world, 2),
             "rtf": round(elapsed / audio_s * world, 6),
             "x_realtime_per_gpu": round(value / world, 1),
-            "gathered": gather_summary(gathered.get("tokens"), world * args.clips, max_tok),
+            "gathered": gather_summary(gathered.get("tokens"), world * args.clips,
+                                       max_tok if args.decode_steps else None),
+            "decode_work": decode_work,
             "roofline": roof,
             "roofline_encoder": roof_enc,
             "one_lane": roof_1lane,

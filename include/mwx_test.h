@@ -31,6 +31,12 @@ int mwx_test_encode(struct mwx_context* ctx, struct mwx_state* state, const floa
 int mwx_test_decode(struct mwx_context* ctx, struct mwx_state* state, const int* tokens, int n,
                     float* logits_out);
 
+/* Decode work counters of a state (the first state of a batch drives it):
+ * decode steps launched and prompt positions run by the batched prompt
+ * prefill since the last reset. reset != 0 zeroes them after reading. */
+int mwx_test_decode_counters(struct mwx_state* state, long* steps, long* prefill_positions,
+                             int reset);
+
 /* As mwx_test_decode, but only the logits of the last token are copied out
  * (logits_last [n_vocab]). */
 int mwx_test_decode_last(struct mwx_context* ctx, struct mwx_state* state, const int* tokens,

@@ -32,7 +32,7 @@ run() {  # name, seconds, command...
   local rc=$?
   if [ $rc -ne 0 ]; then
     echo "$name failed rc=$rc"
-    tail -30 "$O/${TAG}_${name}.out" "$O/${TAG}_${name}.err"
+    tail -n 30 "$O/${TAG}_${name}.out" "$O/${TAG}_${name}.err"
     exit $rc
   fi
   tail -1 "$O/${TAG}_${name}.out" | cut -c1-400

@@ -207,6 +207,12 @@ struct State {
   // decoder workspace (row-batched)
   DBuf xd, hd, qd, od, ffd, logits, kself, vself, stepin, ctl, tokout, probs, logprobs, smask;
   DBuf pqkv, pres, pq;  // split-K partial slabs of the decode GEMMs
+  // batched prompt prefill: virtual-row inputs [tok|pos|act|xidx|crow] and the
+  // layer stack's activations / slabs for up to MWX_PREFILL_ROWS virtual rows
+  DBuf pf_in, pf_x, pf_h, pf_o, pf_ff, pf_pqkv, pf_pres, pf_pq;
+  // counters (mwx_test_decode_counters): decode steps launched, prompt
+  // positions prefilled
+  long n_steps = 0, n_prefill = 0;
   DBuf lpflt, lpparts, lpres;  // logits-processing scratch
   // beam search KV hand-over without copies: per row, positions below
   // kvown[row] are read from row kvmap[row][pos] (host copies in kvmap_h/kvown_h)
@@ -976,44 +982,69 @@ struct Driver {
     return gs;
   }
 
-  // decoder step for rows [r0, r0+n) of an R-row step, launched on `s`
-  void decode_group(int R, int r0, int n, size_t prow, bool want_probs, hipStream_t s) {
-    int* si = (int*)S.stepin.p;
-    const int* tok = si + r0;
-    const int* pos = si + R + r0;
-    const int* act = si + 2 * R + r0;
-    const int* xidx = si + 3 * R + r0;
-    float* xd = (float*)S.xd.p + (size_t)r0 * d;
-    T* hd = (T*)S.hd.p + prow * d;
-    T* od = (T*)S.od.p + prow * d;
-    T* ffd = (T*)S.ffd.p + prow * 4 * d;
+  // The rows one pass of the decoder layer stack runs on: a decode step's
+  // rows (one position each), or the virtual rows of a prompt prefill (one
+  // per (row, prompt position)).
+  struct LayerRows {
+    int n = 0;
+    const int *tok = nullptr, *pos = nullptr, *act = nullptr, *xidx = nullptr;
+    // prefill: the self-cache row of each virtual row (nullptr: row = its own)
+    const int* crow = nullptr;
+    float* xd = nullptr;
+    T *hd = nullptr, *od = nullptr, *ffd = nullptr;
+    float *Pqkv = nullptr, *Pres = nullptr, *Pq = nullptr;
+    _Float16 *kself = nullptr, *vself = nullptr;  // layer-0 self cache of row 0
+    const int *kvmap = nullptr, *kvown = nullptr;
+    int map_row0 = 0;
+    int xgroup = 1;
+    // prefill: the K/V of every virtual row are appended to the self cache
+    // before the self-attention (a position reads the prompt positions before
+    // it, which other virtual rows of the same launch produce), and the
+    // cross-attention runs in groups of 8 virtual rows of one clip (one K/V
+    // stream per group; every row's arithmetic is the single-row kernel's)
+    bool prefill = false;
+  };
+
+  // embedding + all decoder layers; returns the last FFN2's split-K factor
+  // and bias (folded into the consumer: the final LayerNorm)
+  void run_layers(const LayerRows& rw, hipStream_t s, int& ks_prev, const float*& bias_prev) {
+    const int n = rw.n;
     const float kqs = powf(64.0f, -0.25f);
-    embed<T>(Wt(C.tok_emb), C.dec_pe, tok, pos, act, xd, n, d, s);
+    embed<T>(Wt(C.tok_emb), C.dec_pe, rw.tok, rw.pos, rw.act, rw.xd, n, d, s);
     const size_t layer_self = (size_t)S.row_cap * H * Tctx * 64;
     const size_t layer_cross = (size_t)S.cross_cap * H * hp.n_audio_ctx * 64;  // elements
     const size_t layer_xs = (size_t)S.cross_cap * H * hp.n_audio_ctx * 2;      // kv8 scales
-    // the group's split-K slabs [KS][n][N] live inside the R-row slab buffers
-    float* Pqkv = (float*)S.pqkv.p + (size_t)8 * r0 * 3 * d;
-    float* Pres = (float*)S.pres.p + (size_t)8 * r0 * d;
-    float* Pq = (float*)S.pq.p + (size_t)8 * r0 * d;
+    float* xd = rw.xd;
+    T* hd = rw.hd;
+    T* od = rw.od;
+    T* ffd = rw.ffd;
+    float* Pqkv = rw.Pqkv;
+    float* Pres = rw.Pres;
+    float* Pq = rw.Pq;
+    const int* pos = rw.pos;
+    const int* act = rw.act;
+    const int* xidx = rw.xidx;
+    const int xgroup = rw.xgroup;
     // The d- and 3d-wide projections run as split-K GEMMs writing f32 partial
     // slabs; each consumer (LN: bias + residual, attention: bias/scale/f16 and
     // the KV-cache append) folds the slabs in, so no launch is added.
-    int ks_prev = 0;
-    const float* bias_prev = nullptr;
+    ks_prev = 0;
+    bias_prev = nullptr;
     for (int l = 0; l < L_dec; ++l) {
       const DecLayerW& W = C.dec[l];
-      _Float16* ks = (_Float16*)S.kself.p + l * layer_self + (size_t)r0 * H * Tctx * 64;
-      _Float16* vs = (_Float16*)S.vself.p + l * layer_self + (size_t)r0 * H * Tctx * 64;
+      _Float16* ks = rw.kself + l * layer_self;
+      _Float16* vs = rw.vself + l * layer_self;
       layer_norm_dec<T>(xd, W.ln1_w, W.ln1_b, hd, n, d, act, s, ks_prev ? Pres : nullptr,
                         ks_prev, bias_prev);
       int k1;
       { PerfScope ps(S, "dec_gemm", s);
         k1 = gemm_splitk_partials<T>(hd, Dw(W.qkv), n, 3 * d, d, Pqkv, s); }
+      if (rw.prefill)
+        kv_append<T>(Pqkv, k1, 3 * d, W.qkv_b, kqs, ks, vs, rw.crow, pos, act, Tctx, n, H, s);
       { PerfScope ps(S, "dec_attn_self", s);
-        dec_attention<T>(Pqkv, k1, 3 * d, W.qkv_b, kqs, kqs, ks, vs, nullptr, pos, act, 0, Tctx,
-                         od, n, H, 1.0f, s, (const int*)S.kvmap.p + (size_t)r0 * Tctx,
-                         (const int*)S.kvown.p + r0, r0, xgroup); }
+        dec_attention<T>(Pqkv, k1, 3 * d, W.qkv_b, kqs, kqs, ks, vs, rw.crow, pos, act, 0, Tctx,
+                         od, n, H, 1.0f, s, rw.kvmap, rw.kvown, rw.map_row0,
+                         rw.prefill ? 1 : xgroup); }
       int k2;
       { PerfScope ps(S, "dec_gemm", s);
         k2 = gemm_splitk_partials<T>(od, Dw(W.o), n, d, d, Pres, s); }
@@ -1021,36 +1052,37 @@ struct Driver {
       int k3;
       { PerfScope ps(S, "dec_gemm", s);
         k3 = gemm_splitk_partials<T>(hd, Dw(W.cq), n, d, d, Pq, s); }
-      if (perf_on(S, "event_bracket")) {
+      if (!rw.prefill && perf_on(S, "event_bracket")) {
         // calibration: the same event pair around an empty kernel at the same
         // point of the chain (bench.py subtracts its average from the
         // cross-attention brackets: the two event nodes' own cost)
         PerfScope ps(S, "event_bracket", s);
         launch_perf_empty(s);
       }
-      { PerfScope ps(S, "dec_attn_cross", s);
+      { PerfScope ps(S, rw.prefill ? "prefill_cross" : "dec_attn_cross", s);
         // the decoders of a beam / best-of group share their clip's cross K/V:
         // stream it once per group; an MX-fp8 cache is read by the grouped
         // kernel for any group size
+        const int nq = rw.prefill ? 8 : std::max(1, xgroup);
         if (C.kv8) {
           if (!dec_cross_attention_grouped<T>(
                   Pq, k3, d, W.cq_b, (const uint8_t*)S.cross_k.p + l * layer_cross,
                   (const uint8_t*)S.cross_v.p + l * layer_cross, xidx, act, hp.n_audio_ctx,
-                  hp.n_audio_ctx, od, n, H, kqs, std::max(1, xgroup), s,
+                  hp.n_audio_ctx, od, n, H, kqs, nq, s,
                   (const uint8_t*)S.cross_ks.p + l * layer_xs,
                   (const uint8_t*)S.cross_vs.p + l * layer_xs))
             throw std::runtime_error("mwx: unsupported fp8 cross-attention group");
-        } else if (xgroup < 2 ||
+        } else if (nq < 2 ||
             !dec_cross_attention_grouped<T>(Pq, k3, d, W.cq_b,
                                             (const _Float16*)S.cross_k.p + l * layer_cross,
                                             (const _Float16*)S.cross_v.p + l * layer_cross, xidx,
                                             act, hp.n_audio_ctx, hp.n_audio_ctx, od, n, H, kqs,
-                                            xgroup, s))
+                                            nq, s))
           dec_attention<T>(Pq, k3, d, W.cq_b, 1.0f, 1.0f,
                            (_Float16*)S.cross_k.p + l * layer_cross,
                            (_Float16*)S.cross_v.p + l * layer_cross, xidx, pos, act,
                            hp.n_audio_ctx, hp.n_audio_ctx, od, n, H, kqs, s, nullptr, nullptr, 0,
-                           xgroup); }
+                           nq); }
       int k4;
       { PerfScope ps(S, "dec_gemm", s);
         k4 = gemm_splitk_partials<T>(od, Dw(W.co), n, d, d, Pres, s); }
@@ -1068,6 +1100,118 @@ struct Driver {
       bias_prev = W.fc2_b;
       if (!k1 || !k2 || !k3 || !k4 || !k5 || !ks_prev) throw std::runtime_error("mwx: unsupported split-K shape");
     }
+  }
+
+  // Batched prompt prefill (whisper.cpp decodes a window's prompt in one
+  // whisper_decode call, src/stt_engine.cpp:233 passes initial_prompt and
+  // long-form windows carry prompt_past): positions 0 .. n_i - 1 of row i's
+  // prompt run through the layer stack as virtual rows (one per position)
+  // instead of one decode step each. Only the K / V they leave in the self
+  // cache are kept (no logits: the prompt's last position is the first
+  // sampling step of the decode loop). Every virtual row's arithmetic is a
+  // decode step's for that row and position (row-blocked GEMMs, the same
+  // attention kernels), so the cache holds the same bits as step by step.
+  // Rows in chunks of <= MWX_PREFILL_ROWS virtual rows (default 2048), each
+  // row's positions padded to a multiple of 8 (cross-attention groups).
+  struct PrefillRow {
+    int row;                 // self-cache row
+    int clip;                // cross slot
+    const int* tokens;       // prompt tokens
+    int n;                   // positions to prefill (0 .. n-1)
+  };
+  void prefill(const std::vector<PrefillRow>& prs) {
+    static const int vcap = std::max(64, getenv("MWX_PREFILL_ROWS")
+                                             ? atoi(getenv("MWX_PREFILL_ROWS")) : 2048);
+    int nmax = 0, nrows = 0;
+    for (const auto& r : prs)
+      if (r.n > 0) {
+        nmax = std::max(nmax, r.n);
+        ++nrows;
+      }
+    if (nrows == 0) return;
+    for (const auto& r : prs) S.n_prefill += std::max(0, r.n);
+    // positions per chunk: every row with work gets the same span (x 8)
+    const int span = std::max(8, (vcap / nrows) / 8 * 8);
+    const size_t mcap = (size_t)nrows * std::min(span, (nmax + 7) / 8 * 8);
+    const size_t m64 = (mcap + 63) / 64 * 64;
+    int* din = (int*)S.pf_in.get(mcap * 5 * 4);
+    LayerRows rw;
+    rw.xd = (float*)S.pf_x.get(mcap * d * 4);
+    rw.hd = (T*)S.pf_h.get(m64 * d * sizeof(T), true);
+    rw.od = (T*)S.pf_o.get(m64 * d * sizeof(T), true);
+    rw.ffd = (T*)S.pf_ff.get(m64 * 4 * d * sizeof(T), true);
+    rw.Pqkv = (float*)S.pf_pqkv.get((size_t)8 * mcap * 3 * d * 4);
+    rw.Pres = (float*)S.pf_pres.get((size_t)8 * mcap * d * 4);
+    rw.Pq = (float*)S.pf_pq.get((size_t)8 * mcap * d * 4);
+    rw.kself = (_Float16*)S.kself.p;
+    rw.vself = (_Float16*)S.vself.p;
+    rw.prefill = true;
+    std::vector<std::vector<int>> hin;  // host inputs, alive until the final sync
+    for (int p0 = 0; p0 < nmax; p0 += span) {
+      std::vector<int> tok, pos, act, xidx, crow;
+      for (const auto& r : prs) {
+        const int len = std::min(r.n, p0 + span) - p0;
+        if (len <= 0) continue;
+        const int padded = (len + 7) / 8 * 8;
+        for (int j = 0; j < padded; ++j) {
+          const bool a = j < len;
+          tok.push_back(a ? r.tokens[p0 + j] : 0);
+          pos.push_back(a ? p0 + j : 0);
+          act.push_back(a ? 1 : 0);
+          xidx.push_back(r.clip);
+          crow.push_back(r.row);
+        }
+      }
+      const int M = (int)tok.size();
+      if (M == 0) continue;
+      if ((size_t)M > mcap) throw std::runtime_error("mwx: prefill chunk exceeds its buffers");
+      hin.emplace_back();
+      std::vector<int>& h = hin.back();
+      for (auto* v : {&tok, &pos, &act, &xidx, &crow}) h.insert(h.end(), v->begin(), v->end());
+      HIPC(hipMemcpyAsync(din, h.data(), h.size() * 4, hipMemcpyHostToDevice, st));
+      rw.n = M;
+      rw.tok = din;
+      rw.pos = din + M;
+      rw.act = din + 2 * M;
+      rw.xidx = din + 3 * M;
+      rw.crow = din + 4 * M;
+      int ks_prev = 0;
+      const float* bias_prev = nullptr;
+      run_layers(rw, st, ks_prev, bias_prev);
+    }
+    HIPC(hipStreamSynchronize(st));  // (host inputs / the next chunk's reuse of din)
+  }
+
+  // decoder step for rows [r0, r0+n) of an R-row step, launched on `s`
+  void decode_group(int R, int r0, int n, size_t prow, bool want_probs, hipStream_t s) {
+    int* si = (int*)S.stepin.p;
+    LayerRows rw;
+    rw.n = n;
+    rw.tok = si + r0;
+    rw.pos = si + R + r0;
+    rw.act = si + 2 * R + r0;
+    rw.xidx = si + 3 * R + r0;
+    rw.xd = (float*)S.xd.p + (size_t)r0 * d;
+    rw.hd = (T*)S.hd.p + prow * d;
+    rw.od = (T*)S.od.p + prow * d;
+    rw.ffd = (T*)S.ffd.p + prow * 4 * d;
+    // the group's split-K slabs [KS][n][N] live inside the R-row slab buffers
+    rw.Pqkv = (float*)S.pqkv.p + (size_t)8 * r0 * 3 * d;
+    rw.Pres = (float*)S.pres.p + (size_t)8 * r0 * d;
+    rw.Pq = (float*)S.pq.p + (size_t)8 * r0 * d;
+    rw.kself = (_Float16*)S.kself.p + (size_t)r0 * H * Tctx * 64;
+    rw.vself = (_Float16*)S.vself.p + (size_t)r0 * H * Tctx * 64;
+    rw.kvmap = (const int*)S.kvmap.p + (size_t)r0 * Tctx;
+    rw.kvown = (const int*)S.kvown.p + r0;
+    rw.map_row0 = r0;
+    rw.xgroup = xgroup;
+    const int* act = rw.act;
+    float* xd = rw.xd;
+    T* hd = rw.hd;
+    float* Pres = rw.Pres;
+    int ks_prev = 0;
+    const float* bias_prev = nullptr;
+    run_layers(rw, s, ks_prev, bias_prev);
     layer_norm_dec<T>(xd, C.dec_ln_w, C.dec_ln_b, hd, n, d, act, s, Pres, ks_prev, bias_prev);
     EpiParams e;
     e.c32 = (float*)S.logits.p + (size_t)r0 * V;

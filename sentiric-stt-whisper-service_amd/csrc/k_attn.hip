@@ -904,6 +904,54 @@ template bool dec_cross_attention_grouped<__bf16>(const float*, int, int, const 
                                                   int, hipStream_t, const uint8_t*,
                                                   const uint8_t*);
 
+// Prompt prefill: the self-attention K / V of every (virtual) row appended
+// to its cache row crow[row] at position pos[row] before the self-attention
+// launch of the same layer, so a prompt position can read the positions
+// before it that other rows of the same launch produce. The values are those
+// dec_attn_kernel<T, true> forms for its own position (same slab sum, same
+// roundings), which it also writes again (the same bits).
+__global__ __launch_bounds__(128) void kv_append_kernel(const float* __restrict__ P, int KS,
+                                                       int pcols, const float* __restrict__ bias,
+                                                       float kscale, _Float16* __restrict__ kbase,
+                                                       _Float16* __restrict__ vbase,
+                                                       const int* __restrict__ crow,
+                                                       const int* __restrict__ pos,
+                                                       const int* __restrict__ active, int cap,
+                                                       int R, int H) {
+  const int h = blockIdx.x, row = blockIdx.y;
+  if (!active[row]) return;
+  const int tid = threadIdx.x, part = 1 + (tid >> 6), e = tid & 63;
+  const int D = H * 64;
+  const int col = part * D + h * 64 + e;
+  const long pstride = (long)R * pcols;
+  const float* pp = P + (long)row * pcols + col;
+  float pk[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) pk[k] = pp[min(k, KS - 1) * pstride];
+  float acc = pk[0];
+#pragma unroll
+  for (int k = 1; k < 8; ++k) acc += k < KS ? pk[k] : 0.0f;
+  const long dst = (((long)(crow ? crow[row] : row) * H + h) * cap + pos[row]) * 64 + e;
+  if (part == 1)
+    kbase[dst] = (_Float16)(acc * kscale);
+  else
+    vbase[dst] = (_Float16)(acc + bias[col]);
+}
+
+template <typename T>
+void kv_append(const float* P, int KS, int pcols, const float* bias, float kscale,
+               _Float16* kbase, _Float16* vbase, const int* crow, const int* pos,
+               const int* active, int cap, int R, int H, hipStream_t st) {
+  if (R <= 0) return;
+  kv_append_kernel<<<dim3(H, R), 128, 0, st>>>(P, KS, pcols, bias, kscale, kbase, vbase, crow, pos,
+                                              active, cap, R, H);
+}
+template void kv_append<_Float16>(const float*, int, int, const float*, float, _Float16*,
+                                  _Float16*, const int*, const int*, const int*, int, int, int,
+                                  hipStream_t);
+template void kv_append<__bf16>(const float*, int, int, const float*, float, _Float16*, _Float16*,
+                                const int*, const int*, const int*, int, int, int, hipStream_t);
+
 template <typename T>
 void dec_attention(const float* P, int KS, int pcols, const float* bias, float qscale,
                    float kscale, _Float16* kbase, _Float16* vbase, const int* kv_index,

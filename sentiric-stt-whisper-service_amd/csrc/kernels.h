@@ -182,6 +182,14 @@ void dec_attention(const float* P, int KS, int pcols, const float* bias, float q
                    int H, float scale, hipStream_t st, const int* kvmap = nullptr,
                    const int* own_from = nullptr, int map_row0 = 0, int nq = 1);
 
+// Prompt prefill: K / V of every row (reduced from the QKV slabs exactly as
+// dec_attention's self kernel reduces its own position) appended to cache row
+// crow[row] (nullptr: row) at position pos[row].
+template <typename T>
+void kv_append(const float* P, int KS, int pcols, const float* bias, float kscale,
+               _Float16* kbase, _Float16* vbase, const int* crow, const int* pos,
+               const int* active, int cap, int R, int H, hipStream_t st);
+
 // Cross-attention for groups of nq consecutive rows that share one cross
 // slot (beam-search / best-of decoders of a clip; kv_index[row] equal within a
 // group): K/V of the slot are streamed once per group. Same per-row results as

@@ -196,6 +196,8 @@ def lib() -> C.CDLL:
     L.mwx_test_decode.argtypes = [P, P, C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_float)]
     L.mwx_test_decode_last.restype = C.c_int
     L.mwx_test_decode_last.argtypes = [P, P, C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_float)]
+    L.mwx_test_decode_counters.restype = C.c_int
+    L.mwx_test_decode_counters.argtypes = [P, C.POINTER(C.c_long), C.POINTER(C.c_long), C.c_int]
     L.mwx_test_sample_draws.restype = C.c_int
     L.mwx_test_sample_draws.argtypes = [P, fpp, fpp, C.c_int, C.c_int, C.POINTER(C.c_double),
                                         C.POINTER(C.c_int), C.c_int, C.c_int, C.c_int,
@@ -533,6 +535,14 @@ class Context:
         if r != 0:
             raise RuntimeError(f"mwx_test_decode returned {r}")
         return out
+
+    def decode_counters(self, state_index: int = 0, reset: bool = True):
+        """(decode steps launched, prompt positions prefilled) on a state since
+        the last reset (mwx_test_decode_counters)."""
+        st, pf = C.c_long(), C.c_long()
+        lib().mwx_test_decode_counters(self.state(state_index), C.byref(st), C.byref(pf),
+                                       1 if reset else 0)
+        return st.value, pf.value
 
     def test_decode_last(self, tokens: Sequence[int], out: Optional[np.ndarray] = None,
                          state_index: int = 0) -> np.ndarray:

@@ -113,4 +113,7 @@ def test_v3_geometry_plain_weights_greedy_matches_oracle(make_model):
             print(f"plain large-v3-l2 clip {k}: {len(oids)} tokens in {len(windows)} window(s), "
                   f"oracle top-1 margin min {m.min():.4f} median {np.median(m):.4f}")
             assert len(oids) > 10
-            assert_same(segs, osegs, p_tol=3e-2, tid_tie_tol=2e-3)
+            # (plain weights carry no timestamp signal: the timestamp argmax
+            # behind the diagnostic `tid` field is a tie within bf16 noise —
+            # seen: pt 0.3441 / 0.3416 on the same text token, equal t0 / t1)
+            assert_same(segs, osegs, p_tol=3e-2, tid_tie_tol=1e-2)
