@@ -189,12 +189,27 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
   // over the 8 XCDs (id % 8), so consecutive tile ids -- the column tiles of
   // one row tile, sharing its A rows -- are given to workgroups of one XCD
   // and the A tile is fetched into that XCD's L2 once
+  //
+  // Grouped order (P.group_m = G > 0, the default): the logical tile ids of
+  // that contiguous range walk G row tiles before moving to the next column
+  // tile, so the ~32 workgroups an XCD runs at once cover G row tiles x 32/G
+  // column tiles and share both operand tiles in its 4-MiB L2 (row-major:
+  // 1-2 row tiles x every column tile, whose W slices miss L2 once per row
+  // tile: the all-layer cross-K/V GEMM re-read its 210-MB W ~188 times).
   int wgid = blockIdx.x;
   if (P.xcd_remap) {
     const int nwg = gridDim.x, xcd = wgid % 8, q = nwg / 8, r = nwg % 8;
     wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + wgid / 8;
   }
-  const int m0 = (wgid / nbn) * BM, n0 = (wgid % nbn) * BN;
+  int mt = wgid / nbn, nt = wgid % nbn;
+  if (P.group_m > 0) {
+    const int nbm = (M + BM - 1) / BM;
+    const int per = P.group_m * nbn, g = wgid / per, i = wgid - g * per;
+    const int gm = min(P.group_m, nbm - g * P.group_m);
+    mt = g * P.group_m + i % gm;
+    nt = i / gm;
+  }
+  const int m0 = mt * BM, n0 = nt * BN;
   const int bz = blockIdx.y;
   A += (long)bz * a_bstride;
   // LDS DMA: one wave instruction fills 1 KB = 8 rows x 128 B of the tile
@@ -791,6 +806,11 @@ static bool xcd_remap_enabled() {
   static const bool on = getenv("MWX_NO_XCD_REMAP") == nullptr;
   return on;
 }
+// row tiles per group of the grouped tile order (MWX_GEMM_GROUP; 0 = row-major)
+static int gemm_group_m() {
+  static const int g = getenv("MWX_GEMM_GROUP") ? std::max(0, atoi(getenv("MWX_GEMM_GROUP"))) : 8;
+  return g;
+}
 
 template <typename T, int EPI, bool OUT16>
 static void gemm_dispatch(const T* A, long lda, long a_bstride, const T* W, long ldw, int M,
@@ -798,9 +818,11 @@ static void gemm_dispatch(const T* A, long lda, long a_bstride, const T* W, long
   if (K % BK) throw std::runtime_error("mwx: gemm K must be a multiple of 64");
   dim3 g(((N + BN - 1) / BN) * ((M + BM - 1) / BM), batch);
   EpiParams P = P0;
-  // (measured: -3..-5% on the encoder GEMMs, +5% on the all-layer cross K/V
-  // GEMM whose 320 column tiles stream 210 MB of weights per row tile)
-  P.xcd_remap = xcd_remap_enabled() && EPI != EPI_CROSS_KV;
+  // (row-major order measured: XCD remap -3..-5% on the encoder GEMMs, +5%
+  // on the all-layer cross K/V GEMM whose 320 column tiles stream 210 MB of
+  // weights per row tile; with the grouped order both take the remap)
+  P.group_m = gemm_group_m();
+  P.xcd_remap = xcd_remap_enabled() && (EPI != EPI_CROSS_KV || P.group_m > 0);
   gemm_big<T, EPI, OUT16><<<g, 512, 0, st>>>(A, lda, a_bstride, W, ldw, M, N, K, P);
 }
 
@@ -810,7 +832,8 @@ void gemm_mx(int epi, const uint8_t* A, long lda, long a_bstride, const uint8_t*
   if (K % 128) throw std::runtime_error("mwx: MX-fp8 gemm K must be a multiple of 128");
   dim3 g(((N + BN - 1) / BN) * ((M + BM - 1) / BM), batch);
   EpiParams P = P0;
-  P.xcd_remap = xcd_remap_enabled() && epi != EPI_CROSS_KV;
+  P.group_m = gemm_group_m();
+  P.xcd_remap = xcd_remap_enabled() && (epi != EPI_CROSS_KV || P.group_m > 0);
 #define MXL(E) gemm_big<T, E, false, true><<<g, 512, 0, st>>>(A, lda, a_bstride, W, ldw, M, N, K, P)
   switch (epi) {
     case EPI_ENC_QKV: MXL(EPI_ENC_QKV); break;

@@ -47,6 +47,7 @@ struct EpiParams {
   long sa_bstride = 0;
   const uint8_t* sw = nullptr;
   bool xcd_remap = true;  // gemm_big: XCD-aware tile order
+  int group_m = 0;        // gemm_big: row tiles per group of the grouped tile order (0: row-major)
   int mt = 0;             // gemm_decode: rows per block = 16 * mt (0: the default rule)
   // EPI_CROSS_KV with an MX-fp8 cache: k / v hold e4m3 codes, ks8 / vs8 the
   // E8M0 scales (two per (time, head) row of 64)
