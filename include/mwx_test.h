@@ -31,6 +31,15 @@ int mwx_test_encode(struct mwx_context* ctx, struct mwx_state* state, const floa
 int mwx_test_decode(struct mwx_context* ctx, struct mwx_state* state, const int* tokens, int n,
                     float* logits_out);
 
+/* As mwx_test_decode_last, with tokens 0 .. n-2 run by the batched prompt
+ * prefill (one pass of the layer stack) and only token n-1 as a decode step. */
+int mwx_test_decode_last_prefill(struct mwx_context* ctx, struct mwx_state* state,
+                                 const int* tokens, int n, float* logits_last);
+
+/* Self-attention K / V cache of row 0 of a state for one decoder layer,
+ * positions 0 .. n_pos-1, as f32 [n_pos][n_text_head][64] each. */
+int mwx_test_self_kv(struct mwx_state* state, int layer, int n_pos, float* k_out, float* v_out);
+
 /* Decode work counters of a state (the first state of a batch drives it):
  * decode steps launched and prompt positions run by the batched prompt
  * prefill since the last reset. reset != 0 zeroes them after reading. */

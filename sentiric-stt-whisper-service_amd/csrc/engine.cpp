@@ -1039,12 +1039,14 @@ struct Driver {
       int k1;
       { PerfScope ps(S, "dec_gemm", s);
         k1 = gemm_splitk_partials<T>(hd, Dw(W.qkv), n, 3 * d, d, Pqkv, s); }
+      static const int pf_selfwrite =
+          getenv("MWX_PREFILL_SELFWRITE") ? atoi(getenv("MWX_PREFILL_SELFWRITE")) : 0;
       if (rw.prefill)
         kv_append<T>(Pqkv, k1, 3 * d, W.qkv_b, kqs, ks, vs, rw.crow, pos, act, Tctx, n, H, s);
       { PerfScope ps(S, "dec_attn_self", s);
         dec_attention<T>(Pqkv, k1, 3 * d, W.qkv_b, kqs, kqs, ks, vs, rw.crow, pos, act, 0, Tctx,
                          od, n, H, 1.0f, s, rw.kvmap, rw.kvown, rw.map_row0,
-                         rw.prefill ? 1 : xgroup); }
+                         rw.prefill ? 1 : xgroup, pf_selfwrite || !rw.prefill); }
       int k2;
       { PerfScope ps(S, "dec_gemm", s);
         k2 = gemm_splitk_partials<T>(od, Dw(W.o), n, d, d, Pres, s); }
@@ -1063,7 +1065,9 @@ struct Driver {
         // the decoders of a beam / best-of group share their clip's cross K/V:
         // stream it once per group; an MX-fp8 cache is read by the grouped
         // kernel for any group size
-        const int nq = rw.prefill ? 8 : std::max(1, xgroup);
+        static const int pf_xnq =
+            getenv("MWX_PREFILL_XNQ") ? std::max(1, atoi(getenv("MWX_PREFILL_XNQ"))) : 8;
+        const int nq = rw.prefill ? pf_xnq : std::max(1, xgroup);
         if (C.kv8) {
           if (!dec_cross_attention_grouped<T>(
                   Pq, k3, d, W.cq_b, (const uint8_t*)S.cross_k.p + l * layer_cross,
@@ -1131,8 +1135,9 @@ struct Driver {
     if (nrows == 0) return;
     for (const auto& r : prs) S.n_prefill += std::max(0, r.n);
     // positions per chunk: every row with work gets the same span (x 8)
-    const int span = std::max(8, (vcap / nrows) / 8 * 8);
-    const size_t mcap = (size_t)nrows * std::min(span, (nmax + 7) / 8 * 8);
+    static const int span_env = getenv("MWX_PREFILL_SPAN") ? atoi(getenv("MWX_PREFILL_SPAN")) : 0;
+    const int span = span_env > 0 ? span_env : std::max(8, (vcap / nrows) / 8 * 8);
+    const size_t mcap = (size_t)nrows * ((std::min(span, nmax) + 7) / 8 * 8);
     const size_t m64 = (mcap + 63) / 64 * 64;
     int* din = (int*)S.pf_in.get(mcap * 5 * 4);
     LayerRows rw;

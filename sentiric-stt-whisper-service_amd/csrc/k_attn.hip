@@ -285,7 +285,7 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
     const int* __restrict__ kv_index, const int* __restrict__ pos, const int* __restrict__ active,
     int fixed_len, int cap, T* __restrict__ o, int H, float scale,
     const int* __restrict__ kvmap, const int* __restrict__ own_from, int map_row0, int nq,
-    int R) {
+    int R, int write_new = 1) {
   __shared__ float sc[DEC_MAX_KEYS];
   __shared__ float redf[4];
   __shared__ double redd[4];
@@ -393,15 +393,15 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
 #pragma unroll
     for (int k = 1; k < 8; ++k) acc += k < KS ? pk[k] : 0.0f;
     if (part == 0) {
-      sq[e] = (float)(_Float16)((acc + bcol) * qscale);
+      sq[e] = (float)f16r((acc + bcol) * qscale);
     } else if (part == 1) {
-      const _Float16 kv = (_Float16)(acc * kscale);
+      const _Float16 kv = f16r(acc * kscale);
       snk[e] = (float)kv;
-      K[(long)p_row * 64 + e] = kv;
+      if (write_new) K[(long)p_row * 64 + e] = kv;
     } else {
-      const _Float16 vv = (_Float16)(acc + bcol);
+      const _Float16 vv = f16r(acc + bcol);
       snv[e] = (float)vv;
-      V[(long)p_row * 64 + e] = vv;
+      if (write_new) V[(long)p_row * 64 + e] = vv;
     }
   }
   __syncthreads();
@@ -444,7 +444,7 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
     }
     sum = block_sum_256d(sum, redd);
     const float inv = (float)(1.0 / sum);
-    for (int j = tid; j < n; j += 256) sc[j] = (float)(_Float16)(sc[j] * inv);
+    for (int j = tid; j < n; j += 256) sc[j] = (float)f16r(sc[j] * inv);
     __syncthreads();
   };
   float acc[8];
@@ -668,7 +668,7 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
       float acc = pq[i][0];
 #pragma unroll
       for (int k = 1; k < 8; ++k) acc += k < KS ? pq[i][k] : 0.0f;
-      sq[q][e] = (float)(_Float16)(acc + bq);  // (e == tid & 63)
+      sq[q][e] = (float)f16r(acc + bq);  // (e == tid & 63)
     }
   }
   __syncthreads();
@@ -766,7 +766,7 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
   for (int q = 0; q < NQ; ++q) {
     const double t = (redd[0][q] + redd[1][q]) + (redd[2][q] + redd[3][q]);
     const float inv = (float)(1.0 / t);
-    for (int j = tid; j < n; j += 256) sc[q][j] = (float)(_Float16)(sc[q][j] * inv);
+    for (int j = tid; j < n; j += 256) sc[q][j] = (float)f16r(sc[q][j] * inv);
   }
   __syncthreads();
   float acc[NQ][8];
@@ -933,9 +933,9 @@ __global__ __launch_bounds__(128) void kv_append_kernel(const float* __restrict_
   for (int k = 1; k < 8; ++k) acc += k < KS ? pk[k] : 0.0f;
   const long dst = (((long)(crow ? crow[row] : row) * H + h) * cap + pos[row]) * 64 + e;
   if (part == 1)
-    kbase[dst] = (_Float16)(acc * kscale);
+    kbase[dst] = f16r(acc * kscale);
   else
-    vbase[dst] = (_Float16)(acc + bias[col]);
+    vbase[dst] = f16r(acc + bias[col]);
 }
 
 template <typename T>
@@ -957,7 +957,7 @@ void dec_attention(const float* P, int KS, int pcols, const float* bias, float q
                    float kscale, _Float16* kbase, _Float16* vbase, const int* kv_index,
                    const int* pos, const int* active, int fixed_len, int kv_len_cap, T* o, int R,
                    int H, float scale, hipStream_t st, const int* kvmap, const int* own_from,
-                   int map_row0, int nq) {
+                   int map_row0, int nq, int write_new) {
   dim3 g(H, R);
   if (nq > 1 && R % nq == 0) {
     const int groups = (R / nq) * H;
@@ -978,11 +978,12 @@ void dec_attention(const float* P, int KS, int pcols, const float* bias, float q
     dec_attn_kernel<T, true, 4><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale, kbase,
                                                    vbase, kv_index, pos, active, fixed_len,
                                                    kv_len_cap, o, H, scale, kvmap, own_from,
-                                                   map_row0, nq, R);
+                                                   map_row0, nq, R, write_new);
   else if (fixed_len == 0)
     dec_attn_kernel<T, true><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale, kbase, vbase,
                                                 kv_index, pos, active, fixed_len, kv_len_cap, o,
-                                                H, scale, kvmap, own_from, map_row0, nq, R);
+                                                H, scale, kvmap, own_from, map_row0, nq, R,
+                                                write_new);
   else if (xattn_nt && fixed_len == 1500 && xattn_nbc)  // (every Whisper model: 1500 frames)
     dec_attn_kernel<T, false, 8, true, 6><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale,
                                                              kbase, vbase, kv_index, pos, active,
@@ -1007,9 +1008,10 @@ template void enc_attention<__bf16>(const _Float16*, const _Float16*, const _Flo
 template void dec_attention<_Float16>(const float*, int, int, const float*, float, float,
                                       _Float16*, _Float16*, const int*, const int*, const int*, int,
                                       int, _Float16*, int, int, float, hipStream_t, const int*,
-                                      const int*, int, int);
+                                      const int*, int, int, int);
 template void dec_attention<__bf16>(const float*, int, int, const float*, float, float, _Float16*,
                                     _Float16*, const int*, const int*, const int*, int, int,
-                                    __bf16*, int, int, float, hipStream_t, const int*, const int*, int, int);
+                                    __bf16*, int, int, float, hipStream_t, const int*, const int*, int, int,
+                                    int);
 
 }  // namespace mwx

@@ -35,7 +35,7 @@ __device__ __forceinline__ void epi_store(const EpiParams& P, int bz, int m, int
     const int nn = n - part * d;
     const int h = nn >> 6, e = nn & 63;
     const int b = m / P.L, t = m - b * P.L;
-    const _Float16 hv = (_Float16)(acc + P.bias[n]);
+    const _Float16 hv = f16r(acc + P.bias[n]);
     if (part == 0)
       P.q[(((long)b * P.H + h) * P.L + t) * 64 + e] = hv;
     else if (part == 1)
@@ -70,9 +70,9 @@ __device__ __forceinline__ void epi_store(const EpiParams& P, int bz, int m, int
     const int bl = m / P.L, t = m - bl * P.L;
     const long idx = ((((long)layer * P.ncap + P.slot[bl]) * P.H + h) * P.L + t) * 64 + e;
     if (!kv)
-      P.k[idx] = (_Float16)(acc * P.kscale);
+      P.k[idx] = f16r(acc * P.kscale);
     else
-      P.v[idx] = (_Float16)(acc + P.bias[n]);
+      P.v[idx] = f16r(acc + P.bias[n]);
   } else if constexpr (EPI == EPI_DEC_QKV) {
     if (!P.active[m]) return;
     const int d = P.d;
@@ -80,16 +80,16 @@ __device__ __forceinline__ void epi_store(const EpiParams& P, int bz, int m, int
     const int nn = n - part * d;
     const int h = nn >> 6, e = nn & 63;
     if (part == 0) {
-      P.q[(long)m * d + nn] = (_Float16)((acc + P.bias[n]) * P.qscale);
+      P.q[(long)m * d + nn] = f16r((acc + P.bias[n]) * P.qscale);
     } else {
       const long idx = (((long)m * P.H + h) * P.L + P.pos[m]) * 64 + e;
       if (part == 1)
-        P.k[idx] = (_Float16)(acc * P.kscale);
+        P.k[idx] = f16r(acc * P.kscale);
       else
-        P.v[idx] = (_Float16)(acc + P.bias[n]);
+        P.v[idx] = f16r(acc + P.bias[n]);
     }
   } else if constexpr (EPI == EPI_STORE16) {
-    ((_Float16*)P.c16)[(long)m * P.ldc + n] = (_Float16)(acc + P.bias[n]);
+    ((_Float16*)P.c16)[(long)m * P.ldc + n] = f16r(acc + P.bias[n]);
   }
 }
 
@@ -399,10 +399,10 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
                 bits = __builtin_bit_cast(uint16_t, tv);
               }
             } else if constexpr (EPI == EPI_ENC_QKV) {
-              const _Float16 hv = (_Float16)(a + P.bias[n]);
+              const _Float16 hv = f16r(a + P.bias[n]);
               bits = __builtin_bit_cast(uint16_t, hv);
             } else {  // cross K: f16(acc * kscale); V: f16(acc + b)
-              const _Float16 hv = part ? (_Float16)(a + P.bias[n]) : (_Float16)(a * P.kscale);
+              const _Float16 hv = part ? f16r(a + P.bias[n]) : f16r(a * P.kscale);
               bits = __builtin_bit_cast(uint16_t, hv);
             }
             wl[transposed ? lc * 128 + lr : lr * 64 + lc] = bits;

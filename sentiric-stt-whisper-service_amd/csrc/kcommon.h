@@ -44,8 +44,19 @@ struct Elt<__bf16> {
   }
 };
 
+// f32 -> f16 of a value computed in f32. ggml stores the f32 result and then
+// converts it (two roundings: the f32 op, then f16). The empty asm keeps the
+// value materialised as f32, so the compiler cannot fuse the producing
+// multiply / add into v_fma_mix{lo,hi}_f16, which rounds a*b(+c) to f16 once
+// (it does so even with -ffp-contract=off; seen on the decode K scaling and
+// the softmax's P).
+__device__ __forceinline__ _Float16 f16r(float x) {
+  asm volatile("" : "+v"(x));
+  return (_Float16)x;
+}
 template <typename T>
 __device__ __forceinline__ T to_t(float x) {
+  asm volatile("" : "+v"(x));  // (as f16r)
   return (T)x;  // v_cvt_f16_f32 / v_cvt_pk_bf16_f32: round to nearest even
 }
 template <typename T>
@@ -64,8 +75,8 @@ __device__ __forceinline__ float gelu_f32(float x) {
 __device__ __forceinline__ float gelu_ggml(float x) {
   if (x <= -10.0f) return 0.0f;
   if (x >= 10.0f) return x;
-  const float xh = (float)(_Float16)x;
-  return (float)(_Float16)gelu_f32(xh);
+  const float xh = (float)f16r(x);
+  return (float)f16r(gelu_f32(xh));
 }
 
 // OCP MX-fp8 block rule (k_mx.hip, the cross K/V cache epilogue; host:

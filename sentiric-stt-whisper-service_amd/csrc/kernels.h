@@ -181,7 +181,8 @@ void dec_attention(const float* P, int KS, int pcols, const float* bias, float q
                    float kscale, _Float16* kbase, _Float16* vbase, const int* kv_index,
                    const int* pos, const int* active, int fixed_len, int kv_len_cap, T* o, int R,
                    int H, float scale, hipStream_t st, const int* kvmap = nullptr,
-                   const int* own_from = nullptr, int map_row0 = 0, int nq = 1);
+                   const int* own_from = nullptr, int map_row0 = 0, int nq = 1,
+                   int write_new = 1);
 
 // Prompt prefill: K / V of every row (reduced from the QKV slabs exactly as
 // dec_attention's self kernel reduces its own position) appended to cache row

@@ -196,6 +196,11 @@ def lib() -> C.CDLL:
     L.mwx_test_decode.argtypes = [P, P, C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_float)]
     L.mwx_test_decode_last.restype = C.c_int
     L.mwx_test_decode_last.argtypes = [P, P, C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_float)]
+    L.mwx_test_decode_last_prefill.restype = C.c_int
+    L.mwx_test_decode_last_prefill.argtypes = [P, P, C.POINTER(C.c_int), C.c_int,
+                                               C.POINTER(C.c_float)]
+    L.mwx_test_self_kv.restype = C.c_int
+    L.mwx_test_self_kv.argtypes = [P, C.c_int, C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_float)]
     L.mwx_test_decode_counters.restype = C.c_int
     L.mwx_test_decode_counters.argtypes = [P, C.POINTER(C.c_long), C.POINTER(C.c_long), C.c_int]
     L.mwx_test_sample_draws.restype = C.c_int
@@ -553,6 +558,27 @@ class Context:
                                        toks.ctypes.data_as(C.POINTER(C.c_int)), len(toks), fptr(out))
         if r != 0:
             raise RuntimeError(f"mwx_test_decode_last returned {r}")
+        return out
+
+    def test_self_kv(self, layer: int, n_pos: int, state_index: int = 0):
+        """(K, V) of row 0's self-attention cache, layer `layer`, positions < n_pos."""
+        H = self.d // 64
+        k = np.empty((n_pos, H, 64), np.float32)
+        v = np.empty_like(k)
+        r = lib().mwx_test_self_kv(self.state(state_index), layer, n_pos, fptr(k), fptr(v))
+        if r != 0:
+            raise RuntimeError(f"mwx_test_self_kv returned {r}")
+        return k, v
+
+    def test_decode_last_prefill(self, tokens: Sequence[int], state_index: int = 0) -> np.ndarray:
+        """test_decode_last with tokens[:-1] through the batched prompt prefill."""
+        toks = np.ascontiguousarray(tokens, dtype=np.int32)
+        out = np.empty(self.hparam("n_vocab"), dtype=np.float32)
+        r = lib().mwx_test_decode_last_prefill(self.ctx, self.state(state_index),
+                                               toks.ctypes.data_as(C.POINTER(C.c_int)), len(toks),
+                                               fptr(out))
+        if r != 0:
+            raise RuntimeError(f"mwx_test_decode_last_prefill returned {r}")
         return out
 
     @property

@@ -62,6 +62,26 @@ def run(path, beam, inc, secs, prompt, prefill_min):
     return json.loads(r.stdout.strip().splitlines()[-1])
 
 
+@pytest.mark.parametrize("arch,wtype", [("micro", mwx.GGML_F16), ("tiny.en", mwx.GGML_F16),
+                                        ("large-v3-l2", mwx.GGML_BF16)])
+def test_prefill_logits_equal_stepwise(make_model, arch, wtype):
+    """Teacher-forced: tokens 0 .. n-2 through the prefill (one pass, virtual
+    rows in 16- / 32-row GEMM blocks, cross-attention in groups of 8) and the
+    last as a decode step give the stepwise logits bit for bit, for prompts
+    of 2 .. 226 positions (chunks of up to MWX_PREFILL_ROWS rows)."""
+    path = make_model(arch, wtype)
+    import numpy as np
+    with mwx.Context.open(path) as ctx:
+        ctx.test_encode(pcm_clip(1), cross=False, state_index=0)
+        ctx.test_encode(pcm_clip(1), cross=False, state_index=1)
+        rng = np.random.default_rng(7)
+        for n in (3, 9, 70, 226):
+            toks = [int(t) for t in rng.integers(0, 50000, n)]
+            a = ctx.test_decode_last(toks, state_index=0)
+            b = ctx.test_decode_last_prefill(toks, state_index=1)
+            assert np.array_equal(a, b), (n, np.abs(a - b).max())
+
+
 @pytest.mark.parametrize("arch,wtype,beam,inc", [
     ("micro-rich", mwx.GGML_F16, 1, 0.2),
     ("large-v3-l2-rich", mwx.GGML_BF16, 1, 0.0),
