@@ -124,7 +124,9 @@ def test_prefill_long_form_initial_prompt_matches_oracle(make_model, arch, wtype
     opt.initial_prompt = PROMPT.decode()
     _, osegs, _, windows = orc.Oracle(path).full(pcm, opt)
     assert len(windows) >= 2 and len(segs) >= 2
-    assert_same(segs, osegs, p_tol=2e-2)
+    # (bf16 at v3 geometry: the diagnostic `tid` of a text token can be a
+    # timestamp tie within rounding noise, seen pt 0.4272 / 0.4253)
+    assert_same(segs, osegs, p_tol=2e-2, tid_tie_tol=5e-3)
     n_tok = sum(len(w) for w in windows)
     # every window's decode loop starts at the prompt's last position: steps
     # = sampled tokens (+ the stop step and at most one run-ahead step per
