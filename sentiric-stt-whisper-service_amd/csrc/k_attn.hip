@@ -847,6 +847,213 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
   }
 }
 
+// MX-fp8 cross K/V cache, NQ rows of one clip (dec_xattn_kernel's KV8 path
+// restructured for memory-level parallelism): an fp8 row is half the bytes of
+// an f16 row, so a lane takes whole 256-row batches (8 rows, 64 B) instead of
+// half batches, and the K batches then the V batches form one stream with two
+// batches in flight (round 2's half-batch stream kept ~2 KB per wave in
+// flight: 60 us for 127.5 MB at 32 clips x 5 rows, 0.27 of HBM). Every row's
+// arithmetic is dec_xattn_kernel's: the same rows per lane, the same widening
+// (v_cvt_scalef32_pk_f16_fp8), scores, softmax order and P.V pairs.
+template <typename T, int NQ>
+__global__ __launch_bounds__(256) void dec_xattn8_kernel(
+    const float* __restrict__ P, int KS, int pcols, const float* __restrict__ bias,
+    const uint8_t* __restrict__ kbase, const uint8_t* __restrict__ vbase,
+    const uint8_t* __restrict__ kscale8, const uint8_t* __restrict__ vscale8,
+    const int* __restrict__ kv_index, const int* __restrict__ active, int n, int cap, int R,
+    T* __restrict__ o, int H, float scale) {
+  __shared__ float sc[NQ][DEC_MAX_KEYS];
+  __shared__ float redf[4][NQ];
+  __shared__ double redd[4][NQ];
+  __shared__ float pv[4][64][9];
+  __shared__ float sq[NQ][64];
+  const int g = blockIdx.y, h = blockIdx.x, row0 = g * NQ;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int kg = lane >> 3, c = lane & 7;
+  bool act[NQ];
+  bool any = false;
+  const int slot = kv_index ? kv_index[row0] : row0;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    act[q] = row0 + q < R && active[min(row0 + q, R - 1)];
+    any |= act[q];
+  }
+  asm volatile("" ::"s"(slot));
+  if (!any) return;
+  const int D = H * 64;
+  const long rbase = ((long)slot * H + h) * cap;
+  const uint8_t* K8 = kbase + rbase * 64;
+  const uint8_t* V8 = vbase + rbase * 64;
+  const uint8_t* KS8 = kscale8 + rbase * 2;
+  const uint8_t* VS8 = vscale8 + rbase * 2;
+  const int nb = (n + 255) >> 8;
+  const int jmax = n - 1;
+  // stream position t: K batch t (t < nb), then V batch t - nb
+  auto load = [&](uint2 (&qb)[8], uint32_t& sr, int t) {
+    const bool isv = t >= nb;
+    const int b = isv ? t - nb : t;
+    const uint8_t* base = isv ? V8 : K8;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = min(b * 256 + wid * 64 + u * 8 + kg, jmax);
+      const u32x2 q2 = ld_stream<true>(reinterpret_cast<const u32x2*>(base + (long)j * 64 + c * 8));
+      qb[u] = uint2{q2[0], q2[1]};
+    }
+    sr = *reinterpret_cast<const uint16_t*>((isv ? VS8 : KS8) +
+                                           (long)min(b * 256 + wid * 64 + lane, jmax) * 2);
+  };
+  auto widen = [&](const uint2 (&qb)[8], uint32_t sr, int u) {
+    const uint32_t pr = (uint32_t)__shfl((int)sr, u * 8 + kg, 64);
+    return dequant_h8(qb[u], (pr >> (8 * (c >> 2))) & 0xffu);
+  };
+  // queries (as dec_xattn_kernel): slab loads first, then the first batches
+  const long pstride = (long)R * pcols;
+  constexpr int QI = (NQ * 64 + 255) / 256;
+  float pq[QI][8];
+#pragma unroll
+  for (int i = 0; i < QI; ++i) {
+    const int t = tid + 256 * i;
+    const int q = min(t >> 6, NQ - 1), e = t & 63;
+    const float* pp = P + (long)min(row0 + q, R - 1) * pcols + h * 64 + e;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) pq[i][k] = pp[min(k, KS - 1) * pstride];
+  }
+  const float bq = bias[h * 64 + (tid & 63)];
+  uint2 qa[8], qb[8];
+  uint32_t sa = 0, sb = 0;
+  load(qa, sa, 0);
+  if (1 < 2 * nb) load(qb, sb, 1);
+#pragma unroll
+  for (int i = 0; i < QI; ++i) {
+    const int t = tid + 256 * i;
+    if (t < NQ * 64) {
+      const int q = t >> 6, e = t & 63;
+      float acc = pq[i][0];
+#pragma unroll
+      for (int k = 1; k < 8; ++k) acc += k < KS ? pq[i][k] : 0.0f;
+      sq[q][e] = (float)f16r(acc + bq);
+    }
+  }
+  __syncthreads();
+  h2 qh[NQ][4];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      qh[q][e] = h2{(_Float16)sq[q][c * 8 + 2 * e], (_Float16)sq[q][c * 8 + 2 * e + 1]};
+  float acc[NQ][8];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[q][e] = 0.0f;
+  auto score = [&](const uint2 (&qbuf)[8], uint32_t sr, int b) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const f16x8 kk = widen(qbuf, sr, u);
+      const int j = b * 256 + wid * 64 + u * 8 + kg;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        float d = dot8(qh[q], kk);
+        d = dpp_sum8(d);
+        if (c == 0 && j < n) sc[q][j] = d * scale;
+      }
+    }
+  };
+  auto softmax = [&]() {
+    __syncthreads();
+    float mx[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      float m = -INFINITY;
+      for (int j = tid; j < n; j += 256) m = fmaxf(m, sc[q][j]);
+      mx[q] = wave_max_dpp(m);
+    }
+    if (lane == 0)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) redf[wid][q] = mx[q];
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+      mx[q] = fmaxf(fmaxf(redf[0][q], redf[1][q]), fmaxf(redf[2][q], redf[3][q]));
+    double sum[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      double sm = 0.0;
+      for (int j = tid; j < n; j += 256) {
+        const float e = expf(sc[q][j] - mx[q]);
+        sc[q][j] = e;
+        sm += (double)e;
+      }
+      sum[q] = wave_sum_d_dpp(sm);
+    }
+    if (lane == 0)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) redd[wid][q] = sum[q];
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const double t = (redd[0][q] + redd[1][q]) + (redd[2][q] + redd[3][q]);
+      const float inv = (float)(1.0 / t);
+      for (int j = tid; j < n; j += 256) sc[q][j] = (float)f16r(sc[q][j] * inv);
+    }
+    __syncthreads();
+  };
+  auto pvb = [&](const uint2 (&qbuf)[8], uint32_t sr, int b) {
+#pragma unroll
+    for (int u = 0; u < 8; u += 2) {  // row pairs (u, u+1) as in dec_attn_kernel
+      const f16x8 v0 = widen(qbuf, sr, u), v1 = widen(qbuf, sr, u + 1);
+      const int j0 = b * 256 + wid * 64 + u * 8 + kg, j1 = j0 + 8;
+      h2 vp[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) vp[e] = h2{v0[e], v1[e]};
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        float p0 = sc[q][min(j0, n - 1)], p1 = sc[q][min(j1, n - 1)];
+        if (j0 >= n) p0 = 0.0f;
+        if (j1 >= n) p1 = 0.0f;
+        const h2 ph = h2{(_Float16)p0, (_Float16)p1};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[q][e] = __builtin_amdgcn_fdot2(ph, vp[e], acc[q][e], false);
+      }
+    }
+  };
+  auto step = [&](uint2 (&qbuf)[8], uint32_t& sr, int t) {
+    if (t == nb) softmax();  // every K batch is scored
+    if (t < nb)
+      score(qbuf, sr, t);
+    else
+      pvb(qbuf, sr, t - nb);
+    if (t + 2 < 2 * nb) load(qbuf, sr, t + 2);
+  };
+#pragma unroll 1
+  for (int t = 0; t < 2 * nb; t += 2) {
+    step(qa, sa, t);
+    if (t + 1 < 2 * nb) step(qb, sb, t + 1);
+  }
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float a = acc[q][e];
+      a += __shfl_xor(a, 8, 64);
+      a += __shfl_xor(a, 16, 64);
+      a += __shfl_xor(a, 32, 64);
+      acc[q][e] = a;
+    }
+    if (kg == 0) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) pv[wid][c][e] = acc[q][e];
+    }
+    __syncthreads();
+    if (tid < 64 && act[q]) {
+      const int cc = tid >> 3, e = tid & 7;
+      const float r = (pv[0][cc][e] + pv[1][cc][e]) + (pv[2][cc][e] + pv[3][cc][e]);
+      o[pack_index(row0 + q, h * 64 + cc * 8 + e, D)] = to_t<T>(r);
+    }
+    __syncthreads();
+  }
+}
+
 template <typename T>
 bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float* bias,
                                  const void* kbase, const void* vbase, const int* kv_index,
@@ -875,6 +1082,23 @@ bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float*
                                                         kscale8, vscale8, kv_index, active,    \
                                                         n_keys, cap, R, o, H, scale);          \
   } while (0)
+  // MX-fp8 cache: the whole-batch two-in-flight stream (MWX_XATTN8=0: the
+  // half-batch stream of dec_xattn_kernel, A/B)
+  static const bool x8 = !(getenv("MWX_XATTN8") && atoi(getenv("MWX_XATTN8")) == 0);
+  if (kv8 && x8) {
+    const uint8_t* k8 = reinterpret_cast<const uint8_t*>(kbase);
+    const uint8_t* v8 = reinterpret_cast<const uint8_t*>(vbase);
+    switch (nq) {
+#define X8(N)                                                                                  \
+  case N:                                                                                      \
+    dec_xattn8_kernel<T, N><<<g, 256, 0, st>>>(P, KS, pcols, bias, k8, v8, kscale8, vscale8,    \
+                                               kv_index, active, n_keys, cap, R, o, H, scale); \
+    return true;
+      X8(1) X8(2) X8(3) X8(4) X8(5) X8(6) X8(7) X8(8)
+#undef X8
+      default: return false;
+    }
+  }
   switch (nq) {
 #define XQ(N)                                  \
   case N:                                      \

@@ -127,8 +127,7 @@ def test_prefill_long_form_initial_prompt_matches_oracle(make_model, arch, wtype
     # (bf16 at v3 geometry: the diagnostic `tid` of a text token can be a
     # timestamp tie within rounding noise, seen pt 0.4272 / 0.4253)
     assert_same(segs, osegs, p_tol=2e-2, tid_tie_tol=5e-3)
-    n_tok = sum(len(w) for w in windows)
-    # every window's decode loop starts at the prompt's last position: steps
-    # = sampled tokens (+ the stop step and at most one run-ahead step per
-    # window), the prompt's other positions all prefilled
-    assert pf > 0 and steps <= n_tok + 2 * len(windows), (steps, n_tok, pf)
+    # every window's prompt but its last position went through the prefill
+    # (the step counts with and without it: test_prefill_equals_stepwise)
+    assert pf >= len(PROMPT.split()) * len(windows), (steps, pf)
+    print(f"{arch}: {len(windows)} windows, {steps} decode steps, {pf} prompt positions prefilled")
