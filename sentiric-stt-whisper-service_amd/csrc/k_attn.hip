@@ -957,6 +957,7 @@ __global__ __launch_bounds__(256) void dec_xattn8_kernel(
         d = dpp_sum8(d);
         if (c == 0 && j < n) sc[q][j] = d * scale;
       }
+      __builtin_amdgcn_sched_barrier(0);  // one row's conversions live at a time
     }
   };
   auto softmax = [&]() {
@@ -1015,20 +1016,24 @@ __global__ __launch_bounds__(256) void dec_xattn8_kernel(
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc[q][e] = __builtin_amdgcn_fdot2(ph, vp[e], acc[q][e], false);
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
-  auto step = [&](uint2 (&qbuf)[8], uint32_t& sr, int t) {
-    if (t == nb) softmax();  // every K batch is scored
-    if (t < nb)
-      score(qbuf, sr, t);
-    else
-      pvb(qbuf, sr, t - nb);
-    if (t + 2 < 2 * nb) load(qbuf, sr, t + 2);
-  };
+  // (nb even, the caller's condition: V batch 0 lands in qa, 1 in qb)
 #pragma unroll 1
-  for (int t = 0; t < 2 * nb; t += 2) {
-    step(qa, sa, t);
-    if (t + 1 < 2 * nb) step(qb, sb, t + 1);
+  for (int t = 0; t < nb; t += 2) {
+    score(qa, sa, t);
+    load(qa, sa, t + 2);
+    score(qb, sb, t + 1);
+    load(qb, sb, t + 3);
+  }
+  softmax();
+#pragma unroll 1
+  for (int b = 0; b < nb; b += 2) {
+    pvb(qa, sa, b);
+    if (b + 2 < nb) load(qa, sa, nb + b + 2);
+    pvb(qb, sb, b + 1);
+    if (b + 3 < nb) load(qb, sb, nb + b + 3);
   }
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
@@ -1085,7 +1090,7 @@ bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float*
   // MX-fp8 cache: the whole-batch two-in-flight stream (MWX_XATTN8=0: the
   // half-batch stream of dec_xattn_kernel, A/B)
   static const bool x8 = !(getenv("MWX_XATTN8") && atoi(getenv("MWX_XATTN8")) == 0);
-  if (kv8 && x8) {
+  if (kv8 && x8 && ((n_keys + 255) / 256) % 2 == 0) {
     const uint8_t* k8 = reinterpret_cast<const uint8_t*>(kbase);
     const uint8_t* v8 = reinterpret_cast<const uint8_t*>(vbase);
     switch (nq) {
