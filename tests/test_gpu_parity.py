@@ -129,14 +129,21 @@ def assert_same(segs, osegs, p_tol=5e-3, tid_tie_tol=0.0):
     oids = [t.id for s in osegs for t in s.tokens]
     assert ids == oids, next(((i, a, b) for i, (a, b) in enumerate(zip(ids, oids)) if a != b), None)
     assert [(s.t0, s.t1, s.text) for s in segs] == [(s.t0, s.t1, s.text) for s in osegs]
-    toks = [t for s in segs for t in s.tokens]
-    otoks = [t for s in osegs for t in s.tokens]
-    for i, (t, to) in enumerate(zip(toks, otoks)):
-        assert (t.t0, t.t1) == (to.t0, to.t1), (
-            f"token {i}: dev t0/t1 {t.t0}/{t.t1} pt {t.pt:.6f} ptsum {t.ptsum:.6f} tid {t.tid} | "
-            f"oracle {to.t0}/{to.t1} pt {to.pt:.6f} ptsum {to.ptsum:.6f} tid {to.tid}")
-        assert t.tid == to.tid or abs(t.pt - to.pt) < tid_tie_tol, (i, t, to)
-        assert abs(t.p - to.p) < p_tol and abs(t.plog - to.plog) < 2 * p_tol, (i, t, to)
+    i = 0
+    for sg, osg in zip(segs, osegs):
+        # a timestamp tie inside the segment (two timestamp tokens within the
+        # rounding noise of the logits: the argmax `tid` differs) feeds
+        # whisper_exp_compute_token_level_timestamps a different timestamp
+        # anchor, which moves that segment's word times; they are compared
+        # only for segments without a tie
+        tie = any(t.tid != to.tid for t, to in zip(sg.tokens, osg.tokens))
+        for t, to in zip(sg.tokens, osg.tokens):
+            assert t.tid == to.tid or abs(t.pt - to.pt) < tid_tie_tol, (i, t, to)
+            assert tie or (t.t0, t.t1) == (to.t0, to.t1), (
+                f"token {i}: dev t0/t1 {t.t0}/{t.t1} pt {t.pt:.6f} ptsum {t.ptsum:.6f} tid {t.tid} | "
+                f"oracle {to.t0}/{to.t1} pt {to.pt:.6f} ptsum {to.ptsum:.6f} tid {to.tid}")
+            assert abs(t.p - to.p) < p_tol and abs(t.plog - to.plog) < 2 * p_tol, (i, t, to)
+            i += 1
 
 
 def test_greedy_tokens_match_oracle(micro):

@@ -55,7 +55,8 @@ def test_v3_geometry_greedy_matches_oracle(v3):
         segs = ctx.segments(i)
         _, osegs, _, _ = o.full(pcm, greedy_opt())
         assert len(osegs) >= 2 and sum(len(s.tokens) for s in osegs) > 10
-        assert_same(segs, osegs, p_tol=2e-2)
+        # (bf16 logits: timestamp ties within ~5e-3 of probability, see assert_same)
+        assert_same(segs, osegs, p_tol=2e-2, tid_tie_tol=5e-3)
 
 
 def test_v3_geometry_batch32_equals_single(v3):
