@@ -206,6 +206,7 @@ struct State {
   }
   // decoder workspace (row-batched)
   DBuf xd, hd, qd, od, ffd, logits, kself, vself, stepin, ctl, tokout, probs, logprobs, smask;
+  DBuf xd2;  // second residual buffer (LayerNorm-fused GEMMs: ping-pong)
   DBuf pqkv, pres, pq;  // split-K partial slabs of the decode GEMMs
   // batched prompt prefill: virtual-row inputs [tok|pos|act|xidx|crow] and the
   // layer stack's activations / slabs for up to MWX_PREFILL_ROWS virtual rows
@@ -898,6 +899,7 @@ struct Driver {
     S.pres.get((size_t)8 * R * d * 4);
     S.pq.get((size_t)8 * R * d * 4);
     S.xd.get((size_t)R * d * 4, true);
+    S.xd2.get((size_t)R * d * 4, true);
     // decode-GEMM A operands (fragment tiles), rows padded to the 64-row block
     // (+ one 64-row block per decode group: each group's region is padded)
     const size_t R64 = (size_t)(R + 63) / 64 * 64 + 64 * MWX_MAX_GROUPS;
@@ -991,6 +993,7 @@ struct Driver {
     // prefill: the self-cache row of each virtual row (nullptr: row = its own)
     const int* crow = nullptr;
     float* xd = nullptr;
+    float* xd2 = nullptr;  // the other residual buffer (LayerNorm-fused GEMMs)
     T *hd = nullptr, *od = nullptr, *ffd = nullptr;
     float *Pqkv = nullptr, *Pres = nullptr, *Pq = nullptr;
     _Float16 *kself = nullptr, *vself = nullptr;  // layer-0 self cache of row 0
@@ -1005,9 +1008,20 @@ struct Driver {
     bool prefill = false;
   };
 
+  // The decode LayerNorms of <= LNF_MAX_ROWS rows (one request, streaming)
+  // are folded into the consumer GEMMs (kernels.h LnFuse): three launches per
+  // layer fewer. MWX_LN_FUSE=0 keeps the separate LayerNorm launches (A/B;
+  // the results are the same bits).
+  static bool ln_fuse_on() {
+    static const bool on = !(getenv("MWX_LN_FUSE") && atoi(getenv("MWX_LN_FUSE")) == 0);
+    return on;
+  }
+
   // embedding + all decoder layers; returns the last FFN2's split-K factor
-  // and bias (folded into the consumer: the final LayerNorm)
-  void run_layers(const LayerRows& rw, hipStream_t s, int& ks_prev, const float*& bias_prev) {
+  // and bias (folded into the consumer: the final LayerNorm) and the buffer
+  // holding the residual stream
+  void run_layers(const LayerRows& rw, hipStream_t s, int& ks_prev, const float*& bias_prev,
+                  float** x_final = nullptr) {
     const int n = rw.n;
     const float kqs = powf(64.0f, -0.25f);
     embed<T>(Wt(C.tok_emb), C.dec_pe, rw.tok, rw.pos, rw.act, rw.xd, n, d, s);
@@ -1016,6 +1030,25 @@ struct Driver {
     const size_t layer_xs = (size_t)S.cross_cap * H * hp.n_audio_ctx * 2;      // kv8 scales
     float* xd = rw.xd;
     T* hd = rw.hd;
+    const bool fuse = !rw.prefill && rw.xd2 && n <= LNF_MAX_ROWS && d <= 2048 && ln_fuse_on();
+    float* xalt = rw.xd2;
+    // the LayerNorm of a fused site: the consumer reads xd (+ the producer's
+    // slabs) and its workgroup 0 writes the completed rows to the other buffer
+    auto lnf = [&](const float* w, const float* b, const float* P, int KS, const float* pb) {
+      LnFuse L;
+      L.x = xd;
+      L.w = w;
+      L.b = b;
+      L.P = P;
+      L.KS = KS;
+      L.pbias = pb;
+      L.active = rw.act;
+      if (P) {
+        L.xout = xalt;
+        std::swap(xd, xalt);
+      }
+      return L;
+    };
     T* od = rw.od;
     T* ffd = rw.ffd;
     float* Pqkv = rw.Pqkv;
@@ -1034,11 +1067,17 @@ struct Driver {
       const DecLayerW& W = C.dec[l];
       _Float16* ks = rw.kself + l * layer_self;
       _Float16* vs = rw.vself + l * layer_self;
-      layer_norm_dec<T>(xd, W.ln1_w, W.ln1_b, hd, n, d, act, s, ks_prev ? Pres : nullptr,
-                        ks_prev, bias_prev);
       int k1;
-      { PerfScope ps(S, "dec_gemm", s);
-        k1 = gemm_splitk_partials<T>(hd, Dw(W.qkv), n, 3 * d, d, Pqkv, s); }
+      if (fuse) {
+        const LnFuse L = lnf(W.ln1_w, W.ln1_b, ks_prev ? Pres : nullptr, ks_prev, bias_prev);
+        PerfScope ps(S, "dec_gemm", s);
+        k1 = gemm_splitk_partials<T>(hd, Dw(W.qkv), n, 3 * d, d, Pqkv, s, &L);
+      } else {
+        layer_norm_dec<T>(xd, W.ln1_w, W.ln1_b, hd, n, d, act, s, ks_prev ? Pres : nullptr,
+                          ks_prev, bias_prev);
+        PerfScope ps(S, "dec_gemm", s);
+        k1 = gemm_splitk_partials<T>(hd, Dw(W.qkv), n, 3 * d, d, Pqkv, s);
+      }
       static const int pf_selfwrite =
           getenv("MWX_PREFILL_SELFWRITE") ? atoi(getenv("MWX_PREFILL_SELFWRITE")) : 0;
       if (rw.prefill)
@@ -1050,10 +1089,16 @@ struct Driver {
       int k2;
       { PerfScope ps(S, "dec_gemm", s);
         k2 = gemm_splitk_partials<T>(od, Dw(W.o), n, d, d, Pres, s); }
-      layer_norm_dec<T>(xd, W.lnc_w, W.lnc_b, hd, n, d, act, s, Pres, k2, W.o_b);
       int k3;
-      { PerfScope ps(S, "dec_gemm", s);
-        k3 = gemm_splitk_partials<T>(hd, Dw(W.cq), n, d, d, Pq, s); }
+      if (fuse) {
+        const LnFuse L = lnf(W.lnc_w, W.lnc_b, Pres, k2, W.o_b);
+        PerfScope ps(S, "dec_gemm", s);
+        k3 = gemm_splitk_partials<T>(hd, Dw(W.cq), n, d, d, Pq, s, &L);
+      } else {
+        layer_norm_dec<T>(xd, W.lnc_w, W.lnc_b, hd, n, d, act, s, Pres, k2, W.o_b);
+        PerfScope ps(S, "dec_gemm", s);
+        k3 = gemm_splitk_partials<T>(hd, Dw(W.cq), n, d, d, Pq, s);
+      }
       if (!rw.prefill && perf_on(S, "event_bracket")) {
         // calibration: the same event pair around an empty kernel at the same
         // point of the chain (bench.py subtracts its average from the
@@ -1090,20 +1135,27 @@ struct Driver {
       int k4;
       { PerfScope ps(S, "dec_gemm", s);
         k4 = gemm_splitk_partials<T>(od, Dw(W.co), n, d, d, Pres, s); }
-      layer_norm_dec<T>(xd, W.ln2_w, W.ln2_b, hd, n, d, act, s, Pres, k4, W.co_b);
       EpiParams e;
       e.bias = W.fc1_b;
       e.c16 = ffd;
       e.ldc = 4 * d;
       e.pack_out = true;
       bool k5;
-      { PerfScope ps(S, "dec_gemm", s);
-        k5 = gemm_decode<T>(EPI_GELU, hd, Dw(W.fc1), n, 4 * d, d, e, s); }
+      if (fuse) {
+        const LnFuse L = lnf(W.ln2_w, W.ln2_b, Pres, k4, W.co_b);
+        PerfScope ps(S, "dec_gemm", s);
+        k5 = gemm_decode<T>(EPI_GELU, hd, Dw(W.fc1), n, 4 * d, d, e, s, &L);
+      } else {
+        layer_norm_dec<T>(xd, W.ln2_w, W.ln2_b, hd, n, d, act, s, Pres, k4, W.co_b);
+        PerfScope ps(S, "dec_gemm", s);
+        k5 = gemm_decode<T>(EPI_GELU, hd, Dw(W.fc1), n, 4 * d, d, e, s);
+      }
       { PerfScope ps(S, "dec_gemm", s);
         ks_prev = gemm_splitk_partials<T>(ffd, Dw(W.fc2), n, d, 4 * d, Pres, s); }
       bias_prev = W.fc2_b;
       if (!k1 || !k2 || !k3 || !k4 || !k5 || !ks_prev) throw std::runtime_error("mwx: unsupported split-K shape");
     }
+    if (x_final) *x_final = fuse ? xd : nullptr;
   }
 
   // Batched prompt prefill (whisper.cpp decodes a window's prompt in one
@@ -1197,6 +1249,7 @@ struct Driver {
     rw.act = si + 2 * R + r0;
     rw.xidx = si + 3 * R + r0;
     rw.xd = (float*)S.xd.p + (size_t)r0 * d;
+    rw.xd2 = (float*)S.xd2.p + (size_t)r0 * d;
     rw.hd = (T*)S.hd.p + prow * d;
     rw.od = (T*)S.od.p + prow * d;
     rw.ffd = (T*)S.ffd.p + prow * 4 * d;
@@ -1216,8 +1269,20 @@ struct Driver {
     float* Pres = rw.Pres;
     int ks_prev = 0;
     const float* bias_prev = nullptr;
-    run_layers(rw, s, ks_prev, bias_prev);
-    layer_norm_dec<T>(xd, C.dec_ln_w, C.dec_ln_b, hd, n, d, act, s, Pres, ks_prev, bias_prev);
+    float* xfin = nullptr;  // (LayerNorm-fused layers: the residual's buffer)
+    run_layers(rw, s, ks_prev, bias_prev, &xfin);
+    LnFuse Lfin;
+    if (xfin) {
+      Lfin.x = xfin;
+      Lfin.w = C.dec_ln_w;
+      Lfin.b = C.dec_ln_b;
+      Lfin.P = Pres;
+      Lfin.KS = ks_prev;
+      Lfin.pbias = bias_prev;
+      Lfin.active = act;  // (xout: the completed residual is not read again)
+    } else {
+      layer_norm_dec<T>(xd, C.dec_ln_w, C.dec_ln_b, hd, n, d, act, s, Pres, ks_prev, bias_prev);
+    }
     EpiParams e;
     e.c32 = (float*)S.logits.p + (size_t)r0 * V;
     e.ldc = V;
@@ -1228,7 +1293,7 @@ struct Driver {
     // launch at 32 rows, scripts/probe/dec_chain_probe.hip).
     e.mt = n <= 64 ? std::max(1, (n + 15) / 16) : 2;
     { PerfScope ps(S, "logits_gemm", s);
-    if (!gemm_decode<T>(EPI_F32, hd, Dw(C.tok_p), n, V, d, e, s))
+    if (!gemm_decode<T>(EPI_F32, hd, Dw(C.tok_p), n, V, d, e, s, xfin ? &Lfin : nullptr))
       throw std::runtime_error("mwx: unsupported logits GEMM shape"); }
     float* pr = nullptr;
     float* lp = nullptr;

@@ -101,16 +101,34 @@ struct DecW {
   DecW(const T* w_) : w(w_) {}
   DecW(const uint8_t* q_, const uint8_t* s_) : q(q_), s(s_) {}
 };
+// Decode LayerNorm folded into the consumer GEMM (rows <= LNF_MAX_ROWS, the
+// single-request / streaming case): every workgroup of the GEMM recomputes
+// the LayerNorm of its rows exactly as layer_norm_dec does (same element
+// ownership, slab sum, double sums and roundings) and forms its A fragments
+// from it; the one workgroup with blockIdx == 0 writes the completed
+// residual x + (sum P + pbias) to xout (the other buffer of a ping-pong pair:
+// the other workgroups are still reading x). The LayerNorm launch goes away.
+constexpr int LNF_MAX_ROWS = 4;
+struct LnFuse {
+  const float* x = nullptr;      // [M][K] residual rows
+  const float* w = nullptr;      // LayerNorm weight / bias [K]
+  const float* b = nullptr;
+  const float* P = nullptr;      // producer's split-K slabs [KS][M][K] (nullptr: x is complete)
+  int KS = 0;
+  const float* pbias = nullptr;  // producer's bias [K]
+  float* xout = nullptr;         // completed residual (nullptr: not written)
+  const int* active = nullptr;   // row flags
+};
 template <typename T>
 int gemm_splitk_partials(const T* Ap, const DecW<T>& W, int M, int N, int K, float* P,
-                         hipStream_t st);
+                         hipStream_t st, const LnFuse* ln = nullptr);
 // Decode full-K GEMM over fragment-tiled weights with a fused epilogue
 // (EPI_GELU / EPI_RES / EPI_F32 / EPI_STORE16 / EPI_DEC_QKV), rows in blocks of
 // 64 so a row's arithmetic does not depend on the batch. Returns false if K is
 // unsupported.
 template <typename T>
 bool gemm_decode(int epi, const T* Ap, const DecW<T>& W, int M, int N, int K, const EpiParams& P,
-                 hipStream_t st);
+                 hipStream_t st, const LnFuse* ln = nullptr);
 // Log-mel of a batch of clips in one pass (three launches): clip c's samples
 // at pcm_base + desc[c].pcm_off (n), its mel [n_mels][n_len] at mel_base +
 // desc[c].mel_off, normalised in place; mx[c] = the clip's raw max; part:

@@ -32,3 +32,17 @@ def test_oracle_library_loads():
     L = orc.lib()
     for n in ("orc_load", "orc_mel", "orc_encode", "orc_cross", "orc_decode_seq", "orc_full"):
         assert hasattr(L, n)
+
+
+def test_option_a_drop_in_compiles_and_links(tmp_path):
+    """INTEGRATION.md Option A: the reference SttEngine's whisper.h calls and
+    parameter fields, with the mwx.h names, compile and link against
+    libmwx.so (tests/abi/option_a_drop_in.cpp; linked, not run)."""
+    import subprocess
+    pkg = os.path.join(ROOT, "sentiric-stt-whisper-service_amd")
+    r = subprocess.run(["g++", "-std=c++17", "-Wall", "-Wextra", "-Werror",
+                        "-I" + os.path.join(ROOT, "include"),
+                        os.path.join(ROOT, "tests", "abi", "option_a_drop_in.cpp"),
+                        "-L" + pkg, "-lmwx", "-Wl,-rpath," + pkg, "-o", str(tmp_path / "a")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
