@@ -175,7 +175,7 @@ void stream(const char* dir) {
       int r = mwx_stt_stream_feed(s, bytes.data() + off, len, out.data(), cap);
       off += len;
       if (r < -2) {
-        CHECK(mwx_stt_stream_feed(s, bytes.data(), 2, out.data(), (int)out.size()) == -1);
+        CHECK(mwx_stt_stream_feed(s, bytes.data(), 2, out.data(), (int)out.size()) == -3);  // pending
         r = mwx_stt_stream_drain(s, out.data(), (int)out.size());
       }
       CHECK(r >= 0);
