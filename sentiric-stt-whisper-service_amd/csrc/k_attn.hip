@@ -1087,9 +1087,11 @@ bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float*
                                                         kscale8, vscale8, kv_index, active,    \
                                                         n_keys, cap, R, o, H, scale);          \
   } while (0)
-  // MX-fp8 cache: the whole-batch two-in-flight stream (MWX_XATTN8=0: the
-  // half-batch stream of dec_xattn_kernel, A/B)
-  static const bool x8 = !(getenv("MWX_XATTN8") && atoi(getenv("MWX_XATTN8")) == 0);
+  // MX-fp8 cache: MWX_XATTN8=1 selects the whole-batch two-in-flight stream
+  // (dec_xattn8_kernel). Off by default: measured 69.2 us per launch against
+  // 52.6 us for the half-batch stream of dec_xattn_kernel at beam 5, large-v3
+  // (gpurun_out s6); kept as the A/B.
+  static const bool x8 = getenv("MWX_XATTN8") && atoi(getenv("MWX_XATTN8")) != 0;
   if (kv8 && x8 && ((n_keys + 255) / 256) % 2 == 0) {
     const uint8_t* k8 = reinterpret_cast<const uint8_t*>(kbase);
     const uint8_t* v8 = reinterpret_cast<const uint8_t*>(vbase);

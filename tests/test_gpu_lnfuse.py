@@ -1,8 +1,8 @@
 """Decode LayerNorm folded into the consumer GEMMs for <= 4 rows (the
 single-request / streaming case, config C2; kernels.h LnFuse): every
 workgroup of the consumer recomputes the rows' LayerNorm exactly as the
-separate ln_dec launch does, so the results must be the same bits as with
-MWX_LN_FUSE=0 (separate LayerNorm launches)."""
+separate ln_dec launch does, so the results with MWX_LN_FUSE=1 must be the same
+bits as with the default separate LayerNorm launches (MWX_LN_FUSE=0)."""
 import json
 import os
 import subprocess
@@ -50,7 +50,7 @@ def run(path, n, inc, fuse):
 @pytest.mark.parametrize("arch,wtype,n,inc", [
     ("micro-rich", mwx.GGML_F16, 1, 0.2),     # d 128, fallback (best_of 5 rows > 4: unfused)
     ("tiny.en-rich", mwx.GGML_F16, 3, 0.0),   # d 384, split-K 3 slabs, 3 rows
-    ("base-rich", mwx.GGML_F16, 1, 0.0),      # d 512 (config C2), one row
+    ("base-rich", mwx.GGML_F16, 2, 0.0),      # d 512 (config C2 shapes), two rows
     ("large-v3-l2-rich", mwx.GGML_BF16, 2, 0.0),  # d 1280, bf16, 2 rows
 ])
 def test_ln_fused_equals_separate(make_model, arch, wtype, n, inc):
@@ -58,4 +58,4 @@ def test_ln_fused_equals_separate(make_model, arch, wtype, n, inc):
     a = run(path, n, inc, True)
     b = run(path, n, inc, False)
     assert a == b
-    assert sum(len(s[3]) for c in a for s in c) > 10
+    assert sum(len(s[3]) for c in a for s in c) > 3 * n
