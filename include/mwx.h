@@ -347,10 +347,14 @@ int mwx_write_synthetic_model(const char* path, const char* arch, int wtype,
                               uint64_t seed);
 
 /* Quantizes a whisper ggml .bin (f32 / f16 / bf16) into a ggml block type
- * (q4_0 = 2, q4_1 = 3, q5_0 = 6, q5_1 = 7, q8_0 = 8) with the rules of
+ * (q4_0 = 2, q4_1 = 3, q5_0 = 6, q5_1 = 7, q8_0 = 8; the 256-element K types
+ * q2_K = 10, q3_K = 11, q4_K = 12, q5_K = 13, q6_K = 14) with the rules of
  * whisper.cpp's `quantize` tool: 2-D tensors except the positional
  * embeddings are quantized, everything else is copied; ftype becomes
- * 2000 + ftype. Returns 0 on success. */
+ * 2000 + ftype. Legacy blocks are ggml's quantize_row_q*_ref bit for bit; K
+ * blocks come from a plain min/max encoder (valid blocks, not ggml's scale
+ * search). A row length that is not a multiple of the block (tiny's 384 for
+ * K types) fails with -8, as ggml's quantizer does. Returns 0 on success. */
 int mwx_model_quantize(const char* in_path, const char* out_path, int type);
 
 #ifdef __cplusplus

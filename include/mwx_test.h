@@ -40,6 +40,12 @@ int mwx_test_decode_last_prefill(struct mwx_context* ctx, struct mwx_state* stat
  * positions 0 .. n_pos-1, as f32 [n_pos][n_text_head][64] each. */
 int mwx_test_self_kv(struct mwx_state* state, int layer, int n_pos, float* k_out, float* v_out);
 
+/* The engine's load-time dequantizer (host code, no device work): n values
+ * of ggml block type `type` (legacy q4_0 .. q8_0 or K q2_K .. q6_K; n a
+ * multiple of the block) from src into dst as f32, before the f16 rounding
+ * of the upload. Returns 0, or -1 for an unsupported type / length. */
+int mwx_test_dequantize(int type, const void* src, long n, float* dst);
+
 /* Decode work counters of a state (the first state of a batch drives it):
  * decode steps launched and prompt positions run by the batched prompt
  * prefill since the last reset. reset != 0 zeroes them after reading. */

@@ -186,9 +186,17 @@ static int lang_id(const std::string& s) {
   return -1;
 }
 
+static inline float h2f_at(const uint8_t* p) {
+  uint16_t h;
+  memcpy(&h, p, 2);
+  return h2f(h);
+}
+
 // ggml legacy block quantizations (ggml-common.h block_q4_0 .. block_q8_0;
 // type ids Q4_0 = 2, Q4_1 = 3, Q5_0 = 6, Q5_1 = 7, Q8_0 = 8): 32 elements per
 // block, f16 scale d (and min m for the _1 variants), ggml dequantize_row_q*.
+// K super-blocks (ggml-common.h block_q2_K .. block_q6_K, type ids 10 .. 14):
+// 256 elements, ggml-quants.c dequantize_row_q*_K, restated per element below.
 static int quant_block_bytes(int tt) {
   switch (tt) {
     case 2: return 18;
@@ -196,11 +204,67 @@ static int quant_block_bytes(int tt) {
     case 6: return 22;
     case 7: return 24;
     case 8: return 34;
+    case 10: return 84;
+    case 11: return 110;
+    case 12: return 144;
+    case 13: return 176;
+    case 14: return 210;
     default: return 0;
   }
 }
+static int quant_block_elems(int tt) { return tt >= 10 && tt <= 14 ? 256 : 32; }
+
+// Element e (0..255) of one K super-block. Within a 128-element half h = e/128
+// the 2-bit planes of q2_K / q3_K interleave four 32-element groups g in one
+// 32-byte run (bits 2g..2g+1 of byte e%32); q3_K's sign-offset bit sits in
+// hmask[e%32] at bit 4h+g; q4_K / q5_K pair 32-element sub-blocks in nibbles
+// of a 32-byte run (sub-block e/32: byte (e/64)*32 + e%32, high nibble when
+// odd; q5_K's fifth bit at qh[e%32] bit e/32); q6_K keeps the low nibbles of
+// groups 0/1 and 2/3 in two 32-byte runs per half and the top two bits of
+// all four groups in one (byte h*32 + e%32, bits 2g..2g+1). Scales belong to
+// 16-element sub-blocks (e/16) except q4_K / q5_K's 32-element ones.
+static float dequant_k_elem(int tt, const uint8_t* b, int e) {
+  const int h = e / 128, g = (e % 128) / 32, l = e % 32;
+  switch (tt) {
+    case 10: {  // scales[16] (scale | min << 4), qs[64], d, dmin
+      const int s = b[e / 16];
+      const int q = (b[16 + h * 32 + l] >> (2 * g)) & 3;
+      return h2f_at(b + 80) * (float)(s & 15) * (float)q - h2f_at(b + 82) * (float)(s >> 4);
+    }
+    case 11: {  // hmask[32], qs[64], scales[12] (6-bit, offset 32), d
+      const int s = e / 16;
+      const int lo = (s < 8 ? b[96 + s] : b[96 + s - 8] >> 4) & 15;
+      const int hi = (b[104 + s % 4] >> (2 * (s / 4))) & 3;
+      const int q = ((b[32 + h * 32 + l] >> (2 * g)) & 3) - ((b[l] >> (4 * h + g)) & 1 ? 0 : 4);
+      return h2f_at(b + 108) * (float)((lo | (hi << 4)) - 32) * (float)q;
+    }
+    case 12:
+    case 13: {  // d, dmin, scales[12] (6-bit scale / min pairs), [qh[32]], qs[128]
+      const int s = e / 32;
+      const uint8_t* t = b + 4;
+      const int sc = s < 4 ? t[s] & 63 : (t[s + 4] & 15) | ((t[s - 4] >> 6) << 4);
+      const int mn = s < 4 ? t[s + 4] & 63 : (t[s + 4] >> 4) | ((t[s] >> 6) << 4);
+      const uint8_t* qs = b + (tt == 13 ? 48 : 16);
+      int q = (qs[(s / 2) * 32 + l] >> (4 * (s & 1))) & 15;
+      if (tt == 13) q += ((b[16 + l] >> s) & 1) << 4;
+      return h2f_at(b) * (float)sc * (float)q - h2f_at(b + 2) * (float)mn;
+    }
+    case 14: {  // ql[128], qh[64], scales[16] (int8), d
+      const int lo = (b[h * 64 + (g & 1) * 32 + l] >> (4 * (g >> 1))) & 15;
+      const int hi = (b[128 + h * 32 + l] >> (2 * g)) & 3;
+      return h2f_at(b + 208) * (float)(int8_t)b[192 + e / 16] * (float)((lo | (hi << 4)) - 32);
+    }
+    default: return 0.0f;
+  }
+}
+
 static void dequant_blocks(int tt, const uint8_t* q, float* y, int64_t n) {
   const int bb = quant_block_bytes(tt);
+  if (quant_block_elems(tt) == 256) {
+    for (int64_t b = 0; b < n / 256; ++b, q += bb, y += 256)
+      for (int e = 0; e < 256; ++e) y[e] = dequant_k_elem(tt, q, e);
+    return;
+  }
   for (int64_t b = 0; b < n / 32; ++b, q += bb, y += 32) {
     uint16_t hd, hm = 0;
     memcpy(&hd, q, 2);
@@ -317,8 +381,8 @@ static bool load(const char* path, Model& m) {
     } else if (quant_block_bytes(tt) > 0) {
       // whisper.cpp quantize-tool output: dequantized (ggml dequantize_row_q*)
       // and rounded once to f16, the engine's compute type for these files
-      if (T.ne[0] % 32) return false;
-      std::vector<uint8_t> q((size_t)(n / 32) * quant_block_bytes(tt));
+      if (T.ne[0] % quant_block_elems(tt)) return false;
+      std::vector<uint8_t> q((size_t)(n / quant_block_elems(tt)) * quant_block_bytes(tt));
       f.read((char*)q.data(), q.size());
       dequant_blocks(tt, q.data(), T.v.data(), n);
       for (int64_t i = 0; i < n; ++i) T.v[i] = f16_round(T.v[i]);

@@ -14,8 +14,9 @@
 namespace mwx {
 
 // ggml tensor types used by whisper .bin files (ggml.h enum ggml_type values):
-// f32 / f16 / bf16 and the legacy 32-element block quantizations written by
-// whisper.cpp's quantize tool.
+// f32 / f16 / bf16, the legacy 32-element block quantizations and the
+// 256-element "K" super-block quantizations written by whisper.cpp's quantize
+// tool.
 enum GgmlType : int32_t {
   GGML_F32 = 0,
   GGML_F16 = 1,
@@ -24,11 +25,18 @@ enum GgmlType : int32_t {
   GGML_Q5_0 = 6,
   GGML_Q5_1 = 7,
   GGML_Q8_0 = 8,
+  GGML_Q2_K = 10,
+  GGML_Q3_K = 11,
+  GGML_Q4_K = 12,
+  GGML_Q5_K = 13,
+  GGML_Q6_K = 14,
   GGML_BF16 = 30
 };
 
 // quant.cpp: block formats (ggml-common.h) and ggml's reference (de)quantizers
 bool ggml_type_is_quant(int type);
+// elements per block: 32 (legacy), 256 (K super-blocks), 1 (f32/f16/bf16), 0 unknown
+int ggml_block_elems(int type);
 // bytes of an n-element tensor with inner dim ne0 (0: unsupported type/shape)
 size_t ggml_tensor_bytes(int type, int64_t ne0, int64_t n);
 void ggml_dequantize(int type, const uint8_t* src, float* dst, int64_t n);

@@ -14,6 +14,7 @@
 #include <regex>
 
 #include "common.h"
+#include "mwx_test.h"
 
 namespace mwx {
 
@@ -430,6 +431,8 @@ static bool arch_hparams(const std::string& arch, Hparams& hp) {
       {"micro", 51864, 1500, 128, 2, 2, 448, 128, 2, 3, 80},
       {"micro-ml", 51865, 1500, 128, 2, 2, 448, 128, 2, 3, 80},
       {"micro-v3", 51866, 1500, 128, 2, 2, 448, 128, 2, 3, 128},
+      // test geometry for the 256-element K quantizations (rows of 256)
+      {"micro256", 51864, 1500, 256, 4, 2, 448, 256, 4, 3, 80},
       {"tiny.en", 51864, 1500, 384, 6, 4, 448, 384, 6, 4, 80},
       {"tiny", 51865, 1500, 384, 6, 4, 448, 384, 6, 4, 80},
       {"base.en", 51864, 1500, 512, 8, 6, 448, 512, 8, 6, 80},
@@ -548,6 +551,13 @@ extern "C" int mwx_write_synthetic_model(const char* path, const char* arch,
   }
   hp.ftype = ggml_ftype_of(wtype);
   if (hp.ftype < 0) return -2;
+  // K super-blocks need rows of a multiple of 256 (ggml_row_size)
+  const int be = ggml_block_elems(wtype);
+  if (hp.n_audio_state % be || hp.n_text_state % be) {
+    MWX_LOG_ERROR("mwx_write_synthetic_model: %s rows (%d) are not a multiple of the %d-element "
+                  "blocks of type %d\n", an.c_str(), hp.n_text_state, be, wtype);
+    return -2;
+  }
   // quantized files keep the 3-D conv kernels in f16 (the quantize tool only
   // rewrites 2-D tensors)
   const int conv_type = ggml_type_is_quant(wtype) ? GGML_F16 : wtype;
@@ -673,7 +683,8 @@ extern "C" int mwx_write_synthetic_model(const char* path, const char* arch,
 
 // ---------------------------------------------------------------------------
 // model quantizer: whisper.cpp's `quantize` tool (examples/quantize +
-// examples/common-ggml.cpp ggml_common_quantize_0 at v1.8.2) — every 2-D
+// examples/common-ggml.cpp ggml_common_quantize_0 at v1.8.2; K types: valid
+// blocks from quant.cpp's plain encoder, not ggml's scale search) — every 2-D
 // tensor except the positional embeddings (and conv biases, which are not
 // 2-D in ggml's sense for the rule below) is rewritten as `type` blocks from
 // its f32 (or f16 / bf16 widened) values; everything else is copied
@@ -741,8 +752,14 @@ extern "C" int mwx_model_quantize(const char* in_path, const char* out_path, int
     const bool skip = name == "encoder.positional_embedding" ||
                       name == "decoder.positional_embedding" ||
                       name == "encoder.conv1.bias" || name == "encoder.conv2.bias";
-    const bool quant = nd == 2 && !skip && ne[0] % 32 == 0 &&
+    const bool quant = nd == 2 && !skip &&
                        (tt == GGML_F32 || tt == GGML_F16 || tt == GGML_BF16);
+    if (quant && ne[0] % ggml_block_elems(type) != 0) {
+      // ggml_quantize_chunk asserts on such rows: whisper.cpp's tool fails too
+      MWX_LOG_ERROR("mwx_model_quantize: '%s' rows of %d are not a multiple of the %d-element "
+                    "blocks of type %d\n", name.c_str(), ne[0], ggml_block_elems(type), type);
+      return -8;
+    }
     const int32_t ot = quant ? type : tt;
     fo.write(reinterpret_cast<const char*>(&nd), 4);
     fo.write(reinterpret_cast<const char*>(&nl), 4);
@@ -769,6 +786,14 @@ extern "C" int mwx_model_quantize(const char* in_path, const char* out_path, int
   }
   fo.close();
   return fo ? 0 : -7;
+}
+
+extern "C" int mwx_test_dequantize(int type, const void* src, long n, float* dst) {
+  using namespace mwx;
+  const int be = ggml_block_elems(type);
+  if (!ggml_type_is_quant(type) || n < 0 || n % be || !src || !dst) return -1;
+  ggml_dequantize(type, static_cast<const uint8_t*>(src), dst, n);
+  return 0;
 }
 
 extern "C" void mwx_log_set(mwx_log_callback cb, void* user_data) {

@@ -30,8 +30,15 @@ GGML_Q4_1 = 3
 GGML_Q5_0 = 6
 GGML_Q5_1 = 7
 GGML_Q8_0 = 8
+GGML_Q2_K = 10
+GGML_Q3_K = 11
+GGML_Q4_K = 12
+GGML_Q5_K = 13
+GGML_Q6_K = 14
 GGML_QUANT_TYPES = {"q4_0": GGML_Q4_0, "q4_1": GGML_Q4_1, "q5_0": GGML_Q5_0,
-                    "q5_1": GGML_Q5_1, "q8_0": GGML_Q8_0}
+                    "q5_1": GGML_Q5_1, "q8_0": GGML_Q8_0, "q2_k": GGML_Q2_K,
+                    "q3_k": GGML_Q3_K, "q4_k": GGML_Q4_K, "q5_k": GGML_Q5_K,
+                    "q6_k": GGML_Q6_K}
 SAMPLING_GREEDY = 0
 SAMPLING_BEAM_SEARCH = 1
 
@@ -201,6 +208,8 @@ def lib() -> C.CDLL:
                                                C.POINTER(C.c_float)]
     L.mwx_test_self_kv.restype = C.c_int
     L.mwx_test_self_kv.argtypes = [P, C.c_int, C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_float)]
+    L.mwx_test_dequantize.restype = C.c_int
+    L.mwx_test_dequantize.argtypes = [C.c_int, C.c_void_p, C.c_long, C.POINTER(C.c_float)]
     L.mwx_test_decode_counters.restype = C.c_int
     L.mwx_test_decode_counters.argtypes = [P, C.POINTER(C.c_long), C.POINTER(C.c_long), C.c_int]
     L.mwx_test_sample_draws.restype = C.c_int
@@ -250,6 +259,16 @@ def write_synthetic_model(path: str, arch: str, wtype: int = GGML_F16, seed: int
     rc = lib().mwx_write_synthetic_model(path.encode(), arch.encode(), wtype, seed)
     if rc != 0:
         raise RuntimeError(f"mwx_write_synthetic_model failed ({rc})")
+
+
+def dequantize(qtype: int, raw: bytes, n: int) -> np.ndarray:
+    """mwx_test_dequantize: the engine's load-time dequantizer (host only)."""
+    out = np.empty(n, np.float32)
+    buf = np.frombuffer(raw, np.uint8)
+    rc = lib().mwx_test_dequantize(qtype, buf.ctypes.data, n, out.ctypes.data_as(C.POINTER(C.c_float)))
+    if rc != 0:
+        raise ValueError(f"mwx_test_dequantize({qtype}, n={n}) returned {rc}")
+    return out
 
 
 def quantize_model(in_path: str, out_path: str, qtype: int) -> None:

@@ -449,6 +449,26 @@ def test_quantized_model_greedy_matches_oracle(make_model, qname):
         assert_same(segs, osegs)
 
 
+@pytest.mark.parametrize("qname", ["q2_k", "q3_k", "q4_k", "q5_k", "q6_k"])
+def test_k_quantized_model_greedy_matches_oracle(make_model, qname):
+    """256-element K super-block files (q2_K .. q6_K; micro256: rows of 256,
+    the smallest geometry ggml can K-quantize), dequantized at load and
+    computed in f16: tokens, timestamps and probabilities against the oracle
+    reading the same file (its own per-element restatement of the blocks)."""
+    path = make_model("micro256-rich", mwx.GGML_QUANT_TYPES[qname])
+    o = orc.Oracle(path)
+    with mwx.Context.open(path) as ctx:
+        pcm = pcm_clip(0)
+        opt = orc.FullOptions.service_defaults()
+        opt.temperature_inc = 0.0
+        opt.language = "en"
+        segs = run_fresh(ctx, pcm, service_params(ctx, temperature_inc=0.0, language=b"en"))
+        _, osegs, _, windows = o.full(pcm, opt)
+        # (q2_K's 2-bit codes leave the -rich weights little to say: 2 segments)
+        assert len(segs) >= (2 if qname == "q2_k" else 20) and len(windows) > 1
+        assert_same(segs, osegs)
+
+
 def np_discrete_draws(probs, u, ndraw):
     """libstdc++ std::discrete_distribution<int>(w.begin(), w.end()) then
     operator()(rng) with generate_canonical value u: S = sequential double sum,

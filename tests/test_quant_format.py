@@ -1,8 +1,16 @@
 """ggml block-quantized model files (whisper.cpp `quantize` tool output:
-q4_0, q4_1, q5_0, q5_1, q8_0 on every 2-D tensor but the positional embeddings;
-conv kernels stay f16). Checks the writer's blocks and the oracle's loader
-against an independent numpy restatement of ggml-common.h / ggml-quants.c
-(dequantize_row_q*, quantize_row_q*_ref) — CPU only."""
+q4_0, q4_1, q5_0, q5_1, q8_0 and the 256-element K types q2_K .. q6_K on every
+2-D tensor but the positional embeddings; conv kernels stay f16). Checks the
+writer's blocks and the oracle's loader against an independent numpy
+restatement of ggml-common.h / ggml-quants.c (dequantize_row_q*,
+quantize_row_q*_ref) — CPU only.
+
+K-quant parity is unpinned against ggml itself (no ggml source, binary or
+K-quantized file is in the reference or this image): the engine (quant.cpp,
+ggml's loop order), the oracle (per-element restatement) and the numpy
+restatement here (vectorised over super-blocks) are three independent
+readings of ggml-quants.c dequantize_row_q2_K .. q6_K that must agree bit for
+bit, on blocks whose every code / scale / min / high-bit plane is exercised."""
 import struct
 
 import numpy as np
@@ -12,9 +20,16 @@ import mwx
 import orc
 
 BLOCK = {mwx.GGML_Q4_0: 18, mwx.GGML_Q4_1: 20, mwx.GGML_Q5_0: 22, mwx.GGML_Q5_1: 24,
-         mwx.GGML_Q8_0: 34}
+         mwx.GGML_Q8_0: 34, mwx.GGML_Q2_K: 84, mwx.GGML_Q3_K: 110, mwx.GGML_Q4_K: 144,
+         mwx.GGML_Q5_K: 176, mwx.GGML_Q6_K: 210}
 FTYPE = {mwx.GGML_Q4_0: 2, mwx.GGML_Q4_1: 3, mwx.GGML_Q8_0: 7, mwx.GGML_Q5_0: 8,
-         mwx.GGML_Q5_1: 9}
+         mwx.GGML_Q5_1: 9, mwx.GGML_Q2_K: 10, mwx.GGML_Q3_K: 11, mwx.GGML_Q4_K: 12,
+         mwx.GGML_Q5_K: 13, mwx.GGML_Q6_K: 14}
+KTYPES = [mwx.GGML_Q2_K, mwx.GGML_Q3_K, mwx.GGML_Q4_K, mwx.GGML_Q5_K, mwx.GGML_Q6_K]
+
+
+def blk_elems(tt):
+    return 256 if tt in KTYPES else 32
 
 
 def read_tensors(path):
@@ -40,14 +55,73 @@ def read_tensors(path):
         name = buf[o:o + nl].decode()
         o += nl
         n = int(np.prod(ne))
-        size = n * 4 if tt == 0 else n * 2 if tt in (1, 30) else n // 32 * BLOCK[tt]
+        size = n * 4 if tt == 0 else n * 2 if tt in (1, 30) else n // blk_elems(tt) * BLOCK[tt]
         out[name] = (tt, ne, buf[o:o + size])
         o += size
     return hp, out
 
 
+def np_dequant_k(tt, raw, n):
+    """ggml dequantize_row_q2_K .. q6_K (f32), vectorised over super-blocks:
+    each block's 256 outputs as [half 2][group 4][lane 32] planes."""
+    b = np.frombuffer(raw, np.uint8).reshape(n // 256, BLOCK[tt])
+    f16 = lambda o: b[:, o:o + 2].copy().view(np.float16).astype(np.float32)  # noqa: E731
+    f = np.float32
+    if tt in (mwx.GGML_Q2_K, mwx.GGML_Q3_K):
+        qs = b[:, 16:80] if tt == mwx.GGML_Q2_K else b[:, 32:96]
+        qs = qs.reshape(-1, 2, 1, 32).astype(np.int32)                 # [blk][half][1][32]
+        q = (qs >> (2 * np.arange(4))[None, None, :, None]) & 3        # [blk][half][grp][32]
+        if tt == mwx.GGML_Q2_K:
+            sc = b[:, 0:16].reshape(-1, 2, 4, 2, 1).astype(np.int32)   # sub-block = 16 lanes
+            d, dmin = f16(80)[:, :, None, None, None], f16(82)[:, :, None, None, None]
+            q5 = q.reshape(-1, 2, 4, 2, 16).astype(f)
+            y = (d * (sc & 15).astype(f)) * q5 - dmin * (sc >> 4).astype(f)
+            return y.reshape(-1)
+        hm = b[:, 0:32].astype(np.int32)
+        bit = np.arange(8).reshape(2, 4)                              # [half][grp] -> hmask bit
+        high = (hm[:, None, None, :] >> bit[None, :, :, None]) & 1
+        q = q - np.where(high == 1, 0, 4)
+        raw12 = b[:, 96:108].astype(np.int32)
+        s = np.arange(16)
+        lo = np.where(s < 8, raw12[:, s % 8] & 15, raw12[:, s % 8] >> 4)
+        hi = (raw12[:, 8 + s % 4] >> (2 * (s // 4))) & 3
+        scales = (lo | (hi << 4)) - 32                                 # [blk][16]
+        d = f16(108)[:, :, None, None, None]
+        y = (d * scales.reshape(-1, 2, 4, 2, 1).astype(f)) * q.reshape(-1, 2, 4, 2, 16).astype(f)
+        return y.reshape(-1)
+    if tt in (mwx.GGML_Q4_K, mwx.GGML_Q5_K):
+        t = b[:, 4:16].astype(np.int32)
+        j = np.arange(8)
+        jl = np.minimum(j, 3)
+        sc = np.where(j < 4, t[:, jl] & 63, (t[:, (j + 4) % 12] & 15) | ((t[:, (j - 4) % 12] >> 6) << 4))
+        mn = np.where(j < 4, t[:, jl + 4] & 63, (t[:, (j + 4) % 12] >> 4) | ((t[:, j % 12] >> 6) << 4))
+        qo = 48 if tt == mwx.GGML_Q5_K else 16
+        ql = b[:, qo:qo + 128].reshape(-1, 4, 1, 32).astype(np.int32)  # [blk][pair][1][32]
+        q = (ql >> np.array([0, 4])[None, None, :, None]) & 15          # [blk][pair][nib][32]
+        q = q.reshape(-1, 8, 32)
+        if tt == mwx.GGML_Q5_K:
+            qh = b[:, 16:48].astype(np.int32)
+            q = q + (((qh[:, None, :] >> j[None, :, None]) & 1) << 4)
+        d, dmin = f16(0), f16(2)
+        y = (d * sc.astype(f))[:, :, None] * q.astype(f) - (dmin * mn.astype(f))[:, :, None]
+        return y.reshape(-1)
+    # q6_K
+    ql = b[:, 0:128].reshape(-1, 2, 2, 32).astype(np.int32)            # [blk][half][run][32]
+    lo = np.stack([ql[:, :, 0] & 15, ql[:, :, 1] & 15, ql[:, :, 0] >> 4, ql[:, :, 1] >> 4], axis=2)
+    qh = b[:, 128:192].reshape(-1, 2, 1, 32).astype(np.int32)
+    hi = (qh >> (2 * np.arange(4))[None, None, :, None]) & 3
+    q = (lo | (hi << 4)) - 32                                           # [blk][half][grp][32]
+    sc = b[:, 192:208].view(np.int8).reshape(-1, 2, 4, 2, 1).astype(f)
+    d = f16(208)[:, :, None, None, None]
+    y = (d * sc) * q.reshape(-1, 2, 4, 2, 16).astype(f)
+    return y.reshape(-1)
+
+
 def np_dequant(tt, raw, n):
-    """ggml dequantize_row_q4_0 / q4_1 / q5_0 / q5_1 / q8_0 (f32)."""
+    """ggml dequantize_row_q4_0 / q4_1 / q5_0 / q5_1 / q8_0 (f32); K types
+    through np_dequant_k."""
+    if tt in KTYPES:
+        return np_dequant_k(tt, raw, n)
     b = np.frombuffer(raw, np.uint8).reshape(n // 32, BLOCK[tt])
     d = b[:, 0:2].copy().view(np.float16).astype(np.float32)
     if tt == mwx.GGML_Q8_0:
@@ -221,3 +295,104 @@ def test_model_quantize_tool(make_model, tmp_path, tt):
     # the oracle (and so the engine's loader, same reader rules) accepts it
     o = orc.Oracle(dst)
     assert o.tensor("decoder.blocks.0.mlp.0.weight").shape[0] > 0
+
+
+# ------------------------------------------------------------- K super-blocks
+KIDS = ["q2_K", "q3_K", "q4_K", "q5_K", "q6_K"]
+
+
+def random_k_blocks(tt, nblk, seed):
+    """Arbitrary bytes in every field of a K super-block (all codes, scale
+    and min values and high-bit planes occur), with finite f16 super-block
+    scales d / dmin in [-2, 2]."""
+    rng = np.random.default_rng(seed)
+    b = rng.integers(0, 256, (nblk, BLOCK[tt]), dtype=np.uint8)
+    offs = {mwx.GGML_Q2_K: (80, 82), mwx.GGML_Q3_K: (108,), mwx.GGML_Q4_K: (0, 2),
+            mwx.GGML_Q5_K: (0, 2), mwx.GGML_Q6_K: (208,)}[tt]
+    for o in offs:
+        b[:, o:o + 2] = rng.uniform(-2, 2, nblk).astype(np.float16).view(np.uint8).reshape(nblk, 2)
+    return b.tobytes()
+
+
+@pytest.mark.parametrize("tt", KTYPES, ids=KIDS)
+def test_k_dequant_engine_equals_numpy_on_arbitrary_blocks(tt):
+    """The engine's load-time dequantizer (quant.cpp, ggml's loop order) and
+    the numpy restatement agree bit for bit (f32) on 512 super-blocks of
+    arbitrary bytes."""
+    n = 512 * 256
+    raw = random_k_blocks(tt, 512, tt)
+    got = mwx.dequantize(tt, raw, n)
+    want = np_dequant_k(tt, raw, n)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), \
+        np.flatnonzero(got != want)[:8]
+    with pytest.raises(ValueError):
+        mwx.dequantize(tt, raw[:BLOCK[tt]], 128)  # not a whole super-block
+
+
+@pytest.mark.parametrize("tt", KTYPES, ids=KIDS)
+def test_k_quantized_file_three_dequantizers_agree(make_model, tt):
+    """micro256 (rows of 256) written as `tt`: quantize-tool tensor types and
+    ftype; for several weights the oracle's loader (per-element restatement,
+    then f16), the engine's dequantizer and numpy agree bit for bit; the
+    blocks encode the f16 file's seeded weights to within one code step of
+    their sub-block; the bit planes that carry high bits / signs are used."""
+    path = make_model("micro256", tt)
+    hp, ts = read_tensors(path)
+    assert hp[10] == 2000 + FTYPE[tt]
+    assert ts["encoder.conv1.weight"][0] == mwx.GGML_F16
+    assert ts["decoder.positional_embedding"][0] == 0
+    for name in ("decoder.token_embedding.weight", "encoder.blocks.0.mlp.0.weight",
+                 "decoder.blocks.1.cross_attn.key.weight"):
+        assert ts[name][0] == tt, name
+    o = orc.Oracle(path)
+    ref16 = orc.Oracle(make_model("micro256", mwx.GGML_F16))
+    sub = 32 if tt in (mwx.GGML_Q4_K, mwx.GGML_Q5_K) else 16
+    qmax = {mwx.GGML_Q2_K: 3, mwx.GGML_Q3_K: 7, mwx.GGML_Q4_K: 15, mwx.GGML_Q5_K: 31,
+            mwx.GGML_Q6_K: 63}[tt]
+    for name in ("encoder.blocks.1.attn.query.weight", "decoder.blocks.2.mlp.2.weight",
+                 "decoder.token_embedding.weight"):
+        t, ne, raw = ts[name]
+        n = int(np.prod(ne))
+        want = np_dequant_k(t, raw, n)
+        assert np.array_equal(mwx.dequantize(t, raw, n), want), name
+        got = o.tensor(name)
+        np.testing.assert_array_equal(got, want.astype(np.float16).astype(np.float32))
+        x = ref16.tensor(name).reshape(-1, sub)
+        # one code step of the sub-block's range, plus the 6- / 4-bit scale
+        # and min quantization (relative to the super-block's largest)
+        step = (x.max(axis=1) - np.minimum(x.min(axis=1), 0)) / qmax
+        sblk = np.abs(x).reshape(-1, 256 // sub, sub).max(axis=(1, 2)).repeat(256 // sub)
+        err = np.abs(got.reshape(-1, sub) - x).max(axis=1)
+        assert np.all(err <= 1.01 * step + 0.02 * sblk + 1e-3), (name, (err - step).max())
+    raw = np.frombuffer(ts["decoder.blocks.0.mlp.0.weight"][2], np.uint8).reshape(-1, BLOCK[tt])
+    plane = {mwx.GGML_Q2_K: raw[:, 16:80], mwx.GGML_Q3_K: raw[:, 0:32],
+             mwx.GGML_Q4_K: raw[:, 16:144], mwx.GGML_Q5_K: raw[:, 16:48],
+             mwx.GGML_Q6_K: raw[:, 128:192]}[tt]
+    bits = np.unpackbits(plane, axis=1).mean(axis=0)
+    assert bits.min() > 0.01 and bits.max() < 0.99, (bits.min(), bits.max())
+
+
+@pytest.mark.parametrize("tt", KTYPES, ids=KIDS)
+def test_model_quantize_tool_k(make_model, tmp_path, tt):
+    """mwx_model_quantize with K types: micro256 f16 -> `tt`, the quantize
+    tool's copy rules; the blocks decode (numpy) to within the encoder's bound
+    of the f16 values; a 384-wide (tiny) model fails as ggml's quantizer does."""
+    src = make_model("micro256", mwx.GGML_F16)
+    dst = str(tmp_path / "qk.bin")
+    mwx.quantize_model(src, dst, tt)
+    hp_s, ts_s = read_tensors(src)
+    hp_d, ts_d = read_tensors(dst)
+    assert hp_d[:10] == hp_s[:10] and hp_d[10] == 2000 + FTYPE[tt]
+    assert list(ts_d) == list(ts_s)
+    for name, (t, ne, raw) in ts_d.items():
+        if t == tt:
+            assert len(ne) == 2 and ts_s[name][0] == mwx.GGML_F16
+        else:
+            assert raw == ts_s[name][2], name
+    t, ne, raw = ts_d["decoder.blocks.1.attn.value.weight"]
+    x = np.frombuffer(ts_s["decoder.blocks.1.attn.value.weight"][2], np.float16).astype(np.float32)
+    y = np_dequant_k(t, raw, x.size)
+    assert np.abs(y - x).max() <= 0.6 * np.abs(x).max()
+    assert np.corrcoef(x, y)[0, 1] > (0.8 if tt == mwx.GGML_Q2_K else 0.97)
+    with pytest.raises(RuntimeError):
+        mwx.quantize_model(make_model("tiny", mwx.GGML_F16), str(tmp_path / "bad.bin"), tt)
