@@ -649,7 +649,11 @@ def main():
     p.bench_fixed_steps = args.decode_steps
     prompt_len = 3 if ARCH[args.arch][5] >= 51865 else 1
     n_windows = max(1, int(np.ceil(args.clip_seconds / 30.0 - 1e-9)))
-    max_tok = (args.decode_steps or 448) * n_windows
+    # record capacity per clip: a fixed-step window emits decode_steps tokens;
+    # decoding to the model's stop, long-form windows advance to the last
+    # timestamp (not a fixed 30 s), so a clip can take several times
+    # n_windows windows of up to n_text_ctx (448) tokens each
+    max_tok = args.decode_steps * n_windows if args.decode_steps else 448 * n_windows * 4
     gathered = {}
 
     # inputs resident in HBM before the timed region (the PCIe-inclusive rate,

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <memory>
@@ -1206,6 +1207,16 @@ struct Driver {
     rw.vself = (_Float16*)S.vself.p;
     rw.prefill = true;
     std::vector<std::vector<int>> hin;  // host inputs, alive until the final sync
+    // MWX_PREFILL_TIME=1: device time of the pass (events) and host time of
+    // the call on stderr (diagnostic)
+    static const bool timing = getenv("MWX_PREFILL_TIME") && atoi(getenv("MWX_PREFILL_TIME")) != 0;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    const auto th0 = std::chrono::steady_clock::now();
+    if (timing) {
+      HIPC(hipEventCreate(&ev0));
+      HIPC(hipEventCreate(&ev1));
+      HIPC(hipEventRecord(ev0, st));
+    }
     for (int p0 = 0; p0 < nmax; p0 += span) {
       std::vector<int> tok, pos, act, xidx, crow;
       for (const auto& r : prs) {
@@ -1238,7 +1249,18 @@ struct Driver {
       const float* bias_prev = nullptr;
       run_layers(rw, st, ks_prev, bias_prev);
     }
+    if (timing) HIPC(hipEventRecord(ev1, st));
     HIPC(hipStreamSynchronize(st));  // (host inputs / the next chunk's reuse of din)
+    if (timing) {
+      float ms = 0.0f;
+      HIPC(hipEventElapsedTime(&ms, ev0, ev1));
+      const double host_ms = std::chrono::duration<double, std::milli>(
+                                 std::chrono::steady_clock::now() - th0).count();
+      fprintf(stderr, "mwx prefill: %d rows, %d positions max, span %d, %zu virtual rows per chunk: "
+              "device %.3f ms, host call %.3f ms\n", nrows, nmax, span, mcap, ms, host_ms);
+      HIPC(hipEventDestroy(ev0));
+      HIPC(hipEventDestroy(ev1));
+    }
   }
 
   // decoder step for rows [r0, r0+n) of an R-row step, launched on `s`

@@ -126,7 +126,7 @@ def test_prefill_long_form_initial_prompt_matches_oracle(make_model, arch, wtype
     assert len(windows) >= 2 and len(segs) >= 2
     # (bf16 at v3 geometry: the diagnostic `tid` of a text token can be a
     # timestamp tie within rounding noise, seen pt 0.4272 / 0.4253)
-    assert_same(segs, osegs, p_tol=2e-2, tid_tie_tol=5e-3)
+    assert_same(segs, osegs, p_tol=2e-2, tid_tie_tol=2e-2)
     # every window's prompt but its last position went through the prefill
     # (the step counts with and without it: test_prefill_equals_stepwise)
     assert pf >= len(PROMPT.split()) * len(windows), (steps, pf)

