@@ -212,6 +212,10 @@ struct State {
   // batched prompt prefill: virtual-row inputs [tok|pos|act|xidx|crow] and the
   // layer stack's activations / slabs for up to MWX_PREFILL_ROWS virtual rows
   DBuf pf_in, pf_x, pf_h, pf_o, pf_ff, pf_pqkv, pf_pres, pf_pq;
+  // the prefill's host-side inputs of all chunks: read by its stream-ordered
+  // uploads, rewritten only by the next prefill (after that window's step
+  // synchronizes)
+  std::vector<int> pf_hin;
   // counters (mwx_test_decode_counters): decode steps launched, prompt
   // positions prefilled
   long n_steps = 0, n_prefill = 0;
@@ -1113,9 +1117,7 @@ struct Driver {
         // the decoders of a beam / best-of group share their clip's cross K/V:
         // stream it once per group; an MX-fp8 cache is read by the grouped
         // kernel for any group size
-        static const int pf_xnq =
-            getenv("MWX_PREFILL_XNQ") ? std::max(1, atoi(getenv("MWX_PREFILL_XNQ"))) : 8;
-        const int nq = rw.prefill ? pf_xnq : std::max(1, xgroup);
+        const int nq = std::max(1, xgroup);  // (prefill: Driver::prefill's q)
         if (C.kv8) {
           if (!dec_cross_attention_grouped<T>(
                   Pq, k3, d, W.cq_b, (const uint8_t*)S.cross_k.p + l * layer_cross,
@@ -1171,7 +1173,8 @@ struct Driver {
   // decode step's for that row and position (row-blocked GEMMs, the same
   // attention kernels), so the cache holds the same bits as step by step.
   // Rows in chunks of <= MWX_PREFILL_ROWS virtual rows (default 2048), each
-  // row's positions padded to a multiple of 8 (cross-attention groups).
+  // row's positions padded to a multiple of the cross-attention group q
+  // (min(8, prompt length)). Queued without a host synchronize.
   struct PrefillRow {
     int row;                 // self-cache row
     int clip;                // cross slot
@@ -1192,7 +1195,13 @@ struct Driver {
     // positions per chunk: every row with work gets the same span (x 8)
     static const int span_env = getenv("MWX_PREFILL_SPAN") ? atoi(getenv("MWX_PREFILL_SPAN")) : 0;
     const int span = span_env > 0 ? span_env : std::max(8, (vcap / nrows) / 8 * 8);
-    const size_t mcap = (size_t)nrows * ((std::min(span, nmax) + 7) / 8 * 8);
+    // cross-attention group: q consecutive virtual rows of one clip share one
+    // K/V stream (MWX_PREFILL_XNQ caps it, default 8); each row's positions are
+    // padded to a multiple of q (short prompts: q = their length, no padding)
+    static const int xnq_cap =
+        getenv("MWX_PREFILL_XNQ") ? std::max(1, std::min(8, atoi(getenv("MWX_PREFILL_XNQ")))) : 8;
+    const int q = std::max(1, std::min(xnq_cap, std::min(span, nmax)));
+    const size_t mcap = (size_t)nrows * ((std::min(span, nmax) + q - 1) / q * q);
     const size_t m64 = (mcap + 63) / 64 * 64;
     int* din = (int*)S.pf_in.get(mcap * 5 * 4);
     LayerRows rw;
@@ -1206,7 +1215,14 @@ struct Driver {
     rw.kself = (_Float16*)S.kself.p;
     rw.vself = (_Float16*)S.vself.p;
     rw.prefill = true;
-    std::vector<std::vector<int>> hin;  // host inputs, alive until the final sync
+    rw.xgroup = q;
+    // host inputs of every chunk in one array (no reallocation while its
+    // uploads are queued): the pass is queued without a synchronize, so the
+    // host goes on to capture / launch the decode steps behind it
+    size_t chunks = 0;
+    for (int p0 = 0; p0 < nmax; p0 += span) ++chunks;
+    S.pf_hin.clear();
+    S.pf_hin.reserve(chunks * mcap * 5);
     // MWX_PREFILL_TIME=1: device time of the pass (events) and host time of
     // the call on stderr (diagnostic)
     static const bool timing = getenv("MWX_PREFILL_TIME") && atoi(getenv("MWX_PREFILL_TIME")) != 0;
@@ -1222,7 +1238,7 @@ struct Driver {
       for (const auto& r : prs) {
         const int len = std::min(r.n, p0 + span) - p0;
         if (len <= 0) continue;
-        const int padded = (len + 7) / 8 * 8;
+        const int padded = (len + q - 1) / q * q;
         for (int j = 0; j < padded; ++j) {
           const bool a = j < len;
           tok.push_back(a ? r.tokens[p0 + j] : 0);
@@ -1235,10 +1251,13 @@ struct Driver {
       const int M = (int)tok.size();
       if (M == 0) continue;
       if ((size_t)M > mcap) throw std::runtime_error("mwx: prefill chunk exceeds its buffers");
-      hin.emplace_back();
-      std::vector<int>& h = hin.back();
-      for (auto* v : {&tok, &pos, &act, &xidx, &crow}) h.insert(h.end(), v->begin(), v->end());
-      HIPC(hipMemcpyAsync(din, h.data(), h.size() * 4, hipMemcpyHostToDevice, st));
+      const size_t h0 = S.pf_hin.size();
+      for (auto* v : {&tok, &pos, &act, &xidx, &crow})
+        S.pf_hin.insert(S.pf_hin.end(), v->begin(), v->end());
+      // (din is reused by the next chunk: its upload is ordered after this
+      // chunk's kernels on the same stream)
+      HIPC(hipMemcpyAsync(din, S.pf_hin.data() + h0, (S.pf_hin.size() - h0) * 4,
+                          hipMemcpyHostToDevice, st));
       rw.n = M;
       rw.tok = din;
       rw.pos = din + M;
@@ -1249,9 +1268,9 @@ struct Driver {
       const float* bias_prev = nullptr;
       run_layers(rw, st, ks_prev, bias_prev);
     }
-    if (timing) HIPC(hipEventRecord(ev1, st));
-    HIPC(hipStreamSynchronize(st));  // (host inputs / the next chunk's reuse of din)
     if (timing) {
+      HIPC(hipEventRecord(ev1, st));
+      HIPC(hipStreamSynchronize(st));
       float ms = 0.0f;
       HIPC(hipEventElapsedTime(&ms, ev0, ev1));
       const double host_ms = std::chrono::duration<double, std::milli>(
