@@ -787,6 +787,8 @@ def main():
         rows = args.clips * max(1, args.beam)
         if args.perf_class.startswith("dec_attn"):
             rows = rows / max(1, int(os.environ.get("MWX_DECODE_GROUPS", "1")))
+            if os.environ.get("MWX_DECODE_PAIR", "0") not in ("", "0"):
+                rows = rows / 2  # two interleaved row sets per step (engine.cpp)
         clips_per_launch = args.clips * (rows / (args.clips * max(1, args.beam)))
         bound, work, desc = kernel_model(args.arch, args.perf_class, clips_per_launch, rows,
                                          launches // max(1, nsteps), prompt_len,

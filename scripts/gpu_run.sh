@@ -8,12 +8,19 @@
 #   benchq     default bench without the CPU baseline (quick)
 #   bench1     C3 on one lane
 #   c2         C2: base f16, one clip per request
+#   c2nt       C2 with the cross K/V streamed non-temporally (A/B of the MALL-resident default)
+#   x64 / g2x64  64 clips in one state, one decode chain / two row groups on two streams
+#   pair64     64 clips in one state, decoded as two interleaved 32-row sets (MWX_DECODE_PAIR)
+#   pair64x2   the same on two lanes
+#   pairtest   the paired-decode parity tests only
 #   b5         beam 5 (service default decode), C3 shape
 #   c5         C5: MX-fp8, beam 5, 600-s long-form clips
 #   prompt     long-form leg with previous-window text carried as the prompt
 #   prof       rocprofv3 --kernel-trace --stats of the exact default bench command
 #   prof1      the same for --lanes 1
 #   profc2     kernel trace of the C2 leg
+#   profb5     kernel trace of beam 5 (one lane)
+#   profc5     kernel trace of the C5 leg (one lane, one 600-s batch)
 #   pmc        FETCH_SIZE / WRITE_SIZE / MFMA-busy passes (each its own run) on a short decode
 # Outputs go to gpurun_out/<TAG>_*; copy the summaries to be judged into profiles/.
 set -o pipefail
@@ -39,18 +46,26 @@ run() {  # name, seconds, command...
 }
 for s in "$@"; do
   case $s in
-    tests) run tests 1150 python -u -m pytest tests -m gpu -x -v -s -rf --timeout 300 --timeout-method thread ;;
+    tests) run tests 1150 python -u -m pytest tests -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python -u bench.py --steps 20 --warmup 5 ;;
     benchq) run benchq 400 python -u bench.py --steps 8 --warmup 2 --no-cpu-baseline ;;
     bench1) run bench1 400 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
     c2) run c2 300 python -u bench.py --arch base --wtype f16 --clips 1 --lanes 1 --steps 20 --warmup 3 --no-cpu-baseline ;;
+    c2nt) run c2nt 300 env MWX_XATTN_NT=1 python -u bench.py --arch base --wtype f16 --clips 1 --lanes 1 --steps 20 --warmup 3 --no-cpu-baseline ;;
+    x64) run x64 500 python -u bench.py --clips 64 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    g2x64) run g2x64 500 env MWX_DECODE_GROUPS=2 python -u bench.py --clips 64 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    pair64) run pair64 500 env MWX_DECODE_PAIR=1 python -u bench.py --clips 64 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    pair64x2) run pair64x2 600 env MWX_DECODE_PAIR=1 python -u bench.py --clips 64 --lanes 2 --steps 4 --warmup 1 --no-cpu-baseline ;;
+    pairtest) run pairtest 600 python -u -m pytest tests/test_gpu_pair.py -m gpu -x -v -s -rf --timeout 300 --timeout-method thread ;;
     b5) run b5 500 python -u bench.py --beam 5 --steps 4 --warmup 1 --no-cpu-baseline ;;
     c5) run c5 700 python -u bench.py --fp8 --beam 5 --clip-seconds 600 --steps 2 --warmup 1 --no-cpu-baseline ;;
     prompt) run prompt 700 python -u bench.py --prompt-leg --steps 2 --warmup 1 --no-cpu-baseline ;;
     prof) (cd /tmp && run prof 600 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_prof" -o prof -- $B --steps 4 --warmup 2 --no-cpu-baseline) || exit 4 ;;
     prof1) (cd /tmp && run prof1 600 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_prof1" -o prof -- $B --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline) || exit 4 ;;
     profc2) (cd /tmp && run profc2 400 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_profc2" -o prof -- $B --arch base --wtype f16 --clips 1 --lanes 1 --steps 5 --warmup 2 --no-cpu-baseline) || exit 4 ;;
+    profb5) (cd /tmp && run profb5 600 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_profb5" -o prof -- $B --beam 5 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline) || exit 4 ;;
+    profc5) (cd /tmp && run profc5 700 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_profc5" -o prof -- $B --fp8 --beam 5 --lanes 1 --steps 1 --warmup 0 --no-cpu-baseline) || exit 4 ;;
     pmc)
       for C in FETCH_SIZE WRITE_SIZE; do
         (cd /tmp && run pmc_$C 400 rocprofv3 --pmc $C --output-format csv -d "$O/${TAG}_pmc_$C" -o pmc -- $B --lanes 1 --steps 1 --warmup 0 --decode-steps 8 --no-cpu-baseline) || exit 5

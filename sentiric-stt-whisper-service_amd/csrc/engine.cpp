@@ -150,6 +150,10 @@ struct State {
   // ev_in orders the groups after the step inputs, ev_done joins them
   hipStream_t gstream[MWX_MAX_GROUPS] = {};
   hipEvent_t ev_in = nullptr, ev_done[MWX_MAX_GROUPS] = {};
+  // paired decode (MWX_DECODE_PAIR): the second row set's stream and the
+  // events of its interleave with the first
+  hipStream_t pstream = nullptr;
+  hipEvent_t pev_fork = nullptr, pev_a = nullptr, pev_b = nullptr, pev_join = nullptr;
   // encoder stream (MWX_STREAM_PRIO=enc_low / both): the encoder of a batch runs
   // on a low-priority stream, ordered after / before `stream` by two events,
   // so a concurrent batch's latency-bound decode chain is dispatched first
@@ -1024,143 +1028,168 @@ struct Driver {
     return on;
   }
 
+  // One pass of the decoder layer stack over a set of rows, in parts: the
+  // embedding, and per layer the chain up to the cross-attention's query
+  // projection (pre), the cross-attention (cross) and the chain after it
+  // (post). run_layers runs them in order on one stream; decode_group_pair
+  // interleaves the parts of two row sets on two streams.
+  struct LayerRun {
+    float* xd = nullptr;    // the residual stream's buffer
+    float* xalt = nullptr;  // the other buffer (LayerNorm-fused sites)
+    bool fuse = false;
+    int k1 = 0, k2 = 0, k3 = 0, k4 = 0;
+    bool k5 = false;
+    int ks_prev = 0;  // the last FFN2's split-K factor and bias (folded into
+    const float* bias_prev = nullptr;  // the next consumer)
+  };
+  // the LayerNorm of a fused site: the consumer reads xd (+ the producer's
+  // slabs) and its workgroup 0 writes the completed rows to the other buffer
+  LnFuse lnf(LayerRun& c, const LayerRows& rw, const float* w, const float* b, const float* P,
+             int KS, const float* pb) {
+    LnFuse L;
+    L.x = c.xd;
+    L.w = w;
+    L.b = b;
+    L.P = P;
+    L.KS = KS;
+    L.pbias = pb;
+    L.active = rw.act;
+    if (P) {
+      L.xout = c.xalt;
+      std::swap(c.xd, c.xalt);
+    }
+    return L;
+  }
+  void layers_begin(const LayerRows& rw, LayerRun& c, hipStream_t s) {
+    embed<T>(Wt(C.tok_emb), C.dec_pe, rw.tok, rw.pos, rw.act, rw.xd, rw.n, d, s);
+    c = LayerRun{};
+    c.xd = rw.xd;
+    c.xalt = rw.xd2;
+    c.fuse = !rw.prefill && rw.xd2 && rw.n <= LNF_MAX_ROWS && d <= 2048 && ln_fuse_on();
+  }
+  // The d- and 3d-wide projections run as split-K GEMMs writing f32 partial
+  // slabs; each consumer (LN: bias + residual, attention: bias/scale/f16 and
+  // the KV-cache append) folds the slabs in, so no launch is added.
+  void layer_pre(const LayerRows& rw, LayerRun& c, int l, hipStream_t s) {
+    const int n = rw.n;
+    const float kqs = powf(64.0f, -0.25f);
+    const size_t layer_self = (size_t)S.row_cap * H * Tctx * 64;
+    const DecLayerW& W = C.dec[l];
+    _Float16* ks = rw.kself + l * layer_self;
+    _Float16* vs = rw.vself + l * layer_self;
+    T* hd = rw.hd;
+    if (c.fuse) {
+      const LnFuse L = lnf(c, rw, W.ln1_w, W.ln1_b, c.ks_prev ? rw.Pres : nullptr, c.ks_prev,
+                           c.bias_prev);
+      PerfScope ps(S, "dec_gemm", s);
+      c.k1 = gemm_splitk_partials<T>(hd, Dw(W.qkv), n, 3 * d, d, rw.Pqkv, s, &L);
+    } else {
+      layer_norm_dec<T>(c.xd, W.ln1_w, W.ln1_b, hd, n, d, rw.act, s, c.ks_prev ? rw.Pres : nullptr,
+                        c.ks_prev, c.bias_prev);
+      PerfScope ps(S, "dec_gemm", s);
+      c.k1 = gemm_splitk_partials<T>(hd, Dw(W.qkv), n, 3 * d, d, rw.Pqkv, s);
+    }
+    static const int pf_selfwrite =
+        getenv("MWX_PREFILL_SELFWRITE") ? atoi(getenv("MWX_PREFILL_SELFWRITE")) : 0;
+    if (rw.prefill)
+      kv_append<T>(rw.Pqkv, c.k1, 3 * d, W.qkv_b, kqs, ks, vs, rw.crow, rw.pos, rw.act, Tctx, n, H,
+                   s);
+    { PerfScope ps(S, "dec_attn_self", s);
+      dec_attention<T>(rw.Pqkv, c.k1, 3 * d, W.qkv_b, kqs, kqs, ks, vs, rw.crow, rw.pos, rw.act, 0,
+                       Tctx, rw.od, n, H, 1.0f, s, rw.kvmap, rw.kvown, rw.map_row0,
+                       rw.prefill ? 1 : rw.xgroup, pf_selfwrite || !rw.prefill); }
+    { PerfScope ps(S, "dec_gemm", s);
+      c.k2 = gemm_splitk_partials<T>(rw.od, Dw(W.o), n, d, d, rw.Pres, s); }
+    if (c.fuse) {
+      const LnFuse L = lnf(c, rw, W.lnc_w, W.lnc_b, rw.Pres, c.k2, W.o_b);
+      PerfScope ps(S, "dec_gemm", s);
+      c.k3 = gemm_splitk_partials<T>(hd, Dw(W.cq), n, d, d, rw.Pq, s, &L);
+    } else {
+      layer_norm_dec<T>(c.xd, W.lnc_w, W.lnc_b, hd, n, d, rw.act, s, rw.Pres, c.k2, W.o_b);
+      PerfScope ps(S, "dec_gemm", s);
+      c.k3 = gemm_splitk_partials<T>(hd, Dw(W.cq), n, d, d, rw.Pq, s);
+    }
+  }
+  void layer_cross(const LayerRows& rw, LayerRun& c, int l, hipStream_t s) {
+    const int n = rw.n;
+    const float kqs = powf(64.0f, -0.25f);
+    const size_t layer_cross = (size_t)S.cross_cap * H * hp.n_audio_ctx * 64;  // elements
+    const size_t layer_xs = (size_t)S.cross_cap * H * hp.n_audio_ctx * 2;      // kv8 scales
+    const DecLayerW& W = C.dec[l];
+    if (!rw.prefill && perf_on(S, "event_bracket")) {
+      // calibration: the same event pair around an empty kernel at the same
+      // point of the chain (bench.py subtracts its average from the
+      // cross-attention brackets: the two event nodes' own cost)
+      PerfScope ps(S, "event_bracket", s);
+      launch_perf_empty(s);
+    }
+    PerfScope ps(S, rw.prefill ? "prefill_cross" : "dec_attn_cross", s);
+    // the decoders of a beam / best-of group share their clip's cross K/V:
+    // stream it once per group; an MX-fp8 cache is read by the grouped
+    // kernel for any group size
+    const int nq = std::max(1, rw.xgroup);  // (prefill: Driver::prefill's q)
+    if (C.kv8) {
+      if (!dec_cross_attention_grouped<T>(
+              rw.Pq, c.k3, d, W.cq_b, (const uint8_t*)S.cross_k.p + l * layer_cross,
+              (const uint8_t*)S.cross_v.p + l * layer_cross, rw.xidx, rw.act, hp.n_audio_ctx,
+              hp.n_audio_ctx, rw.od, n, H, kqs, nq, s,
+              (const uint8_t*)S.cross_ks.p + l * layer_xs,
+              (const uint8_t*)S.cross_vs.p + l * layer_xs))
+        throw std::runtime_error("mwx: unsupported fp8 cross-attention group");
+    } else if (nq < 2 ||
+               !dec_cross_attention_grouped<T>(rw.Pq, c.k3, d, W.cq_b,
+                                               (const _Float16*)S.cross_k.p + l * layer_cross,
+                                               (const _Float16*)S.cross_v.p + l * layer_cross,
+                                               rw.xidx, rw.act, hp.n_audio_ctx, hp.n_audio_ctx,
+                                               rw.od, n, H, kqs, nq, s)) {
+      dec_attention<T>(rw.Pq, c.k3, d, W.cq_b, 1.0f, 1.0f,
+                       (_Float16*)S.cross_k.p + l * layer_cross,
+                       (_Float16*)S.cross_v.p + l * layer_cross, rw.xidx, rw.pos, rw.act,
+                       hp.n_audio_ctx, hp.n_audio_ctx, rw.od, n, H, kqs, s, nullptr, nullptr, 0,
+                       nq);
+    }
+  }
+  void layer_post(const LayerRows& rw, LayerRun& c, int l, hipStream_t s) {
+    const int n = rw.n;
+    const DecLayerW& W = C.dec[l];
+    { PerfScope ps(S, "dec_gemm", s);
+      c.k4 = gemm_splitk_partials<T>(rw.od, Dw(W.co), n, d, d, rw.Pres, s); }
+    EpiParams e;
+    e.bias = W.fc1_b;
+    e.c16 = rw.ffd;
+    e.ldc = 4 * d;
+    e.pack_out = true;
+    if (c.fuse) {
+      const LnFuse L = lnf(c, rw, W.ln2_w, W.ln2_b, rw.Pres, c.k4, W.co_b);
+      PerfScope ps(S, "dec_gemm", s);
+      c.k5 = gemm_decode<T>(EPI_GELU, rw.hd, Dw(W.fc1), n, 4 * d, d, e, s, &L);
+    } else {
+      layer_norm_dec<T>(c.xd, W.ln2_w, W.ln2_b, rw.hd, n, d, rw.act, s, rw.Pres, c.k4, W.co_b);
+      PerfScope ps(S, "dec_gemm", s);
+      c.k5 = gemm_decode<T>(EPI_GELU, rw.hd, Dw(W.fc1), n, 4 * d, d, e, s);
+    }
+    { PerfScope ps(S, "dec_gemm", s);
+      c.ks_prev = gemm_splitk_partials<T>(rw.ffd, Dw(W.fc2), n, d, 4 * d, rw.Pres, s); }
+    c.bias_prev = W.fc2_b;
+    if (!c.k1 || !c.k2 || !c.k3 || !c.k4 || !c.k5 || !c.ks_prev)
+      throw std::runtime_error("mwx: unsupported split-K shape");
+  }
+
   // embedding + all decoder layers; returns the last FFN2's split-K factor
   // and bias (folded into the consumer: the final LayerNorm) and the buffer
   // holding the residual stream
   void run_layers(const LayerRows& rw, hipStream_t s, int& ks_prev, const float*& bias_prev,
                   float** x_final = nullptr) {
-    const int n = rw.n;
-    const float kqs = powf(64.0f, -0.25f);
-    embed<T>(Wt(C.tok_emb), C.dec_pe, rw.tok, rw.pos, rw.act, rw.xd, n, d, s);
-    const size_t layer_self = (size_t)S.row_cap * H * Tctx * 64;
-    const size_t layer_cross = (size_t)S.cross_cap * H * hp.n_audio_ctx * 64;  // elements
-    const size_t layer_xs = (size_t)S.cross_cap * H * hp.n_audio_ctx * 2;      // kv8 scales
-    float* xd = rw.xd;
-    T* hd = rw.hd;
-    const bool fuse = !rw.prefill && rw.xd2 && n <= LNF_MAX_ROWS && d <= 2048 && ln_fuse_on();
-    float* xalt = rw.xd2;
-    // the LayerNorm of a fused site: the consumer reads xd (+ the producer's
-    // slabs) and its workgroup 0 writes the completed rows to the other buffer
-    auto lnf = [&](const float* w, const float* b, const float* P, int KS, const float* pb) {
-      LnFuse L;
-      L.x = xd;
-      L.w = w;
-      L.b = b;
-      L.P = P;
-      L.KS = KS;
-      L.pbias = pb;
-      L.active = rw.act;
-      if (P) {
-        L.xout = xalt;
-        std::swap(xd, xalt);
-      }
-      return L;
-    };
-    T* od = rw.od;
-    T* ffd = rw.ffd;
-    float* Pqkv = rw.Pqkv;
-    float* Pres = rw.Pres;
-    float* Pq = rw.Pq;
-    const int* pos = rw.pos;
-    const int* act = rw.act;
-    const int* xidx = rw.xidx;
-    const int xgroup = rw.xgroup;
-    // The d- and 3d-wide projections run as split-K GEMMs writing f32 partial
-    // slabs; each consumer (LN: bias + residual, attention: bias/scale/f16 and
-    // the KV-cache append) folds the slabs in, so no launch is added.
-    ks_prev = 0;
-    bias_prev = nullptr;
+    LayerRun c;
+    layers_begin(rw, c, s);
     for (int l = 0; l < L_dec; ++l) {
-      const DecLayerW& W = C.dec[l];
-      _Float16* ks = rw.kself + l * layer_self;
-      _Float16* vs = rw.vself + l * layer_self;
-      int k1;
-      if (fuse) {
-        const LnFuse L = lnf(W.ln1_w, W.ln1_b, ks_prev ? Pres : nullptr, ks_prev, bias_prev);
-        PerfScope ps(S, "dec_gemm", s);
-        k1 = gemm_splitk_partials<T>(hd, Dw(W.qkv), n, 3 * d, d, Pqkv, s, &L);
-      } else {
-        layer_norm_dec<T>(xd, W.ln1_w, W.ln1_b, hd, n, d, act, s, ks_prev ? Pres : nullptr,
-                          ks_prev, bias_prev);
-        PerfScope ps(S, "dec_gemm", s);
-        k1 = gemm_splitk_partials<T>(hd, Dw(W.qkv), n, 3 * d, d, Pqkv, s);
-      }
-      static const int pf_selfwrite =
-          getenv("MWX_PREFILL_SELFWRITE") ? atoi(getenv("MWX_PREFILL_SELFWRITE")) : 0;
-      if (rw.prefill)
-        kv_append<T>(Pqkv, k1, 3 * d, W.qkv_b, kqs, ks, vs, rw.crow, pos, act, Tctx, n, H, s);
-      { PerfScope ps(S, "dec_attn_self", s);
-        dec_attention<T>(Pqkv, k1, 3 * d, W.qkv_b, kqs, kqs, ks, vs, rw.crow, pos, act, 0, Tctx,
-                         od, n, H, 1.0f, s, rw.kvmap, rw.kvown, rw.map_row0,
-                         rw.prefill ? 1 : xgroup, pf_selfwrite || !rw.prefill); }
-      int k2;
-      { PerfScope ps(S, "dec_gemm", s);
-        k2 = gemm_splitk_partials<T>(od, Dw(W.o), n, d, d, Pres, s); }
-      int k3;
-      if (fuse) {
-        const LnFuse L = lnf(W.lnc_w, W.lnc_b, Pres, k2, W.o_b);
-        PerfScope ps(S, "dec_gemm", s);
-        k3 = gemm_splitk_partials<T>(hd, Dw(W.cq), n, d, d, Pq, s, &L);
-      } else {
-        layer_norm_dec<T>(xd, W.lnc_w, W.lnc_b, hd, n, d, act, s, Pres, k2, W.o_b);
-        PerfScope ps(S, "dec_gemm", s);
-        k3 = gemm_splitk_partials<T>(hd, Dw(W.cq), n, d, d, Pq, s);
-      }
-      if (!rw.prefill && perf_on(S, "event_bracket")) {
-        // calibration: the same event pair around an empty kernel at the same
-        // point of the chain (bench.py subtracts its average from the
-        // cross-attention brackets: the two event nodes' own cost)
-        PerfScope ps(S, "event_bracket", s);
-        launch_perf_empty(s);
-      }
-      { PerfScope ps(S, rw.prefill ? "prefill_cross" : "dec_attn_cross", s);
-        // the decoders of a beam / best-of group share their clip's cross K/V:
-        // stream it once per group; an MX-fp8 cache is read by the grouped
-        // kernel for any group size
-        const int nq = std::max(1, xgroup);  // (prefill: Driver::prefill's q)
-        if (C.kv8) {
-          if (!dec_cross_attention_grouped<T>(
-                  Pq, k3, d, W.cq_b, (const uint8_t*)S.cross_k.p + l * layer_cross,
-                  (const uint8_t*)S.cross_v.p + l * layer_cross, xidx, act, hp.n_audio_ctx,
-                  hp.n_audio_ctx, od, n, H, kqs, nq, s,
-                  (const uint8_t*)S.cross_ks.p + l * layer_xs,
-                  (const uint8_t*)S.cross_vs.p + l * layer_xs))
-            throw std::runtime_error("mwx: unsupported fp8 cross-attention group");
-        } else if (nq < 2 ||
-            !dec_cross_attention_grouped<T>(Pq, k3, d, W.cq_b,
-                                            (const _Float16*)S.cross_k.p + l * layer_cross,
-                                            (const _Float16*)S.cross_v.p + l * layer_cross, xidx,
-                                            act, hp.n_audio_ctx, hp.n_audio_ctx, od, n, H, kqs,
-                                            nq, s))
-          dec_attention<T>(Pq, k3, d, W.cq_b, 1.0f, 1.0f,
-                           (_Float16*)S.cross_k.p + l * layer_cross,
-                           (_Float16*)S.cross_v.p + l * layer_cross, xidx, pos, act,
-                           hp.n_audio_ctx, hp.n_audio_ctx, od, n, H, kqs, s, nullptr, nullptr, 0,
-                           nq); }
-      int k4;
-      { PerfScope ps(S, "dec_gemm", s);
-        k4 = gemm_splitk_partials<T>(od, Dw(W.co), n, d, d, Pres, s); }
-      EpiParams e;
-      e.bias = W.fc1_b;
-      e.c16 = ffd;
-      e.ldc = 4 * d;
-      e.pack_out = true;
-      bool k5;
-      if (fuse) {
-        const LnFuse L = lnf(W.ln2_w, W.ln2_b, Pres, k4, W.co_b);
-        PerfScope ps(S, "dec_gemm", s);
-        k5 = gemm_decode<T>(EPI_GELU, hd, Dw(W.fc1), n, 4 * d, d, e, s, &L);
-      } else {
-        layer_norm_dec<T>(xd, W.ln2_w, W.ln2_b, hd, n, d, act, s, Pres, k4, W.co_b);
-        PerfScope ps(S, "dec_gemm", s);
-        k5 = gemm_decode<T>(EPI_GELU, hd, Dw(W.fc1), n, 4 * d, d, e, s);
-      }
-      { PerfScope ps(S, "dec_gemm", s);
-        ks_prev = gemm_splitk_partials<T>(ffd, Dw(W.fc2), n, d, 4 * d, Pres, s); }
-      bias_prev = W.fc2_b;
-      if (!k1 || !k2 || !k3 || !k4 || !k5 || !ks_prev) throw std::runtime_error("mwx: unsupported split-K shape");
+      layer_pre(rw, c, l, s);
+      layer_cross(rw, c, l, s);
+      layer_post(rw, c, l, s);
     }
-    if (x_final) *x_final = fuse ? xd : nullptr;
+    ks_prev = c.ks_prev;
+    bias_prev = c.bias_prev;
+    if (x_final) *x_final = c.fuse ? c.xd : nullptr;
   }
 
   // Batched prompt prefill (whisper.cpp decodes a window's prompt in one
@@ -1283,7 +1312,8 @@ struct Driver {
   }
 
   // decoder step for rows [r0, r0+n) of an R-row step, launched on `s`
-  void decode_group(int R, int r0, int n, size_t prow, bool want_probs, hipStream_t s) {
+  // the decode-step rows [r0, r0 + n) of R (packed A operands from row prow)
+  LayerRows step_rows(int R, int r0, int n, size_t prow) {
     int* si = (int*)S.stepin.p;
     LayerRows rw;
     rw.n = n;
@@ -1306,14 +1336,81 @@ struct Driver {
     rw.kvown = (const int*)S.kvown.p + r0;
     rw.map_row0 = r0;
     rw.xgroup = xgroup;
-    const int* act = rw.act;
-    float* xd = rw.xd;
-    T* hd = rw.hd;
-    float* Pres = rw.Pres;
+    return rw;
+  }
+
+  // Two row sets decoded as one step graph on two streams, their layers
+  // interleaved: the cross-attention of set B at layer l starts after set A's
+  // (layer l) has ended and set A's at layer l + 1 after set B's at layer l,
+  // so the two HBM-bound cross K/V streams never run at the same time and
+  // each runs beside the other set's latency-bound projection / LayerNorm
+  // chain (two independent chains on two streams have no such phase: their
+  // cross-attentions collide about as often as their chains do). Each set's
+  // kernels and arithmetic are those of a decode step of that set alone.
+  // MWX_DECODE_PAIR=1 enables it for steps of >= 2 x MWX_PAIR_MIN rows
+  // (default 16); the sets split at a clip boundary.
+  static bool pair_on() {
+    static const bool on = getenv("MWX_DECODE_PAIR") && atoi(getenv("MWX_DECODE_PAIR")) != 0;
+    return on;
+  }
+  bool pair_rows(int n) const {
+    static const int pmin = getenv("MWX_PAIR_MIN") ? std::max(1, atoi(getenv("MWX_PAIR_MIN"))) : 16;
+    return pair_on() && n >= 2 * pmin * std::max(1, xgroup);
+  }
+  // (outside any capture) the second stream and the interleave's events
+  void pair_prepare() {
+    if (!S.pstream) HIPC(hipStreamCreateWithFlags(&S.pstream, hipStreamNonBlocking));
+    for (auto* e : {&S.pev_fork, &S.pev_a, &S.pev_b, &S.pev_join})
+      if (!*e) HIPC(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  }
+  void decode_group_pair(int R, int r0, int n, size_t prow, bool want_probs, hipStream_t s) {
+    const int xg = std::max(1, xgroup);
+    const int na = (n / 2) / xg * xg, nb = n - na;
+    const LayerRows ra = step_rows(R, r0, na, prow);
+    const LayerRows rb = step_rows(R, r0 + na, nb, prow + (size_t)(na + 63) / 64 * 64);
+    hipStream_t s2 = S.pstream;
+    HIPC(hipEventRecord(S.pev_fork, s));
+    HIPC(hipStreamWaitEvent(s2, S.pev_fork, 0));
+    LayerRun ca, cb;
+    layers_begin(ra, ca, s);
+    layers_begin(rb, cb, s2);
+    for (int l = 0; l < L_dec; ++l) {
+      layer_pre(ra, ca, l, s);
+      if (l > 0) HIPC(hipStreamWaitEvent(s, S.pev_b, 0));
+      layer_cross(ra, ca, l, s);
+      HIPC(hipEventRecord(S.pev_a, s));
+      layer_post(ra, ca, l, s);
+      layer_pre(rb, cb, l, s2);
+      HIPC(hipStreamWaitEvent(s2, S.pev_a, 0));
+      layer_cross(rb, cb, l, s2);
+      HIPC(hipEventRecord(S.pev_b, s2));
+      layer_post(rb, cb, l, s2);
+    }
+    step_tail(R, ra, ca.ks_prev, ca.bias_prev, ca.fuse ? ca.xd : nullptr, want_probs, s);
+    step_tail(R, rb, cb.ks_prev, cb.bias_prev, cb.fuse ? cb.xd : nullptr, want_probs, s2);
+    HIPC(hipEventRecord(S.pev_join, s2));
+    HIPC(hipStreamWaitEvent(s, S.pev_join, 0));
+  }
+
+  void decode_group(int R, int r0, int n, size_t prow, bool want_probs, hipStream_t s) {
+    if (pair_rows(n)) return decode_group_pair(R, r0, n, prow, want_probs, s);
+    const LayerRows rw = step_rows(R, r0, n, prow);
     int ks_prev = 0;
     const float* bias_prev = nullptr;
     float* xfin = nullptr;  // (LayerNorm-fused layers: the residual's buffer)
     run_layers(rw, s, ks_prev, bias_prev, &xfin);
+    step_tail(R, rw, ks_prev, bias_prev, xfin, want_probs, s);
+  }
+
+  // final LayerNorm, logits and logits processing of a step's row set
+  void step_tail(int R, const LayerRows& rw, int ks_prev, const float* bias_prev, float* xfin,
+                 bool want_probs, hipStream_t s) {
+    const int n = rw.n;
+    const int r0 = rw.map_row0;
+    const int* act = rw.act;
+    float* xd = rw.xd;
+    T* hd = rw.hd;
+    float* Pres = rw.Pres;
     LnFuse Lfin;
     if (xfin) {
       Lfin.x = xfin;

@@ -1200,8 +1200,14 @@ void dec_attention(const float* P, int KS, int pcols, const float* bias, float q
   // (self rows per lane group per batch: 4 -- 66 VGPRs, 7 waves/SIMD: beam 5
   // 659 -> 687 audio-s/s; 8 with MWX_SELF_UB=8 for A/B)
   static const bool self_ub4 = !(getenv("MWX_SELF_UB") && atoi(getenv("MWX_SELF_UB")) == 8);
-  // cross K/V streamed with non-temporal loads (MWX_XATTN_NT=0: default policy)
-  static const bool xattn_nt = !(getenv("MWX_XATTN_NT") && atoi(getenv("MWX_XATTN_NT")) == 0);
+  // cross K/V streamed with non-temporal loads (MWX_XATTN_NT=0: default policy
+  // always, 1: nt always). Default: nt unless the launch's cross K/V is small
+  // (<= 4 MB: one base / small-model request), where the model's whole cross
+  // cache stays resident in the 256-MB MALL across decode steps with the
+  // default policy and nt would evict it every step
+  static const int xattn_nt_env = getenv("MWX_XATTN_NT") ? atoi(getenv("MWX_XATTN_NT")) : -1;
+  const bool xattn_nt =
+      xattn_nt_env >= 0 ? xattn_nt_env != 0 : (long)R * H * fixed_len * 256 > (4l << 20);
   // MWX_XATTN_NBC=0: the runtime-batch-count cross kernel (A/B of the
   // constant-count load stream)
   static const bool xattn_nbc = !(getenv("MWX_XATTN_NBC") && atoi(getenv("MWX_XATTN_NBC")) == 0);
@@ -1220,6 +1226,11 @@ void dec_attention(const float* P, int KS, int pcols, const float* bias, float q
                                                              kbase, vbase, kv_index, pos, active,
                                                              fixed_len, kv_len_cap, o, H, scale,
                                                              nullptr, nullptr, 0, nq, R);
+  else if (fixed_len == 1500 && xattn_nbc)
+    dec_attn_kernel<T, false, 8, false, 6><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale,
+                                                              kbase, vbase, kv_index, pos, active,
+                                                              fixed_len, kv_len_cap, o, H, scale,
+                                                              nullptr, nullptr, 0, nq, R);
   else if (xattn_nt)
     dec_attn_kernel<T, false, 8, true><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale,
                                                           kbase, vbase, kv_index, pos, active,

@@ -448,6 +448,10 @@ class Context:
     def hparam(self, name: str) -> int:
         return getattr(lib(), f"mwx_{name}")(self.ctx)
 
+    def token(self, name: str) -> int:
+        """special token id: eot, sot, beg, not, nosp, transcribe, translate"""
+        return getattr(lib(), f"mwx_token_{name}")(self.ctx)
+
     def test_mel(self, pcm: np.ndarray, state_index: int = 0) -> np.ndarray:
         pcm = np.ascontiguousarray(pcm, dtype=np.float32)
         n_mels = self.hparam("n_mels")
