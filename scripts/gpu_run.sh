@@ -12,6 +12,9 @@
 #   x64 / g2x64  64 clips in one state, one decode chain / two row groups on two streams
 #   pair64     64 clips in one state, decoded as two interleaved 32-row sets (MWX_DECODE_PAIR)
 #   pair64x2   the same on two lanes
+#   pair32 / pair32x2  one 32-clip batch per lane split into two interleaved 16-row sets
+#   mfstest    the MX-fp8 tests with the MFMA-score cross-attention (MWX_XATTN_MFS=1)
+#   c5mfs / c5one  C5 on one lane with / without the MFMA scores
 #   pairtest   the paired-decode parity tests only
 #   b5         beam 5 (service default decode), C3 shape
 #   c5         C5: MX-fp8, beam 5, 600-s long-form clips
@@ -21,6 +24,7 @@
 #   profc2     kernel trace of the C2 leg
 #   profb5     kernel trace of beam 5 (one lane)
 #   profc5     kernel trace of the C5 leg (one lane, one 600-s batch)
+#   pmcb5      instruction-mix / stall counters of a short beam-5 decode, bf16 and MX-fp8
 #   pmc        FETCH_SIZE / WRITE_SIZE / MFMA-busy passes (each its own run) on a short decode
 # Outputs go to gpurun_out/<TAG>_*; copy the summaries to be judged into profiles/.
 set -o pipefail
@@ -55,8 +59,13 @@ for s in "$@"; do
     c2nt) run c2nt 300 env MWX_XATTN_NT=1 python -u bench.py --arch base --wtype f16 --clips 1 --lanes 1 --steps 20 --warmup 3 --no-cpu-baseline ;;
     x64) run x64 500 python -u bench.py --clips 64 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
     g2x64) run g2x64 500 env MWX_DECODE_GROUPS=2 python -u bench.py --clips 64 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
-    pair64) run pair64 500 env MWX_DECODE_PAIR=1 python -u bench.py --clips 64 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
-    pair64x2) run pair64x2 600 env MWX_DECODE_PAIR=1 python -u bench.py --clips 64 --lanes 2 --steps 4 --warmup 1 --no-cpu-baseline ;;
+    pair64) run pair64 500 python -u bench.py --pair --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    pair64x2) run pair64x2 600 python -u bench.py --pair --lanes 2 --steps 4 --warmup 1 --no-cpu-baseline ;;
+    pair32) run pair32 500 env MWX_DECODE_PAIR=1 python -u bench.py --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    pair32x2) run pair32x2 500 env MWX_DECODE_PAIR=1 python -u bench.py --lanes 2 --steps 4 --warmup 1 --no-cpu-baseline ;;
+    mfstest) run mfstest 600 env MWX_XATTN_MFS=1 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shapes.py -k "mxfp8" -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
+    c5mfs) run c5mfs 700 env MWX_XATTN_MFS=1 python -u bench.py --fp8 --beam 5 --clip-seconds 600 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline ;;
+    c5one) run c5one 700 python -u bench.py --fp8 --beam 5 --clip-seconds 600 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline ;;
     pairtest) run pairtest 600 python -u -m pytest tests/test_gpu_pair.py -m gpu -x -v -s -rf --timeout 300 --timeout-method thread ;;
     b5) run b5 500 python -u bench.py --beam 5 --steps 4 --warmup 1 --no-cpu-baseline ;;
     c5) run c5 700 python -u bench.py --fp8 --beam 5 --clip-seconds 600 --steps 2 --warmup 1 --no-cpu-baseline ;;
@@ -66,6 +75,9 @@ for s in "$@"; do
     profc2) (cd /tmp && run profc2 400 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_profc2" -o prof -- $B --arch base --wtype f16 --clips 1 --lanes 1 --steps 5 --warmup 2 --no-cpu-baseline) || exit 4 ;;
     profb5) (cd /tmp && run profb5 600 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_profb5" -o prof -- $B --beam 5 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline) || exit 4 ;;
     profc5) (cd /tmp && run profc5 700 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_profc5" -o prof -- $B --fp8 --beam 5 --lanes 1 --steps 1 --warmup 0 --no-cpu-baseline) || exit 4 ;;
+    pmcb5)  # instruction mix / stall counters of the beam-5 (and fp8) kernels
+      (cd /tmp && run pmcb5 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d "$O/${TAG}_pmcb5" -o pmc -- $B --beam 5 --lanes 1 --steps 1 --warmup 0 --decode-steps 8 --no-cpu-baseline) || exit 5
+      (cd /tmp && run pmcc5 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d "$O/${TAG}_pmcc5" -o pmc -- $B --fp8 --beam 5 --lanes 1 --steps 1 --warmup 0 --decode-steps 8 --no-cpu-baseline) || exit 5 ;;
     pmc)
       for C in FETCH_SIZE WRITE_SIZE; do
         (cd /tmp && run pmc_$C 400 rocprofv3 --pmc $C --output-format csv -d "$O/${TAG}_pmc_$C" -o pmc -- $B --lanes 1 --steps 1 --warmup 0 --decode-steps 8 --no-cpu-baseline) || exit 5

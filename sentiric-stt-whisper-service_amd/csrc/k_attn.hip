@@ -576,7 +576,19 @@ __device__ __forceinline__ f16x8 dequant_h8(uint2 raw, uint32_t e) {
   return f16x8{a[0], a[1], b[0], b[1], c[0], c[1], d[0], d[1]};
 }
 
-template <typename T, int NQ, bool KV8 = false, bool NTL = true, int NBC = 0>
+// MFS (MX-fp8 cache only, MWX_XATTN_MFS): the scores on MFMA instead of
+// v_dot2 chains. A 16-key tile is the A operand of two
+// v_mfma_f32_16x16x32_f16 (one per 32-element scale half; lane l holds key
+// l&15's 8 codes at e = 8(l>>4) .. +7 of that half, widened to f16 unscaled:
+// e4m3 codes are f16-exact), the queries (f16, rows >= NQ zero) the B
+// operand; lane l receives query l&15's dot products with keys 4(l>>4) .. +3
+// of the tile per half, which the two E8M0 scales of each key combine:
+// score = (s0 * dot0 + s1 * dot1) * scale (scales are powers of two, so this
+// is the dot product of the dequantized values up to the order of the f32
+// sums). A query's scores depend only on its own row, so results do not depend
+// on the group size NQ. Each wave streams its tiles (wave w: w, w + 4, ...)
+// four at a time, two groups in flight. Softmax and P.V are the kernel's own.
+template <typename T, int NQ, bool KV8 = false, bool NTL = true, int NBC = 0, bool MFS = false>
 __global__ __launch_bounds__(256) void dec_xattn_kernel(
     const float* __restrict__ P, int KS, int pcols, const float* __restrict__ bias,
     const void* __restrict__ kbase, const void* __restrict__ vbase,
@@ -655,7 +667,40 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
   // the bias is requested with the slabs (after the key loads, the query
   // would wait for them)
   const float bq = bias[h * 64 + (tid & 63)];
-  if constexpr (KV8) {
+  // MFS: key tiles in flight (TD tiles of 2 x 8 code bytes + 4 scale pairs)
+  constexpr int TD = 4;
+  const int ntile = (n + 15) >> 4;
+  const int mrow = lane & 15, gq = lane >> 4;
+  uint2 kr[MFS ? 2 : 1][MFS ? TD : 1][2];
+  uint32_t ksr[MFS ? 2 : 1][MFS ? TD : 1][2];
+  auto mfs_load = [&](int buf, int grp) {  // tiles wid + 4 * (TD * grp + i)
+#pragma unroll
+    for (int i = 0; i < TD; ++i) {
+      const int t = min(wid + 4 * (TD * grp + i), ntile - 1);
+      const uint8_t* row = K8 + (long)min(t * 16 + mrow, jmax) * 64 + 8 * gq;
+      const u32x2 a = ld_stream<NTL>(reinterpret_cast<const u32x2*>(row));
+      const u32x2 b = ld_stream<NTL>(reinterpret_cast<const u32x2*>(row + 32));
+      kr[buf][i][0] = uint2{a[0], a[1]};
+      kr[buf][i][1] = uint2{b[0], b[1]};
+      const int k0 = t * 16 + 4 * gq;  // the lane's 4 output keys (scale pairs)
+      if (k0 + 3 <= jmax) {
+        const u32x2 sp = *reinterpret_cast<const u32x2*>(KS8 + (long)k0 * 2);
+        ksr[buf][i][0] = sp[0];
+        ksr[buf][i][1] = sp[1];
+      } else {
+        uint32_t w[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          w[r] = *reinterpret_cast<const uint16_t*>(KS8 + (long)min(k0 + r, jmax) * 2);
+        ksr[buf][i][0] = w[0] | (w[1] << 16);
+        ksr[buf][i][1] = w[2] | (w[3] << 16);
+      }
+    }
+  };
+  const int ngrp = ((ntile + 3) / 4 + TD - 1) / TD;  // (tile groups per wave, upper bound)
+  if constexpr (MFS) {
+    mfs_load(0, 0);
+  } else if constexpr (KV8) {
     LOADROWS8(qa, sa, K8, KS8, 0, 0)
   } else {
     LOADROWS16(ka, K, 0, 0)
@@ -719,7 +764,43 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
       score_batch(kb2, b, 1);
     }
   };
-  if constexpr (NBC > 0) {
+  if constexpr (MFS) {
+    // B operand: query l&15 at e = 8(l>>4) + j (half 0) and 32 + 8(l>>4) + j
+    f16x8 qb0, qb1;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      qb0[j] = mrow < NQ ? (_Float16)sq[min(mrow, NQ - 1)][8 * gq + j] : (_Float16)0.0f;
+      qb1[j] = mrow < NQ ? (_Float16)sq[min(mrow, NQ - 1)][32 + 8 * gq + j] : (_Float16)0.0f;
+    }
+    auto e8m0 = [](uint32_t e) { return e ? __uint_as_float(e << 23) : __uint_as_float(0x00400000u); };
+    auto score_tile = [&](int buf, int i, int t) {
+      const f16x8 a0 = dequant_h8(kr[buf][i][0], 127u), a1 = dequant_h8(kr[buf][i][1], 127u);
+      const f32x4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+      const f32x4 d0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, qb0, z, 0, 0, 0);
+      const f32x4 d1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, qb1, z, 0, 0, 0);
+      if (mrow < NQ && t < ntile) {
+        f32x4 out;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t sp = (ksr[buf][i][r >> 1] >> (16 * (r & 1))) & 0xffffu;
+          out[r] = (e8m0(sp & 0xffu) * d0[r] + e8m0(sp >> 8) * d1[r]) * scale;
+        }
+        *reinterpret_cast<f32x4*>(&sc[min(mrow, NQ - 1)][t * 16 + 4 * gq]) = out;
+      }
+    };
+#pragma unroll 1
+    for (int grp = 0; grp < ngrp; grp += 2) {
+      if (grp + 1 < ngrp) mfs_load(1, grp + 1);
+#pragma unroll
+      for (int i = 0; i < TD; ++i) score_tile(0, i, wid + 4 * (TD * grp + i));
+      if (grp + 2 < ngrp) mfs_load(0, grp + 2);
+      if (grp + 1 < ngrp) {
+#pragma unroll
+        for (int i = 0; i < TD; ++i) score_tile(1, i, wid + 4 * (TD * (grp + 1) + i));
+      }
+    }
+    LOADROWS8(qa, sa, V8, VS8, 0, 0)
+  } else if constexpr (NBC > 0) {
 #pragma unroll 1
     for (int b = 0; b < NBC - 1; ++b) k_trip(b, false);
     k_trip(NBC - 1, true);
@@ -1106,10 +1187,15 @@ bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float*
       default: return false;
     }
   }
+  // MX-fp8 cache: scores on MFMA (MWX_XATTN_MFS=1; A/B against the v_dot2 scores)
+  static const bool mfs = getenv("MWX_XATTN_MFS") && atoi(getenv("MWX_XATTN_MFS")) != 0;
   switch (nq) {
 #define XQ(N)                                  \
   case N:                                      \
-    if (kv8 && nt)                             \
+    if (kv8 && mfs)                            \
+      dec_xattn_kernel<T, N, true, true, 0, true><<<g, 256, 0, st>>>(P, KS, pcols, bias, kbase, \
+          vbase, kscale8, vscale8, kv_index, active, n_keys, cap, R, o, H, scale);             \
+    else if (kv8 && nt)                        \
       XL(N, true, true);                       \
     else if (kv8)                              \
       XL(N, true, false);                      \
