@@ -70,11 +70,11 @@ for s in "$@"; do
     b5) run b5 500 python -u bench.py --beam 5 --steps 4 --warmup 1 --no-cpu-baseline ;;
     c5) run c5 700 python -u bench.py --fp8 --beam 5 --clip-seconds 600 --steps 2 --warmup 1 --no-cpu-baseline ;;
     prompt) run prompt 700 python -u bench.py --prompt-leg --steps 2 --warmup 1 --no-cpu-baseline ;;
-    prof) (cd /tmp && run prof 600 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_prof" -o prof -- $B --steps 4 --warmup 2 --no-cpu-baseline) || exit 4 ;;
-    prof1) (cd /tmp && run prof1 600 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_prof1" -o prof -- $B --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline) || exit 4 ;;
-    profc2) (cd /tmp && run profc2 400 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_profc2" -o prof -- $B --arch base --wtype f16 --clips 1 --lanes 1 --steps 5 --warmup 2 --no-cpu-baseline) || exit 4 ;;
-    profb5) (cd /tmp && run profb5 600 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_profb5" -o prof -- $B --beam 5 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline) || exit 4 ;;
-    profc5) (cd /tmp && run profc5 700 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_profc5" -o prof -- $B --fp8 --beam 5 --lanes 1 --steps 1 --warmup 0 --no-cpu-baseline) || exit 4 ;;
+    prof) (cd /tmp && run prof 600 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_prof" -o prof -- $B --steps 4 --warmup 2 --no-cpu-baseline) || exit 4; python3 scripts/prof_box.py "$O/${TAG}_prof" || exit 4 ;;
+    prof1) (cd /tmp && run prof1 600 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_prof1" -o prof -- $B --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline) || exit 4; python3 scripts/prof_box.py "$O/${TAG}_prof1" || exit 4 ;;
+    profc2) (cd /tmp && run profc2 400 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_profc2" -o prof -- $B --arch base --wtype f16 --clips 1 --lanes 1 --steps 5 --warmup 2 --no-cpu-baseline) || exit 4; python3 scripts/prof_box.py "$O/${TAG}_profc2" || exit 4 ;;
+    profb5) (cd /tmp && run profb5 600 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_profb5" -o prof -- $B --beam 5 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline) || exit 4; python3 scripts/prof_box.py "$O/${TAG}_profb5" || exit 4 ;;
+    profc5) (cd /tmp && run profc5 700 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_profc5" -o prof -- $B --fp8 --beam 5 --clip-seconds 60 --lanes 1 --steps 1 --warmup 0 --no-cpu-baseline) || exit 4; python3 scripts/prof_box.py "$O/${TAG}_profc5" || exit 4 ;;
     pmcb5)  # instruction mix / stall counters of the beam-5 (and fp8) kernels
       (cd /tmp && run pmcb5 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d "$O/${TAG}_pmcb5" -o pmc -- $B --beam 5 --lanes 1 --steps 1 --warmup 0 --decode-steps 8 --no-cpu-baseline) || exit 5
       (cd /tmp && run pmcc5 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d "$O/${TAG}_pmcc5" -o pmc -- $B --fp8 --beam 5 --lanes 1 --steps 1 --warmup 0 --decode-steps 8 --no-cpu-baseline) || exit 5 ;;

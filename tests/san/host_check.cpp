@@ -139,10 +139,16 @@ void batched(const char* dir) {
   std::vector<std::string> got(12);
   std::vector<int> rc(12);
   std::vector<std::thread> th;
+  // inputs made first and the requests released together, so they arrive
+  // within the batching window even on a loaded host (sanitizer builds)
+  std::vector<std::vector<int16_t>> pcm;
+  for (int t = 0; t < 12; ++t) pcm.push_back(clip(100 + t, 16000 * (3 + t % 4)));
+  std::atomic<int> ready{0};
   for (int t = 0; t < 12; ++t)
     th.emplace_back([&, t] {
-      rc[t] = transcribe(eng, clip(100 + t, 16000 * (3 + t % 4)), 16000, t % 2 ? 5 : 1,
-                         t == 5 ? 1 : -1, nullptr, &got[t]);
+      ready.fetch_add(1);
+      while (ready.load() < 12) std::this_thread::yield();
+      rc[t] = transcribe(eng, pcm[t], 16000, t % 2 ? 5 : 1, t == 5 ? 1 : -1, nullptr, &got[t]);
     });
   for (auto& x : th) x.join();
   for (int t = 0; t < 12; ++t) {
