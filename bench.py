@@ -593,6 +593,9 @@ def main():
     ap.add_argument("--lane-stagger", type=float, default=0.0,
                     help="seconds lane i waits (x i) before its first timed batch")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-one-lane", action="store_true",
+                    help="skip the one-lane pass after the timed region (a kernel trace of the "
+                         "run then holds the multi-lane launches only)")
     ap.add_argument("--fp8", action="store_true",
                     help="MX-fp8 compute (C5): encoder, cross-K/V and decoder weight GEMMs, cross K/V cache")
     ap.add_argument("--host-input", action="store_true",
@@ -717,6 +720,11 @@ def main():
     classes = [args.perf_class] + (["enc_gemm"] if args.perf_class != "enc_gemm" else [])
     if args.perf_class.startswith("dec_attn"):
         classes.append("event_bracket")
+    # launch spans (device clock stamps of the first workgroup start and the
+    # last workgroup end, kcommon.h span_start): the duration a kernel trace
+    # measures, without the dispatch queueing behind the other lane's kernels
+    # that an event bracket includes
+    classes += [c + ".span" for c in (args.perf_class, "enc_gemm") if c in classes]
     for so in owners:
         L.mwx_perf_read(so, None, None)
         L.mwx_perf_enable(so, ",".join(classes).encode())
@@ -757,7 +765,7 @@ def main():
                    "tokens_per_clip": round(sum(tok_count) / args.steps / args.clips, 1),
                    "windows_per_clip": n_windows if args.decode_steps else None}
     timed_1lane, steps_1lane, elapsed_1lane = None, 0, None
-    if lanes > 1:
+    if lanes > 1 and not args.no_one_lane:
         # after the timed region (not part of `value`): the same batches on one
         # lane (B = 32 strictly one batch at a time), timed and with the
         # kernels' rooflines measured without another lane's kernels sharing
@@ -789,7 +797,10 @@ def main():
         ev_s = None
         if tm.get("event_bracket", (0, 0))[1] > 0:
             ev_s = tm["event_bracket"][0] / 1e3 / tm["event_bracket"][1]
-        avg_s = avg_raw - ev_s if ev_s is not None and ev_s < 0.5 * avg_raw else avg_raw
+        avg_ev = avg_raw - ev_s if ev_s is not None and ev_s < 0.5 * avg_raw else avg_raw
+        sp = tm.get(args.perf_class + ".span", (0.0, 0))
+        avg_span = sp[0] / 1e3 / sp[1] if sp[1] > 0 else None
+        avg_s = avg_span if avg_span is not None else avg_ev
         # decode kernels run per row group (MWX_DECODE_GROUPS chains on their
         # own streams, default 1); the engine times every 8th decode step's
         # launches (MWX_PERF_PERIOD), all inside the timed region
@@ -821,6 +832,10 @@ def main():
                     "unit": "TFLOP/s", "frac": round(achieved / MFMA_PEAK_TFLOPS, 4),
                     "traffic": traffic}
         roof.update({"kernel": args.perf_class, "avg_launch_us": round(avg_s * 1e6, 2),
+                     "timing": "launch span (device clock)" if avg_span is not None
+                               else "event bracket - event cost",
+                     "span_launches": sp[1],
+                     "avg_bracket_minus_events_us": round(avg_ev * 1e6, 2),
                      "avg_bracket_us": round(avg_raw * 1e6, 2),
                      "event_bracket_us": round(ev_s * 1e6, 2) if ev_s is not None else None,
                      "launches": tm[args.perf_class][1], "work_per_launch": work,
@@ -832,11 +847,17 @@ def main():
                                            en // max(1, nsteps), prompt_len, args.decode_steps,
                                            n_windows)
             eavg = ems / 1e3 / en
+            esp = tm.get("enc_gemm.span", (0.0, 0))
+            eavg_ev = eavg
+            if esp[1] == en:
+                eavg = esp[0] / 1e3 / esp[1]
             epeak = 2 * MFMA_PEAK_TFLOPS if args.fp8 else MFMA_PEAK_TFLOPS
             each = ework / eavg / 1e12
             roof_enc = {"bound": "mfma", "achieved": round(each, 1), "peak": epeak,
                         "unit": "TFLOP/s", "frac": round(each / epeak, 4), "kernel": "enc_gemm",
                         "avg_launch_us": round(eavg * 1e6, 2), "launches": en,
+                        "timing": "launch span (device clock)" if esp[1] == en else "event bracket",
+                        "avg_bracket_us": round(eavg_ev * 1e6, 2),
                         "work_per_launch": ework, "work_desc": edesc}
         return roof, roof_enc
 

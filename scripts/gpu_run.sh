@@ -15,6 +15,7 @@
 #   pair32 / pair32x2  one 32-clip batch per lane split into two interleaved 16-row sets
 #   mfstest    the MX-fp8 tests with the MFMA-score cross-attention (MWX_XATTN_MFS=1)
 #   c5mfs / c5one  C5 on one lane with / without the MFMA scores
+#   bench1np / bench1g0  one lane without the prompt prefill / with row-major encoder tile order
 #   pairtest   the paired-decode parity tests only
 #   b5         beam 5 (service default decode), C3 shape
 #   c5         C5: MX-fp8, beam 5, 600-s long-form clips
@@ -66,11 +67,13 @@ for s in "$@"; do
     mfstest) run mfstest 600 env MWX_XATTN_MFS=1 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shapes.py -k "mxfp8" -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
     c5mfs) run c5mfs 700 env MWX_XATTN_MFS=1 python -u bench.py --fp8 --beam 5 --clip-seconds 600 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline ;;
     c5one) run c5one 700 python -u bench.py --fp8 --beam 5 --clip-seconds 600 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline ;;
+    bench1np) run bench1np 400 env MWX_PREFILL_MIN=0 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
+    bench1g0) run bench1g0 400 env MWX_GEMM_GROUP=0 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
     pairtest) run pairtest 600 python -u -m pytest tests/test_gpu_pair.py -m gpu -x -v -s -rf --timeout 300 --timeout-method thread ;;
     b5) run b5 500 python -u bench.py --beam 5 --steps 4 --warmup 1 --no-cpu-baseline ;;
     c5) run c5 700 python -u bench.py --fp8 --beam 5 --clip-seconds 600 --steps 2 --warmup 1 --no-cpu-baseline ;;
     prompt) run prompt 700 python -u bench.py --prompt-leg --steps 2 --warmup 1 --no-cpu-baseline ;;
-    prof) (cd /tmp && run prof 600 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_prof" -o prof -- $B --steps 4 --warmup 2 --no-cpu-baseline) || exit 4; python3 scripts/prof_box.py "$O/${TAG}_prof" || exit 4 ;;
+    prof) (cd /tmp && run prof 600 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_prof" -o prof -- $B --steps 4 --warmup 2 --no-cpu-baseline --no-one-lane) || exit 4; python3 scripts/prof_box.py "$O/${TAG}_prof" || exit 4 ;;
     prof1) (cd /tmp && run prof1 600 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_prof1" -o prof -- $B --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline) || exit 4; python3 scripts/prof_box.py "$O/${TAG}_prof1" || exit 4 ;;
     profc2) (cd /tmp && run profc2 400 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_profc2" -o prof -- $B --arch base --wtype f16 --clips 1 --lanes 1 --steps 5 --warmup 2 --no-cpu-baseline) || exit 4; python3 scripts/prof_box.py "$O/${TAG}_profc2" || exit 4 ;;
     profb5) (cd /tmp && run profb5 600 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_profb5" -o prof -- $B --beam 5 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline) || exit 4; python3 scripts/prof_box.py "$O/${TAG}_profb5" || exit 4 ;;

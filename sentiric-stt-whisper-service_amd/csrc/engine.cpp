@@ -251,6 +251,17 @@ struct State {
   bool capture_perf = true;  // false while capturing the uninstrumented step graph
   std::vector<double> perf_acc_ms;
   std::vector<long> perf_acc_n;
+  // launch spans (classes "<class>.span", kcommon.h span_start): device stamp
+  // pairs [SPAN_SLOTS][2], graph slots first (zeroed by one memset node at the
+  // head of each instrumented graph), eager slots after them (zeroed per
+  // launch); the class of each slot; a pinned host copy and its stream
+  static constexpr int SPAN_G = 2048, SPAN_E = 2048;
+  DBuf perf_span;
+  unsigned long long* span_host = nullptr;
+  hipStream_t span_stream = nullptr;
+  std::vector<int> span_gtag, span_etag;
+  size_t span_gused = 0, span_eused = 0;
+  double span_tick_ms = 0.0;  // ms per s_memrealtime tick
 };
 
 static void harvest_events(std::vector<hipEvent_t>& ev, const std::vector<int>& tag, size_t used,
@@ -264,6 +275,31 @@ static void harvest_events(std::vector<hipEvent_t>& ev, const std::vector<int>& 
   }
 }
 
+static int perf_class_index(const State& S, const char* cls);
+
+// Launch spans: accumulate the (end - start) of the used slots of one region
+// into their classes (graph: after an instrumented replay has completed;
+// eager: after the state's stream has drained)
+static void harvest_spans(State& S, bool graph) {
+  const size_t n = graph ? S.span_gused : S.span_eused;
+  if (n == 0 || !S.span_host) return;
+  const size_t base = graph ? 0 : State::SPAN_G;
+  HIPC(hipMemcpyAsync(S.span_host, (unsigned long long*)S.perf_span.p + 2 * base, n * 16,
+                      hipMemcpyDeviceToHost, S.span_stream));
+  HIPC(hipStreamSynchronize(S.span_stream));
+  const std::vector<int>& tag = graph ? S.span_gtag : S.span_etag;
+  for (size_t i = 0; i < n; ++i) {
+    const unsigned long long a = S.span_host[2 * i], b = S.span_host[2 * i + 1];
+    if (a == 0 || b == 0) continue;  // (not launched)
+    const unsigned long long t0 = ~a;
+    if (b < t0) continue;
+    const int c = tag[i];
+    S.perf_acc_ms[c] += (double)(b - t0) * S.span_tick_ms;
+    S.perf_acc_n[c] += 1;
+  }
+  if (!graph) S.span_eused = 0;
+}
+
 static int perf_class_index(const State& S, const char* cls) {
   for (size_t i = 0; i < S.perf_classes.size(); ++i)
     if (S.perf_classes[i] == cls) return (int)i;
@@ -274,6 +310,34 @@ static int perf_class_index(const State& S, const char* cls) {
 static bool perf_on(const State& s, const char* cls) {
   if (s.perf_class.empty() || (s.capturing && !s.capture_perf)) return false;
   return perf_class_index(s, cls) >= 0;
+}
+
+// The stamp pair a launch of class `cls` writes its span to (kcommon.h
+// span_start / span_end) when "<cls>.span" is an enabled perf class, else
+// nullptr. Queued on the launch's stream: in an instrumented graph capture the
+// first slot adds one memset node zeroing every graph slot; eagerly, the
+// slot's 16 bytes are zeroed before the launch.
+static unsigned long long* span_slot(State& S, const char* cls, hipStream_t s) {
+  if (S.perf_class.empty() || (S.capturing && !S.capture_perf) || !S.perf_span.p) return nullptr;
+  const int ci = perf_class_index(S, (std::string(cls) + ".span").c_str());
+  if (ci < 0) return nullptr;
+  unsigned long long* base = (unsigned long long*)S.perf_span.p;
+  if (S.capturing) {
+    if (S.span_gused >= (size_t)State::SPAN_G) return nullptr;
+    if (S.span_gused == 0) HIPC(hipMemsetAsync(base, 0, (size_t)State::SPAN_G * 16, s));
+    if (S.span_gtag.size() <= S.span_gused) S.span_gtag.resize(S.span_gused + 1);
+    S.span_gtag[S.span_gused] = ci;
+    return base + 2 * S.span_gused++;
+  }
+  if (S.span_eused >= (size_t)State::SPAN_E) {
+    HIPC(hipStreamSynchronize(s));
+    harvest_spans(S, false);
+  }
+  unsigned long long* p = base + 2 * (State::SPAN_G + S.span_eused);
+  HIPC(hipMemsetAsync(p, 0, 16, s));
+  if (S.span_etag.size() <= S.span_eused) S.span_etag.resize(S.span_eused + 1);
+  S.span_etag[S.span_eused++] = ci;
+  return p;
 }
 
 // Records a start/stop HIP event pair around a launch when `cls` is the
@@ -788,6 +852,7 @@ struct Driver {
     e.ldc = d;
     e.c_bstride = (long)(T2 + 2) * d;
     { PerfScope ps(S, "enc_gemm", st);
+      e.span = span_slot(S, "enc_gemm", st);
     gemm<_Float16>(EPI_GELU, true, melT, cp, (long)(T2 + 2) * cp, C.conv1_w, 3 * cp, T2, d,
                    3 * cp, nb, e, st); }
     // conv2 (k3 s2 p1) + GELU + positional embedding -> residual stream x
@@ -798,6 +863,7 @@ struct Driver {
     e.c_bstride = (long)Lc * d;
     e.pe = C.enc_pe;
     { PerfScope ps(S, "enc_gemm", st);
+      e.span = span_slot(S, "enc_gemm", st);
     gemm<_Float16>(EPI_CONV2, false, h1p, 2 * d, (long)(T2 + 2) * d, C.conv2_w, 3 * d, Lc, d,
                    3 * d, nb, e, st); }
     const float kq_scale = 1.0f / sqrtf(64.0f);
@@ -829,6 +895,7 @@ struct Driver {
       e.d = d;
       e.ldv = Lp;  // V^T rows are padded to Lp (16-B aligned tile loads)
       { PerfScope ps(S, "enc_gemm", st);
+      e.span = span_slot(S, "enc_gemm", st);
       mgemm(EPI_ENC_QKV, h, d, W.qkv_x, W.qkv_w, 3 * d, e); }
       { PerfScope ps(S, "enc_attn", st);
       enc_attention<T>(q, k, vt, o, nb, H, Lc, kq_scale, st); }
@@ -838,6 +905,7 @@ struct Driver {
       e.r32 = x;
       e.ldc = d;
       { PerfScope ps(S, "enc_gemm", st);
+      e.span = span_slot(S, "enc_gemm", st);
       mgemm(EPI_RES, o, d, W.o_x, W.o_w, d, e); }
       layer_norm<T>(x, W.ln2_w, W.ln2_b, h, M, d, nullptr, st);
       e = EpiParams();
@@ -845,6 +913,7 @@ struct Driver {
       e.c16 = ff;
       e.ldc = 4 * d;
       { PerfScope ps(S, "enc_gemm", st);
+      e.span = span_slot(S, "enc_gemm", st);
       mgemm(EPI_GELU, h, d, W.fc1_x, W.fc1_w, 4 * d, e); }
       e = EpiParams();
       e.bias = W.fc2_b;
@@ -852,6 +921,7 @@ struct Driver {
       e.r32 = x;
       e.ldc = d;
       { PerfScope ps(S, "enc_gemm", st);
+      e.span = span_slot(S, "enc_gemm", st);
       mgemm(EPI_RES, ff, 4 * d, W.fc2_x, W.fc2_w, d, e); }
     }
     layer_norm<T>(x, C.enc_ln_w, C.enc_ln_b, enc, M, d, nullptr, st);
@@ -1146,7 +1216,7 @@ struct Driver {
                        (_Float16*)S.cross_k.p + l * layer_cross,
                        (_Float16*)S.cross_v.p + l * layer_cross, rw.xidx, rw.pos, rw.act,
                        hp.n_audio_ctx, hp.n_audio_ctx, rw.od, n, H, kqs, s, nullptr, nullptr, 0,
-                       nq);
+                       nq, 1, rw.prefill ? nullptr : span_slot(S, "dec_attn_cross", s));
     }
   }
   void layer_post(const LayerRows& rw, LayerRun& c, int l, hipStream_t s) {

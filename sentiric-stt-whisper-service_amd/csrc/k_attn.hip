@@ -285,12 +285,13 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
     const int* __restrict__ kv_index, const int* __restrict__ pos, const int* __restrict__ active,
     int fixed_len, int cap, T* __restrict__ o, int H, float scale,
     const int* __restrict__ kvmap, const int* __restrict__ own_from, int map_row0, int nq,
-    int R, int write_new = 1) {
+    int R, int write_new = 1, unsigned long long* span = nullptr) {
   __shared__ float sc[DEC_MAX_KEYS];
   __shared__ float redf[4];
   __shared__ double redd[4];
   __shared__ float pv[4][64][9];
   __shared__ float sq[64], snk[64], snv[64];
+  span_start(span);
   int row = blockIdx.y, h = blockIdx.x;
   if (nq > 1) {
     // nq rows per clip (beam / best-of decoders: cross, the same K/V; self,
@@ -301,7 +302,10 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
     // others from that XCD's L2
     const int L = blockIdx.x, W = 8 * nq;
     const int q = (L % W) / 8, g = (L / W) * 8 + L % 8;
-    if (g >= (R / nq) * H) return;
+    if (g >= (R / nq) * H) {
+      span_end(span);
+      return;
+    }
     row = (g / H) * nq + q;
     h = g % H;
   }
@@ -312,7 +316,10 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
   const int slot = kv_index ? kv_index[row] : row;
   const int own0 = SELF && own_from ? own_from[row] : 0;
   asm volatile("" ::"s"(act_r), "s"(p_row), "s"(slot), "s"(own0));
-  if (!act_r) return;
+  if (!act_r) {
+    span_end(span);
+    return;
+  }
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int kg = lane >> 3, c = lane & 7;
   const int n = SELF ? p_row + 1 : fixed_len;
@@ -551,6 +558,7 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
     const float r = (pv[0][cc][e] + pv[1][cc][e]) + (pv[2][cc][e] + pv[3][cc][e]);
     o[pack_index(row, h * 64 + cc * 8 + e, D)] = to_t<T>(r);
   }
+  span_end(span);
 }
 
 // Cross-attention of NQ rows that share one clip's cross K/V (the decoders
@@ -1187,8 +1195,9 @@ bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float*
       default: return false;
     }
   }
-  // MX-fp8 cache: scores on MFMA (MWX_XATTN_MFS=1; A/B against the v_dot2 scores)
-  static const bool mfs = getenv("MWX_XATTN_MFS") && atoi(getenv("MWX_XATTN_MFS")) != 0;
+  // MX-fp8 cache: scores on MFMA (default; MWX_XATTN_MFS=0: the v_dot2 scores,
+  // the A/B: C5 one lane 735.8 -> 778.8 audio-s/s, 52.4 -> 44.6 us per launch)
+  static const bool mfs = !(getenv("MWX_XATTN_MFS") && atoi(getenv("MWX_XATTN_MFS")) == 0);
   switch (nq) {
 #define XQ(N)                                  \
   case N:                                      \
@@ -1274,7 +1283,7 @@ void dec_attention(const float* P, int KS, int pcols, const float* bias, float q
                    float kscale, _Float16* kbase, _Float16* vbase, const int* kv_index,
                    const int* pos, const int* active, int fixed_len, int kv_len_cap, T* o, int R,
                    int H, float scale, hipStream_t st, const int* kvmap, const int* own_from,
-                   int map_row0, int nq, int write_new) {
+                   int map_row0, int nq, int write_new, unsigned long long* span) {
   dim3 g(H, R);
   if (nq > 1 && R % nq == 0) {
     const int groups = (R / nq) * H;
@@ -1301,7 +1310,7 @@ void dec_attention(const float* P, int KS, int pcols, const float* bias, float q
     dec_attn_kernel<T, true, 4><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale, kbase,
                                                    vbase, kv_index, pos, active, fixed_len,
                                                    kv_len_cap, o, H, scale, kvmap, own_from,
-                                                   map_row0, nq, R, write_new);
+                                                   map_row0, nq, R, write_new, span);
   else if (fixed_len == 0)
     dec_attn_kernel<T, true><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale, kbase, vbase,
                                                 kv_index, pos, active, fixed_len, kv_len_cap, o,
@@ -1311,22 +1320,22 @@ void dec_attention(const float* P, int KS, int pcols, const float* bias, float q
     dec_attn_kernel<T, false, 8, true, 6><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale,
                                                              kbase, vbase, kv_index, pos, active,
                                                              fixed_len, kv_len_cap, o, H, scale,
-                                                             nullptr, nullptr, 0, nq, R);
+                                                             nullptr, nullptr, 0, nq, R, 1, span);
   else if (fixed_len == 1500 && xattn_nbc)
     dec_attn_kernel<T, false, 8, false, 6><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale,
                                                               kbase, vbase, kv_index, pos, active,
                                                               fixed_len, kv_len_cap, o, H, scale,
-                                                              nullptr, nullptr, 0, nq, R);
+                                                              nullptr, nullptr, 0, nq, R, 1, span);
   else if (xattn_nt)
     dec_attn_kernel<T, false, 8, true><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale,
                                                           kbase, vbase, kv_index, pos, active,
                                                           fixed_len, kv_len_cap, o, H, scale,
-                                                          nullptr, nullptr, 0, nq, R);
+                                                          nullptr, nullptr, 0, nq, R, 1, span);
   else
     dec_attn_kernel<T, false, 8, false><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale,
                                                            kbase, vbase, kv_index, pos, active,
                                                            fixed_len, kv_len_cap, o, H, scale,
-                                                           nullptr, nullptr, 0, nq, R);
+                                                           nullptr, nullptr, 0, nq, R, 1, span);
 }
 
 template void enc_attention<_Float16>(const _Float16*, const _Float16*, const _Float16*, _Float16*,
@@ -1336,10 +1345,10 @@ template void enc_attention<__bf16>(const _Float16*, const _Float16*, const _Flo
 template void dec_attention<_Float16>(const float*, int, int, const float*, float, float,
                                       _Float16*, _Float16*, const int*, const int*, const int*, int,
                                       int, _Float16*, int, int, float, hipStream_t, const int*,
-                                      const int*, int, int, int);
+                                      const int*, int, int, int, unsigned long long*);
 template void dec_attention<__bf16>(const float*, int, int, const float*, float, float, _Float16*,
                                     _Float16*, const int*, const int*, const int*, int, int,
                                     __bf16*, int, int, float, hipStream_t, const int*, const int*, int, int,
-                                    int);
+                                    int, unsigned long long*);
 
 }  // namespace mwx

@@ -177,6 +177,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
   constexpr int GDA = BM / RPI / 8, GDB = BN / RPI / 8;          // DMA instructions per wave per tile
   // chunk swizzle: 16 consecutive rows read one chunk column conflict-free
   auto swz = [](int row) { return CPR == 8 ? (row & 7) : ((row >> 2) & 3); };
+  span_start(P.span);
   const TE* A = reinterpret_cast<const TE*>(Av);
   const TE* W = reinterpret_cast<const TE*>(Wv);
   // one __shared__ array only (a second one can make hipcc drain the LDS DMA
@@ -362,7 +363,10 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
     // Epilogue through LDS: the ring is idle now; each wave stages its 128x64
     // tile (16 KB) so every global store is a 16-B (8-B for V^T) vector.
     __builtin_amdgcn_s_barrier();  // all waves are past their last ring read
-    if (wc0 >= N) return;          // (N % 64 == 0: a wave's 64 columns are all in or all out)
+    if (wc0 >= N) {                // (N % 64 == 0: a wave's 64 columns are all in or all out)
+      span_end(P.span);
+      return;
+    }
     uint16_t* wl = reinterpret_cast<uint16_t*>(&lds[0][0]) + wid * 8192;
     float* wlf = reinterpret_cast<float*>(wl);
     if constexpr (STAGED16) {
@@ -519,6 +523,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
     }
+    span_end(P.span);
     return;
   }
 #pragma unroll
@@ -532,6 +537,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
         if (m < M && n < N) epi_store<EPI, T, OUT16>(P, bz, m, n, acc[i][j][r]);
       }
     }
+  span_end(P.span);
 }
 
 // ---------------------------------------------------------------------------

@@ -162,4 +162,19 @@ __device__ __forceinline__ float wave_max_dpp(float v) {
                      __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(v), 48))));
 }
 
+// Launch span stamps (perf classes "<class>.span", engine.cpp span_slot): the
+// earliest workgroup start and the latest workgroup end of a launch on the
+// constant-rate device clock (s_memrealtime), i.e. the launch's duration as a
+// kernel trace measures it, without the queueing in front of it that a HIP
+// event bracket also counts when another stream's kernels hold the CUs.
+// span[0] = max over workgroups of ~start (= ~earliest start), span[1] = max
+// of the ends; both zeroed before the launch. One vector atomic per workgroup
+// and stamp (thread 0 of the workgroup / of wave 0).
+__device__ __forceinline__ void span_start(unsigned long long* span) {
+  if (span && threadIdx.x == 0) atomicMax(span, ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+__device__ __forceinline__ void span_end(unsigned long long* span) {
+  if (span && threadIdx.x == 0) atomicMax(span + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+
 }  // namespace mwx

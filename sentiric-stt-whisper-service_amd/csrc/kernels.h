@@ -43,6 +43,7 @@ struct EpiParams {
   float qscale = 1.0f;
   bool pack_out = false;  // EPI_GELU: write the output as decode-GEMM A tiles (pack_index, K = ldc)
   // MX-fp8 GEMMs: E8M0 scales [rows][K/32] of A (per grid.z batch stride) and W
+  unsigned long long* span = nullptr;  // launch span stamps (perf; kcommon.h span_start)
   const uint8_t* sa = nullptr;
   long sa_bstride = 0;
   const uint8_t* sw = nullptr;
@@ -200,7 +201,7 @@ void dec_attention(const float* P, int KS, int pcols, const float* bias, float q
                    const int* pos, const int* active, int fixed_len, int kv_len_cap, T* o, int R,
                    int H, float scale, hipStream_t st, const int* kvmap = nullptr,
                    const int* own_from = nullptr, int map_row0 = 0, int nq = 1,
-                   int write_new = 1);
+                   int write_new = 1, unsigned long long* span = nullptr);
 
 // Prompt prefill: K / V of every row (reduced from the QKV slabs exactly as
 // dec_attention's self kernel reduces its own position) appended to cache row
