@@ -255,7 +255,7 @@ struct State {
   // pairs [SPAN_SLOTS][2], graph slots first (zeroed by one memset node at the
   // head of each instrumented graph), eager slots after them (zeroed per
   // launch); the class of each slot; a pinned host copy and its stream
-  static constexpr int SPAN_G = 2048, SPAN_E = 2048;
+  static constexpr int SPAN_G = 256, SPAN_E = 2048;  // slots of SPAN_SLOT_U64 u64 (1 KB)
   DBuf perf_span;
   unsigned long long* span_host = nullptr;
   hipStream_t span_stream = nullptr;
@@ -284,17 +284,21 @@ static void harvest_spans(State& S, bool graph) {
   const size_t n = graph ? S.span_gused : S.span_eused;
   if (n == 0 || !S.span_host) return;
   const size_t base = graph ? 0 : State::SPAN_G;
-  HIPC(hipMemcpyAsync(S.span_host, (unsigned long long*)S.perf_span.p + 2 * base, n * 16,
+  const size_t su = SPAN_SLOT_U64;
+  HIPC(hipMemcpyAsync(S.span_host, (unsigned long long*)S.perf_span.p + su * base, n * su * 8,
                       hipMemcpyDeviceToHost, S.span_stream));
   HIPC(hipStreamSynchronize(S.span_stream));
   const std::vector<int>& tag = graph ? S.span_gtag : S.span_etag;
   for (size_t i = 0; i < n; ++i) {
-    const unsigned long long a = S.span_host[2 * i], b = S.span_host[2 * i + 1];
-    if (a == 0 || b == 0) continue;  // (not launched)
-    const unsigned long long t0 = ~a;
-    if (b < t0) continue;
+    unsigned long long t0 = ~0ull, t1 = 0;
+    for (int sh = 0; sh < SPAN_SHARDS; ++sh) {
+      const unsigned long long a = S.span_host[su * i + 16 * sh], b = S.span_host[su * i + 16 * sh + 1];
+      if (a) t0 = std::min(t0, ~a);
+      t1 = std::max(t1, b);
+    }
+    if (t0 == ~0ull || t1 < t0) continue;  // (not launched)
     const int c = tag[i];
-    S.perf_acc_ms[c] += (double)(b - t0) * S.span_tick_ms;
+    S.perf_acc_ms[c] += (double)(t1 - t0) * S.span_tick_ms;
     S.perf_acc_n[c] += 1;
   }
   if (!graph) S.span_eused = 0;
@@ -324,17 +328,18 @@ static unsigned long long* span_slot(State& S, const char* cls, hipStream_t s) {
   unsigned long long* base = (unsigned long long*)S.perf_span.p;
   if (S.capturing) {
     if (S.span_gused >= (size_t)State::SPAN_G) return nullptr;
-    if (S.span_gused == 0) HIPC(hipMemsetAsync(base, 0, (size_t)State::SPAN_G * 16, s));
+    if (S.span_gused == 0)
+      HIPC(hipMemsetAsync(base, 0, (size_t)State::SPAN_G * SPAN_SLOT_U64 * 8, s));
     if (S.span_gtag.size() <= S.span_gused) S.span_gtag.resize(S.span_gused + 1);
     S.span_gtag[S.span_gused] = ci;
-    return base + 2 * S.span_gused++;
+    return base + SPAN_SLOT_U64 * S.span_gused++;
   }
   if (S.span_eused >= (size_t)State::SPAN_E) {
     HIPC(hipStreamSynchronize(s));
     harvest_spans(S, false);
   }
-  unsigned long long* p = base + 2 * (State::SPAN_G + S.span_eused);
-  HIPC(hipMemsetAsync(p, 0, 16, s));
+  unsigned long long* p = base + SPAN_SLOT_U64 * (State::SPAN_G + S.span_eused);
+  HIPC(hipMemsetAsync(p, 0, SPAN_SLOT_U64 * 8, s));
   if (S.span_etag.size() <= S.span_eused) S.span_etag.resize(S.span_eused + 1);
   S.span_etag[S.span_eused++] = ci;
   return p;

@@ -772,6 +772,31 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
       score_batch(kb2, b, 1);
     }
   };
+  // MFS: P.V on MFMA as well. Wave w stages its 32-key V tiles (w, w + 4, ...)
+  // in LDS (fp8 codes, 16-B chunks XOR-swizzled by (row >> 3) so a 32-lane
+  // half's byte reads hit distinct banks) and reads each lane's B operand
+  // (8 keys at one e) from there; the A operand is the query's P times the V
+  // scale of each key (per scale half), so the codes enter the MFMA unscaled
+  __shared__ __attribute__((aligned(16))) uint8_t vtile[MFS ? 4 : 1][MFS ? 32 * 64 : 16];
+  const int nt32 = (n + 31) >> 5;
+  const int vrow = lane >> 1, vch = 2 * (lane & 1);
+  u32x4 vr0, vr1, vsr;  // the next tile's bytes (rows vrow, chunks vch, vch + 1) and V scales
+  auto v_load = [&](int t) {
+    const u32x4* src = reinterpret_cast<const u32x4*>(V8 + (long)min(t * 32 + vrow, jmax) * 64) + vch;
+    vr0 = ld_stream<NTL>(src);
+    vr1 = ld_stream<NTL>(src + 1);
+    const int k0 = t * 32 + 8 * gq;  // scales of the lane's 8 A-operand keys
+    if (k0 + 7 <= jmax) {
+      vsr = *reinterpret_cast<const u32x4*>(VS8 + (long)k0 * 2);
+    } else {
+      uint32_t w[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        w[i] = (uint32_t)*reinterpret_cast<const uint16_t*>(VS8 + (long)min(k0 + 2 * i, jmax) * 2) |
+               ((uint32_t)*reinterpret_cast<const uint16_t*>(VS8 + (long)min(k0 + 2 * i + 1, jmax) * 2) << 16);
+      vsr = u32x4{w[0], w[1], w[2], w[3]};
+    }
+  };
   if constexpr (MFS) {
     // B operand: query l&15 at e = 8(l>>4) + j (half 0) and 32 + 8(l>>4) + j
     f16x8 qb0, qb1;
@@ -807,7 +832,7 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
         for (int i = 0; i < TD; ++i) score_tile(1, i, wid + 4 * (TD * (grp + 1) + i));
       }
     }
-    LOADROWS8(qa, sa, V8, VS8, 0, 0)
+    if (wid < nt32) v_load(wid);  // (in flight across the softmax)
   } else if constexpr (NBC > 0) {
 #pragma unroll 1
     for (int b = 0; b < NBC - 1; ++b) k_trip(b, false);
@@ -858,6 +883,65 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
     for (int j = tid; j < n; j += 256) sc[q][j] = (float)f16r(sc[q][j] * inv);
   }
   __syncthreads();
+  if constexpr (MFS) {
+    auto e8m0 = [](uint32_t e) { return e ? __uint_as_float(e << 23) : __uint_as_float(0x00400000u); };
+    uint8_t* vw = &vtile[0][0] + wid * (32 * 64);
+    f32x4 oacc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) oacc[i] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    const int qrow = min(mrow, NQ - 1);
+#pragma unroll 1
+    for (int t = wid; t < nt32; t += 4) {
+      {  // stage the tile (this wave's region only: in-order LDS, no barrier)
+        const int sw = (vrow >> 3) & 3;
+        *reinterpret_cast<u32x4*>(vw + vrow * 64 + ((vch ^ sw) * 16)) = vr0;
+        *reinterpret_cast<u32x4*>(vw + vrow * 64 + (((vch + 1) ^ sw) * 16)) = vr1;
+      }
+      const u32x4 sv = vsr;
+      if (t + 4 < nt32) v_load(t + 4);
+      // A operands: P'[q][key] = P x V scale of (key, half), keys t*32 + 8(l>>4) + j
+      const int kb = t * 32 + 8 * gq;
+      f16x8 pa[2];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float p = sc[qrow][min(kb + j, n - 1)];
+        if (mrow >= NQ || kb + j >= n) p = 0.0f;
+        const uint32_t sp = (sv[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+        pa[0][j] = (_Float16)(p * e8m0(sp & 0xffu));
+        pa[1][j] = (_Float16)(p * e8m0(sp >> 8));
+      }
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int e = 16 * nt + mrow;
+        uint32_t w0 = 0, w1 = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int r = 8 * gq + j;
+          const uint32_t b = vw[r * 64 + (e ^ (((r >> 3) & 3) * 16))];
+          if (j < 4) w0 |= b << (8 * j); else w1 |= b << (8 * (j - 4));
+        }
+        const f16x8 vb = dequant_h8(uint2{w0, w1}, 127u);
+        oacc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa[nt >> 1], vb, oacc[nt], 0, 0, 0);
+      }
+    }
+    // the four waves' partial sums: (w0 + w1) + (w2 + w3)
+    float* op = &pv[0][0][0];  // [4][NQ][64] floats (pv holds 4 x 64 x 9)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int q = 4 * gq + r;
+        if (q < NQ) op[(wid * NQ + q) * 64 + 16 * nt + mrow] = oacc[nt][r];
+      }
+    __syncthreads();
+    for (int i = tid; i < NQ * 64; i += 256) {
+      const int q = i >> 6, e = i & 63;
+      const float r = (op[q * 64 + e] + op[(NQ + q) * 64 + e]) +
+                      (op[(2 * NQ + q) * 64 + e] + op[(3 * NQ + q) * 64 + e]);
+      if (act[q]) o[pack_index(row0 + q, h * 64 + e, D)] = to_t<T>(r);
+    }
+    return;
+  }
   float acc[NQ][8];
 #pragma unroll
   for (int q = 0; q < NQ; ++q)

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "kernels.h"
+
 namespace mwx {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -13,6 +15,7 @@ typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // 16-/8-byte loads of bytes one CU reads once per launch (the decode cross K/V
 // streams): NT = non-temporal (`nt` cache policy), which keeps them from
@@ -166,15 +169,23 @@ __device__ __forceinline__ float wave_max_dpp(float v) {
 // earliest workgroup start and the latest workgroup end of a launch on the
 // constant-rate device clock (s_memrealtime), i.e. the launch's duration as a
 // kernel trace measures it, without the queueing in front of it that a HIP
-// event bracket also counts when another stream's kernels hold the CUs.
-// span[0] = max over workgroups of ~start (= ~earliest start), span[1] = max
-// of the ends; both zeroed before the launch. One vector atomic per workgroup
-// and stamp (thread 0 of the workgroup / of wave 0).
+// event bracket also counts when another stream's kernels hold the CUs. A
+// slot holds SPAN_SHARDS pairs, 128 B apart (workgroup id % SPAN_SHARDS picks
+// one), so the per-workgroup atomics do not queue on one address: pair[0] =
+// max of ~start (= ~earliest start), pair[1] = max of the ends; all zeroed
+// before the launch; the host reduces over the shards. Thread 0 of the
+// workgroup (of its wave 0 for the end stamp) stamps.
+__device__ __forceinline__ unsigned long long* span_pair(unsigned long long* span) {
+  const unsigned wg = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  return span + (wg % SPAN_SHARDS) * 16;
+}
 __device__ __forceinline__ void span_start(unsigned long long* span) {
-  if (span && threadIdx.x == 0) atomicMax(span, ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
+  if (span && threadIdx.x == 0)
+    atomicMax(span_pair(span), ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 __device__ __forceinline__ void span_end(unsigned long long* span) {
-  if (span && threadIdx.x == 0) atomicMax(span + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  if (span && threadIdx.x == 0)
+    atomicMax(span_pair(span) + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
 }  // namespace mwx

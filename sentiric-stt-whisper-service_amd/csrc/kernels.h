@@ -6,6 +6,10 @@
 
 namespace mwx {
 
+// launch span stamp slots (kcommon.h span_start; engine.cpp span_slot): a slot
+// is SPAN_SHARDS (start, end) pairs 128 B apart
+constexpr int SPAN_SHARDS = 8, SPAN_SLOT_U64 = SPAN_SHARDS * 16;
+
 // GEMM epilogues. Every GEMM computes acc[m][n] = sum_k A[m][k] * W[n][k]
 // (W stored [N][K] as in ggml), accumulating in f32 on MFMA, and then applies
 // exactly the ops ggml applies after the matmul, at the same rounding points.
