@@ -593,6 +593,9 @@ def main():
     ap.add_argument("--lane-stagger", type=float, default=0.0,
                     help="seconds lane i waits (x i) before its first timed batch")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--timing", choices=["span", "events"], default="span",
+                    help="live kernel timing: device-clock launch spans (default) or HIP event "
+                         "brackets")
     ap.add_argument("--no-one-lane", action="store_true",
                     help="skip the one-lane pass after the timed region (a kernel trace of the "
                          "run then holds the multi-lane launches only)")
@@ -717,14 +720,18 @@ def main():
     # SURVEY.md §8 d asks for both bounds), timed in the same steps
     # (+ event_bracket: the timing events around an empty kernel at the same
     # point of the decode chain, whose average is the events' own cost)
-    classes = [args.perf_class] + (["enc_gemm"] if args.perf_class != "enc_gemm" else [])
-    if args.perf_class.startswith("dec_attn"):
-        classes.append("event_bracket")
-    # launch spans (device clock stamps of the first workgroup start and the
-    # last workgroup end, kcommon.h span_start): the duration a kernel trace
-    # measures, without the dispatch queueing behind the other lane's kernels
-    # that an event bracket includes
-    classes += [c + ".span" for c in (args.perf_class, "enc_gemm") if c in classes]
+    # Timing (--timing span, the default): launch spans, device clock stamps of
+    # the first workgroup start and the last workgroup end (kcommon.h
+    # span_start) -- the duration a kernel trace measures, without the
+    # dispatch queueing behind the other lane's kernels that a HIP event
+    # bracket includes (and without event-record nodes in the graph: they
+    # perturbed the other lane). --timing events: event brackets, corrected by
+    # an empty kernel's bracket at the same point of the chain (event_bracket)
+    kinds = [args.perf_class] + (["enc_gemm"] if args.perf_class != "enc_gemm" else [])
+    if args.timing == "span":
+        classes = [c + ".span" for c in kinds]
+    else:
+        classes = kinds + (["event_bracket"] if args.perf_class.startswith("dec_attn") else [])
     for so in owners:
         L.mwx_perf_read(so, None, None)
         L.mwx_perf_enable(so, ",".join(classes).encode())
@@ -789,18 +796,16 @@ def main():
 
     def make_roofs(tm, nsteps):
         """(dominant-kernel roofline, encoder-GEMM roofline) from live timings"""
-        launches = max(1, tm[args.perf_class][1])
-        avg_raw = tm[args.perf_class][0] / 1e3 / launches
-        # the bracket of an empty kernel at the same point of the chain: the
-        # two event nodes' own cost (+ the empty kernel), removed from the
-        # kernel's bracket so the duration compares with rocprofv3's
+        span = args.timing == "span"
+        tot, launches = tm[args.perf_class + (".span" if span else "")]
+        launches = max(1, launches)
+        avg_raw = tot / 1e3 / launches
         ev_s = None
-        if tm.get("event_bracket", (0, 0))[1] > 0:
+        if not span and tm.get("event_bracket", (0, 0))[1] > 0:
+            # the bracket of an empty kernel at the same point of the chain:
+            # the two event nodes' own cost (+ the empty kernel)
             ev_s = tm["event_bracket"][0] / 1e3 / tm["event_bracket"][1]
-        avg_ev = avg_raw - ev_s if ev_s is not None and ev_s < 0.5 * avg_raw else avg_raw
-        sp = tm.get(args.perf_class + ".span", (0.0, 0))
-        avg_span = sp[0] / 1e3 / sp[1] if sp[1] > 0 else None
-        avg_s = avg_span if avg_span is not None else avg_ev
+        avg_s = avg_raw - ev_s if ev_s is not None and ev_s < 0.5 * avg_raw else avg_raw
         # decode kernels run per row group (MWX_DECODE_GROUPS chains on their
         # own streams, default 1); the engine times every 8th decode step's
         # launches (MWX_PERF_PERIOD), all inside the timed region
@@ -832,32 +837,27 @@ def main():
                     "unit": "TFLOP/s", "frac": round(achieved / MFMA_PEAK_TFLOPS, 4),
                     "traffic": traffic}
         roof.update({"kernel": args.perf_class, "avg_launch_us": round(avg_s * 1e6, 2),
-                     "timing": "launch span (device clock)" if avg_span is not None
+                     "timing": ("launch span (device clock: first workgroup start to last "
+                                "workgroup end, every 8th decode step)") if span
                                else "event bracket - event cost",
-                     "span_launches": sp[1],
-                     "avg_bracket_minus_events_us": round(avg_ev * 1e6, 2),
-                     "avg_bracket_us": round(avg_raw * 1e6, 2),
-                     "event_bracket_us": round(ev_s * 1e6, 2) if ev_s is not None else None,
-                     "launches": tm[args.perf_class][1], "work_per_launch": work,
-                     "work_desc": desc})
+                     "launches": launches, "work_per_launch": work, "work_desc": desc})
+        if not span:
+            roof.update({"avg_bracket_us": round(avg_raw * 1e6, 2),
+                         "event_bracket_us": round(ev_s * 1e6, 2) if ev_s is not None else None})
         roof_enc = None
-        if "enc_gemm" in tm and args.perf_class != "enc_gemm" and tm["enc_gemm"][1] > 0:
-            ems, en = tm["enc_gemm"]
+        ecls = "enc_gemm" + (".span" if span else "")
+        if ecls in tm and args.perf_class != "enc_gemm" and tm[ecls][1] > 0:
+            ems, en = tm[ecls]
             _, ework, edesc = kernel_model(args.arch, "enc_gemm", args.clips, rows,
                                            en // max(1, nsteps), prompt_len, args.decode_steps,
                                            n_windows)
             eavg = ems / 1e3 / en
-            esp = tm.get("enc_gemm.span", (0.0, 0))
-            eavg_ev = eavg
-            if esp[1] == en:
-                eavg = esp[0] / 1e3 / esp[1]
             epeak = 2 * MFMA_PEAK_TFLOPS if args.fp8 else MFMA_PEAK_TFLOPS
             each = ework / eavg / 1e12
             roof_enc = {"bound": "mfma", "achieved": round(each, 1), "peak": epeak,
                         "unit": "TFLOP/s", "frac": round(each / epeak, 4), "kernel": "enc_gemm",
                         "avg_launch_us": round(eavg * 1e6, 2), "launches": en,
-                        "timing": "launch span (device clock)" if esp[1] == en else "event bracket",
-                        "avg_bracket_us": round(eavg_ev * 1e6, 2),
+                        "timing": "launch span (device clock)" if span else "event bracket",
                         "work_per_launch": ework, "work_desc": edesc}
         return roof, roof_enc
 

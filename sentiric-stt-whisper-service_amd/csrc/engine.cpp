@@ -280,7 +280,7 @@ static int perf_class_index(const State& S, const char* cls);
 // Launch spans: accumulate the (end - start) of the used slots of one region
 // into their classes (graph: after an instrumented replay has completed;
 // eager: after the state's stream has drained)
-static void harvest_spans(State& S, bool graph) {
+static void harvest_spans(State& S, bool graph, hipStream_t zs = nullptr) {
   const size_t n = graph ? S.span_gused : S.span_eused;
   if (n == 0 || !S.span_host) return;
   const size_t base = graph ? 0 : State::SPAN_G;
@@ -301,7 +301,12 @@ static void harvest_spans(State& S, bool graph) {
     S.perf_acc_ms[c] += (double)(t1 - t0) * S.span_tick_ms;
     S.perf_acc_n[c] += 1;
   }
-  if (!graph) S.span_eused = 0;
+  if (!graph) {
+    // (re-zeroed for the next launches, ordered before them on the state's stream)
+    HIPC(hipMemsetAsync((unsigned long long*)S.perf_span.p + su * base, 0, n * su * 8,
+                        zs ? zs : S.stream));
+    S.span_eused = 0;
+  }
 }
 
 static int perf_class_index(const State& S, const char* cls) {
@@ -318,9 +323,9 @@ static bool perf_on(const State& s, const char* cls) {
 
 // The stamp pair a launch of class `cls` writes its span to (kcommon.h
 // span_start / span_end) when "<cls>.span" is an enabled perf class, else
-// nullptr. Queued on the launch's stream: in an instrumented graph capture the
-// first slot adds one memset node zeroing every graph slot; eagerly, the
-// slot's 16 bytes are zeroed before the launch.
+// nullptr. In an instrumented graph capture the first slot adds one memset
+// node zeroing every graph slot; eager slots are used once each between two
+// harvests, which re-zero them.
 static unsigned long long* span_slot(State& S, const char* cls, hipStream_t s) {
   if (S.perf_class.empty() || (S.capturing && !S.capture_perf) || !S.perf_span.p) return nullptr;
   const int ci = perf_class_index(S, (std::string(cls) + ".span").c_str());
@@ -336,10 +341,10 @@ static unsigned long long* span_slot(State& S, const char* cls, hipStream_t s) {
   }
   if (S.span_eused >= (size_t)State::SPAN_E) {
     HIPC(hipStreamSynchronize(s));
-    harvest_spans(S, false);
+    harvest_spans(S, false, s);
   }
+  // (eager slots are zero: allocated zeroed, re-zeroed by each harvest)
   unsigned long long* p = base + SPAN_SLOT_U64 * (State::SPAN_G + S.span_eused);
-  HIPC(hipMemsetAsync(p, 0, SPAN_SLOT_U64 * 8, s));
   if (S.span_etag.size() <= S.span_eused) S.span_etag.resize(S.span_eused + 1);
   S.span_etag[S.span_eused++] = ci;
   return p;
@@ -1203,25 +1208,26 @@ struct Driver {
     // stream it once per group; an MX-fp8 cache is read by the grouped
     // kernel for any group size
     const int nq = std::max(1, rw.xgroup);  // (prefill: Driver::prefill's q)
+    unsigned long long* sp = rw.prefill ? nullptr : span_slot(S, "dec_attn_cross", s);
     if (C.kv8) {
       if (!dec_cross_attention_grouped<T>(
               rw.Pq, c.k3, d, W.cq_b, (const uint8_t*)S.cross_k.p + l * layer_cross,
               (const uint8_t*)S.cross_v.p + l * layer_cross, rw.xidx, rw.act, hp.n_audio_ctx,
               hp.n_audio_ctx, rw.od, n, H, kqs, nq, s,
               (const uint8_t*)S.cross_ks.p + l * layer_xs,
-              (const uint8_t*)S.cross_vs.p + l * layer_xs))
+              (const uint8_t*)S.cross_vs.p + l * layer_xs, sp))
         throw std::runtime_error("mwx: unsupported fp8 cross-attention group");
     } else if (nq < 2 ||
                !dec_cross_attention_grouped<T>(rw.Pq, c.k3, d, W.cq_b,
                                                (const _Float16*)S.cross_k.p + l * layer_cross,
                                                (const _Float16*)S.cross_v.p + l * layer_cross,
                                                rw.xidx, rw.act, hp.n_audio_ctx, hp.n_audio_ctx,
-                                               rw.od, n, H, kqs, nq, s)) {
+                                               rw.od, n, H, kqs, nq, s, nullptr, nullptr, sp)) {
       dec_attention<T>(rw.Pq, c.k3, d, W.cq_b, 1.0f, 1.0f,
                        (_Float16*)S.cross_k.p + l * layer_cross,
                        (_Float16*)S.cross_v.p + l * layer_cross, rw.xidx, rw.pos, rw.act,
                        hp.n_audio_ctx, hp.n_audio_ctx, rw.od, n, H, kqs, s, nullptr, nullptr, 0,
-                       nq, 1, rw.prefill ? nullptr : span_slot(S, "dec_attn_cross", s));
+                       nq, 1, sp);
     }
   }
   void layer_post(const LayerRows& rw, LayerRun& c, int l, hipStream_t s) {

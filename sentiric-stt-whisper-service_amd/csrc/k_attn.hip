@@ -602,7 +602,8 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
     const void* __restrict__ kbase, const void* __restrict__ vbase,
     const uint8_t* __restrict__ kscale8, const uint8_t* __restrict__ vscale8,
     const int* __restrict__ kv_index, const int* __restrict__ active, int n, int cap, int R,
-    T* __restrict__ o, int H, float scale) {
+    T* __restrict__ o, int H, float scale, unsigned long long* span = nullptr) {
+  span_start(span);
   __shared__ float sc[NQ][DEC_MAX_KEYS];
   __shared__ float redf[4][NQ];
   __shared__ double redd[4][NQ];
@@ -622,7 +623,10 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
     any |= act[q];
   }
   asm volatile("" ::"s"(slot));
-  if (!any) return;
+  if (!any) {
+    span_end(span);
+    return;
+  }
   const int D = H * 64;
   const long rbase = ((long)slot * H + h) * cap;  // first (time) row of this (slot, head)
   const _Float16* K = reinterpret_cast<const _Float16*>(kbase) + rbase * 64;
@@ -940,6 +944,7 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
                       (op[(2 * NQ + q) * 64 + e] + op[(3 * NQ + q) * 64 + e]);
       if (act[q]) o[pack_index(row0 + q, h * 64 + e, D)] = to_t<T>(r);
     }
+    span_end(span);
     return;
   }
   float acc[NQ][8];
@@ -1018,6 +1023,7 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
     }
     __syncthreads();
   }
+  span_end(span);
 }
 
 // MX-fp8 cross K/V cache, NQ rows of one clip (dec_xattn_kernel's KV8 path
@@ -1237,7 +1243,7 @@ bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float*
                                  const void* kbase, const void* vbase, const int* kv_index,
                                  const int* active, int n_keys, int cap, T* o, int R, int H,
                                  float scale, int nq, hipStream_t st, const uint8_t* kscale8,
-                                 const uint8_t* vscale8) {
+                                 const uint8_t* vscale8, unsigned long long* span) {
   if (n_keys > DEC_MAX_KEYS || KS > 8) return false;
   const dim3 g(H, (R + nq - 1) / nq);
   const bool kv8 = kscale8 != nullptr;
@@ -1254,11 +1260,11 @@ bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float*
     if (c6)                                                                                    \
       dec_xattn_kernel<T, N, K8, NT, 6><<<g, 256, 0, st>>>(P, KS, pcols, bias, kbase, vbase,   \
                                                            kscale8, vscale8, kv_index, active, \
-                                                           n_keys, cap, R, o, H, scale);       \
+                                                           n_keys, cap, R, o, H, scale, span); \
     else                                                                                       \
       dec_xattn_kernel<T, N, K8, NT><<<g, 256, 0, st>>>(P, KS, pcols, bias, kbase, vbase,      \
                                                         kscale8, vscale8, kv_index, active,    \
-                                                        n_keys, cap, R, o, H, scale);          \
+                                                        n_keys, cap, R, o, H, scale, span);    \
   } while (0)
   // MX-fp8 cache: MWX_XATTN8=1 selects the whole-batch two-in-flight stream
   // (dec_xattn8_kernel). Off by default: measured 69.2 us per launch against
@@ -1287,7 +1293,7 @@ bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float*
   case N:                                      \
     if (kv8 && mfs)                            \
       dec_xattn_kernel<T, N, true, true, 0, true><<<g, 256, 0, st>>>(P, KS, pcols, bias, kbase, \
-          vbase, kscale8, vscale8, kv_index, active, n_keys, cap, R, o, H, scale);             \
+          vbase, kscale8, vscale8, kv_index, active, n_keys, cap, R, o, H, scale, span);       \
     else if (kv8 && nt)                        \
       XL(N, true, true);                       \
     else if (kv8)                              \
@@ -1307,12 +1313,12 @@ template bool dec_cross_attention_grouped<_Float16>(const float*, int, int, cons
                                                     const void*, const void*, const int*,
                                                     const int*, int, int, _Float16*, int, int,
                                                     float, int, hipStream_t, const uint8_t*,
-                                                    const uint8_t*);
+                                                    const uint8_t*, unsigned long long*);
 template bool dec_cross_attention_grouped<__bf16>(const float*, int, int, const float*,
                                                   const void*, const void*, const int*,
                                                   const int*, int, int, __bf16*, int, int, float,
                                                   int, hipStream_t, const uint8_t*,
-                                                  const uint8_t*);
+                                                  const uint8_t*, unsigned long long*);
 
 // Prompt prefill: the self-attention K / V of every (virtual) row appended
 // to its cache row crow[row] at position pos[row] before the self-attention

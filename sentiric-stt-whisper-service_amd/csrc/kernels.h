@@ -227,7 +227,8 @@ bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float*
                                  const int* active, int n_keys, int cap, T* o, int R, int H,
                                  float scale, int nq, hipStream_t st,
                                  const uint8_t* kscale8 = nullptr,
-                                 const uint8_t* vscale8 = nullptr);
+                                 const uint8_t* vscale8 = nullptr,
+                                 unsigned long long* span = nullptr);
 
 struct RowCtl {
   int active;        // row participates in this step
