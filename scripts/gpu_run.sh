@@ -8,6 +8,7 @@
 #   benchq     default bench without the CPU baseline (quick)
 #   bench1     C3 on one lane
 #   c2         C2: base f16, one clip per request
+#   c2pf       C2 with L2-prefetch helper workgroups in the cross-attention (MWX_XATTN_PF)
 #   c2nt       C2 with the cross K/V streamed non-temporally (A/B of the MALL-resident default)
 #   x64 / g2x64  64 clips in one state, one decode chain / two row groups on two streams
 #   pair64     64 clips in one state, decoded as two interleaved 32-row sets (MWX_DECODE_PAIR)
@@ -57,6 +58,7 @@ for s in "$@"; do
     benchq) run benchq 400 python -u bench.py --steps 8 --warmup 2 --no-cpu-baseline ;;
     bench1) run bench1 400 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
     c2) run c2 300 python -u bench.py --arch base --wtype f16 --clips 1 --lanes 1 --steps 20 --warmup 3 --no-cpu-baseline ;;
+    c2pf) run c2pf 300 env MWX_XATTN_PF=7 python -u bench.py --arch base --wtype f16 --clips 1 --lanes 1 --steps 20 --warmup 3 --no-cpu-baseline ;;
     c2nt) run c2nt 300 env MWX_XATTN_NT=1 python -u bench.py --arch base --wtype f16 --clips 1 --lanes 1 --steps 20 --warmup 3 --no-cpu-baseline ;;
     x64) run x64 500 python -u bench.py --clips 64 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
     g2x64) run g2x64 500 env MWX_DECODE_GROUPS=2 python -u bench.py --clips 64 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;

@@ -278,7 +278,15 @@ __device__ __forceinline__ float dpp_sum8(float d) {
 // written to the cache and taken from LDS (its cache line may be stale in L1).
 // The loop body is straight-line (two batches per trip, no early exit), so the
 // compiler keeps exactly one batch in flight with counted vmcnt waits.
-template <typename T, bool SELF, int UBX = 8, bool NTL = !SELF, int NBC = 0>
+// PF > 0 (cross, small grids: one request): the grid carries PF helper
+// workgroups per (row, head) on the same XCD as the one that attends
+// (blockIdx.y >= R; H % 8 == 0, so linear id % 8 -- the XCD under the
+// round-robin placement -- equals the attending workgroup's). Helper p loads
+// its share of the (row, head)'s K rows then V rows with the default cache
+// policy and discards them: the rows land in that XCD's L2 while the attending
+// workgroup streams the batches before them, so its later batches are L2 hits.
+// The attending workgroup's arithmetic is unchanged (bit-identical).
+template <typename T, bool SELF, int UBX = 8, bool NTL = !SELF, int NBC = 0, int PF = 0>
 __global__ __launch_bounds__(256) void dec_attn_kernel(
     const float* __restrict__ P, int KS, int pcols, const float* __restrict__ bias, float qscale,
     float kscale, _Float16* __restrict__ kbase, _Float16* __restrict__ vbase,
@@ -293,6 +301,35 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
   __shared__ float sq[64], snk[64], snv[64];
   span_start(span);
   int row = blockIdx.y, h = blockIdx.x;
+  if constexpr (PF > 0) {
+    if (row >= R) {
+      const int r = (row - R) % R, p = (row - R) / R;
+      const int hslot = kv_index ? kv_index[r] : r;
+      if (active[r]) {
+        const _Float16* K = kbase + (((long)hslot * H + h) * cap) * 64;
+        const _Float16* V = vbase + (((long)hslot * H + h) * cap) * 64;
+        // 16-B chunks of the K rows then the V rows; helper p takes chunks
+        // [p*per, (p+1)*per): the later ones (the attending workgroup reads
+        // K first, its own first batches itself)
+        const long chunks = (long)fixed_len * 8;  // per matrix
+        const long per = (2 * chunks + PF - 1) / PF;
+        const long c0 = min((long)p * per, 2 * chunks), c1 = min(c0 + per, 2 * chunks);
+        for (long c = c0 + threadIdx.x; c < c1; c += 256 * 4) {
+          f16x8 x[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const long ci = min(c + 256 * i, c1 - 1);
+            const _Float16* src = ci < chunks ? K + ci * 8 : V + (ci - chunks) * 8;
+            x[i] = *reinterpret_cast<const f16x8*>(src);
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(x[i]));
+        }
+      }
+      span_end(span);
+      return;
+    }
+  }
   if (nq > 1) {
     // nq rows per clip (beam / best-of decoders: cross, the same K/V; self,
     // histories taken over from each other): 1-D grid where the nq
@@ -1396,6 +1433,9 @@ void dec_attention(const float* P, int KS, int pcols, const float* bias, float q
   // MWX_XATTN_NBC=0: the runtime-batch-count cross kernel (A/B of the
   // constant-count load stream)
   static const bool xattn_nbc = !(getenv("MWX_XATTN_NBC") && atoi(getenv("MWX_XATTN_NBC")) == 0);
+  // MWX_XATTN_PF=7: 7 L2-prefetch helper workgroups per (row, head) for small
+  // cross-attention grids (A/B; off by default)
+  static const int xattn_pf = getenv("MWX_XATTN_PF") ? (atoi(getenv("MWX_XATTN_PF")) > 0 ? 7 : 0) : 0;
   if (fixed_len == 0 && self_ub4)
     dec_attn_kernel<T, true, 4><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale, kbase,
                                                    vbase, kv_index, pos, active, fixed_len,
@@ -1406,7 +1446,19 @@ void dec_attention(const float* P, int KS, int pcols, const float* bias, float q
                                                 kv_index, pos, active, fixed_len, kv_len_cap, o,
                                                 H, scale, kvmap, own_from, map_row0, nq, R,
                                                 write_new);
-  else if (xattn_nt && fixed_len == 1500 && xattn_nbc)  // (every Whisper model: 1500 frames)
+  else if (xattn_pf > 0 && nq == 1 && H % 8 == 0 && (long)R * H * (1 + xattn_pf) <= 256 &&
+           fixed_len == 1500 && xattn_nbc) {
+    // (one request: helper workgroups pull the K / V rows into L2)
+    const dim3 gp(H, R * (1 + xattn_pf));
+    if (xattn_nt)
+      dec_attn_kernel<T, false, 8, true, 6, 7><<<gp, 256, 0, st>>>(
+          P, KS, pcols, bias, qscale, kscale, kbase, vbase, kv_index, pos, active, fixed_len,
+          kv_len_cap, o, H, scale, nullptr, nullptr, 0, nq, R, 1, span);
+    else
+      dec_attn_kernel<T, false, 8, false, 6, 7><<<gp, 256, 0, st>>>(
+          P, KS, pcols, bias, qscale, kscale, kbase, vbase, kv_index, pos, active, fixed_len,
+          kv_len_cap, o, H, scale, nullptr, nullptr, 0, nq, R, 1, span);
+  } else if (xattn_nt && fixed_len == 1500 && xattn_nbc)  // (every Whisper model: 1500 frames)
     dec_attn_kernel<T, false, 8, true, 6><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale,
                                                              kbase, vbase, kv_index, pos, active,
                                                              fixed_len, kv_len_cap, o, H, scale,
