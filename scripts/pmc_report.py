@@ -62,9 +62,13 @@ def load(path, counters):
 
 def main():
     root, tag = sys.argv[1], sys.argv[2]
-    fetch, _ = load(os.path.join(root, f"pmc_{tag}_FETCH_SIZE"), {"FETCH_SIZE"})
-    write, _ = load(os.path.join(root, f"pmc_{tag}_WRITE_SIZE"), {"WRITE_SIZE"})
-    mf, mdur = load(os.path.join(root, f"pmc_{tag}_MFMA"),
+    def pdir(c):  # (round 2: pmc_<tag>_<c>; scripts/gpu_run.sh: <tag>_pmc_<c>)
+        a = os.path.join(root, f"pmc_{tag}_{c}")
+        return a if os.path.isdir(a) else os.path.join(root, f"{tag}_pmc_{c}")
+
+    fetch, _ = load(pdir("FETCH_SIZE"), {"FETCH_SIZE"})
+    write, _ = load(pdir("WRITE_SIZE"), {"WRITE_SIZE"})
+    mf, mdur = load(pdir("MFMA"),
                     {"SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE",
                      "SQ_WAVE_CYCLES"})
     rows = []
