@@ -17,6 +17,7 @@
 #   mfstest    the MX-fp8 tests with the MFMA-score cross-attention (MWX_XATTN_MFS=1)
 #   c5mfs / c5one  C5 on one lane with / without the MFMA scores
 #   bench1np / bench1g0  one lane without the prompt prefill / with row-major encoder tile order
+#   b5one / b5nr / bench1nr  beam 5 one lane with / without decode row-block grouping; C3 one lane without
 #   pairtest   the paired-decode parity tests only
 #   b5         beam 5 (service default decode), C3 shape
 #   c5         C5: MX-fp8, beam 5, 600-s long-form clips
@@ -71,6 +72,9 @@ for s in "$@"; do
     c5one) run c5one 700 python -u bench.py --fp8 --beam 5 --clip-seconds 600 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline ;;
     bench1np) run bench1np 400 env MWX_PREFILL_MIN=0 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
     bench1g0) run bench1g0 400 env MWX_GEMM_GROUP=0 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
+    b5one) run b5one 500 python -u bench.py --beam 5 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    b5nr) run b5nr 500 env MWX_DEC_GROUP_ROWS=0 python -u bench.py --beam 5 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    bench1nr) run bench1nr 400 env MWX_DEC_GROUP_ROWS=0 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
     pairtest) run pairtest 600 python -u -m pytest tests/test_gpu_pair.py -m gpu -x -v -s -rf --timeout 300 --timeout-method thread ;;
     b5) run b5 500 python -u bench.py --beam 5 --steps 4 --warmup 1 --no-cpu-baseline ;;
     c5) run c5 700 python -u bench.py --fp8 --beam 5 --clip-seconds 600 --steps 2 --warmup 1 --no-cpu-baseline ;;

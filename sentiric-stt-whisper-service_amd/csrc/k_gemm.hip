@@ -665,23 +665,39 @@ __device__ __forceinline__ void skinny_store(const EpiParams& P, int m, int n, f
   epi_store<EPI, T, OUT16>(P, 0, m, n, v);
 }
 
+// Row-block grouping (zrb = row blocks > 1, decode_tile_of): a 1-D grid where
+// the zrb row blocks of one weight tile are consecutive ids of one residue
+// mod 8 -- one XCD under the round-robin placement -- so the tile is read from
+// HBM about once and served to the other row blocks from that XCD's L2 (with
+// the row blocks as grid.z / grid.y, a beam step's 5 row blocks of 32 rows
+// re-read every weight tile from HBM 5 times). Which rows and columns a
+// workgroup computes, and how, is unchanged: results are bit-identical.
+__device__ __forceinline__ bool decode_tile_of(int zrb, int ntiles, int& t, int& z) {
+  const int L = blockIdx.x, W = 8 * zrb, w = L / W, j = L - w * W;
+  t = w * 8 + (j & 7);
+  z = j >> 3;
+  return t < ntiles;
+}
+
 template <typename T, int MT, int KCH, bool W8 = false, bool LNA = false>
 __global__ __launch_bounds__(1024) void gemm_skinny(int epi, const T* __restrict__ Ap,
                                                     const void* __restrict__ Wv,
                                                     const uint8_t* __restrict__ Ws, int KT, int M,
-                                                    int N, EpiParams P, LnFuse LN) {
+                                                    int N, EpiParams P, LnFuse LN, int zrb = 0) {
   using V8 = typename Elt<T>::v8;
   __shared__ f32x4 red[16][MT][64];
   __shared__ typename std::conditional<LNA, LnLds, int>::type lnsh;  // (LNA only)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, NW = blockDim.x >> 6;
-  const int n0 = blockIdx.x * 16;
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (zrb > 0 && !decode_tile_of(zrb, (N + 15) / 16, bx, by)) return;
+  const int n0 = bx * 16;
   // row block of 16*MT rows (grid.y): per-row arithmetic does not depend on M
   // nor on the block size (each output is the same MFMA chain over k)
-  const int m_base = blockIdx.y * 16 * MT;
+  const int m_base = by * 16 * MT;
   const int Mb = min(16 * MT, M - m_base);
   const int kt0 = wid * KCH;
-  const long f0 = (long)blockIdx.x * KT + kt0;  // first weight fragment of this wave
-  const T* at = Ap + ((long)(blockIdx.y * MT) * KT + kt0) * 512 + lane * 8;
+  const long f0 = (long)bx * KT + kt0;  // first weight fragment of this wave
+  const T* at = Ap + ((long)(by * MT) * KT + kt0) * 512 + lane * 8;
   V8 bfr[KCH];
   V8 afr[MT][KCH];
   uint2 wraw[W8 ? KCH : 1];
@@ -767,16 +783,25 @@ static bool skinny_split(int K, int& nw, int& kch) {
   return false;
 }
 
+// decode GEMMs with several row blocks: group them per weight tile on one XCD
+// (decode_tile_of; MWX_DEC_GROUP_ROWS=0: the grid.y / grid.z layout, A/B)
+static bool decode_group_rows() {
+  static const bool on = !(getenv("MWX_DEC_GROUP_ROWS") && atoi(getenv("MWX_DEC_GROUP_ROWS")) == 0);
+  return on;
+}
+
 template <typename T, int MT, bool W8, bool LNA = false>
 static bool skinny_launch(int epi, const T* Ap, const void* Wp, const uint8_t* Ws, int M, int N,
                           int K, const EpiParams& P, hipStream_t st, const LnFuse& ln = LnFuse()) {
   int nw = 0, kch = 0;
   if (!skinny_split(K, nw, kch)) return false;
   if (LNA && (nw < 4 || K > 2048 || M > LNF_MAX_ROWS)) return false;  // (256 LayerNorm threads)
-  const dim3 g((N + 15) / 16, (M + 16 * MT - 1) / (16 * MT)), b(64 * nw);
+  const int nrb = (M + 16 * MT - 1) / (16 * MT), nx = (N + 15) / 16;
+  const int zrb = nrb > 1 && decode_group_rows() ? nrb : 0;
+  const dim3 g = zrb ? dim3((nx + 7) / 8 * 8 * zrb) : dim3(nx, nrb), b(64 * nw);
   switch (kch) {
 #define SK(C) \
-  case C: gemm_skinny<T, MT, C, W8, LNA><<<g, b, 0, st>>>(epi, Ap, Wp, Ws, K / 32, M, N, P, ln); return true;
+  case C: gemm_skinny<T, MT, C, W8, LNA><<<g, b, 0, st>>>(epi, Ap, Wp, Ws, K / 32, M, N, P, ln, zrb); return true;
     SK(1) SK(2) SK(3) SK(4) SK(6) SK(8) SK(10)
 #undef SK
     default: return false;
@@ -796,17 +821,25 @@ __global__ __launch_bounds__(256) void gemm_splitk(const T* __restrict__ Ap,
                                                    const void* __restrict__ Wv,
                                                    const uint8_t* __restrict__ Ws, int KT, int M,
                                                    int N, int kslice, float* __restrict__ P,
-                                                   LnFuse LN) {
+                                                   LnFuse LN, int zrb = 0) {
   using V8 = typename Elt<T>::v8;
   __shared__ f32x4 red[4][MT][64];
   __shared__ typename std::conditional<LNA, LnLds, int>::type lnsh;  // (LNA only)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int n0 = blockIdx.x * 16, ks = blockIdx.y;
-  const int m_base = blockIdx.z * 16 * MT;  // row block (16*MT rows per grid.z slice)
+  int bx = blockIdx.x, ks = blockIdx.y, bz = blockIdx.z;
+  if (zrb > 0) {  // (row-block grouping, gemm_skinny's note)
+    const int nx = (N + 15) / 16, nks = KT * 32 / kslice;
+    int t;
+    if (!decode_tile_of(zrb, nx * nks, t, bz)) return;
+    bx = t % nx;
+    ks = t / nx;
+  }
+  const int n0 = bx * 16;
+  const int m_base = bz * 16 * MT;  // row block (16*MT rows per grid.z slice)
   const int Mb = min(16 * MT, M - m_base);
   const int kt0 = (ks * kslice >> 5) + wid * KCH;
-  const long f0 = (long)blockIdx.x * KT + kt0;
-  const T* at = Ap + ((long)(blockIdx.z * MT) * KT + kt0) * 512 + lane * 8;
+  const long f0 = (long)bx * KT + kt0;
+  const T* at = Ap + ((long)(bz * MT) * KT + kt0) * 512 + lane * 8;
   V8 bfr[KCH];
   V8 afr[MT][KCH];
   uint2 wraw[W8 ? KCH : 1];
@@ -891,7 +924,9 @@ int gemm_splitk_partials(const T* Ap, const DecW<T>& Wd, int M, int N, int K, fl
   if (M > 64 && mt_big >= 2 && mt_big <= 4) MT = mt_big;
   static const bool mt1 = !(getenv("MWX_DEC_MT1") && atoi(getenv("MWX_DEC_MT1")) == 0);
   if (mt1 && M <= 64) MT = 1;  // 16-row blocks (greedy +3%; MWX_DEC_MT1=0 for A/B)
-  const dim3 g((N + 15) / 16, ks, (M + 16 * MT - 1) / (16 * MT));
+  const int nrb = (M + 16 * MT - 1) / (16 * MT), nx = (N + 15) / 16;
+  const int zrb = nrb > 1 && !ln && decode_group_rows() ? nrb : 0;
+  const dim3 g = zrb ? dim3((nx * ks + 7) / 8 * 8 * zrb) : dim3(nx, ks, nrb);
   if (ln) {  // LayerNorm-fused A operand (M <= LNF_MAX_ROWS, one 16-row block)
     if (M > LNF_MAX_ROWS || K > 2048) return 0;
 #define SKF(C)                                                                                  \
@@ -912,10 +947,10 @@ int gemm_splitk_partials(const T* Ap, const DecW<T>& Wd, int M, int N, int K, fl
   if (MT == MTV && kch == C) {                                                            \
     if (w8)                                                                               \
       gemm_splitk<T, MTV, C, true><<<g, 256, 0, st>>>(Ap, Wp, Ws, K / 32, M, N, kslice, P, \
-                                                      LnFuse());                          \
+                                                      LnFuse(), zrb);                     \
     else                                                                                  \
       gemm_splitk<T, MTV, C, false><<<g, 256, 0, st>>>(Ap, Wp, Ws, K / 32, M, N, kslice, P, \
-                                                       LnFuse());                         \
+                                                       LnFuse(), zrb);                    \
     return ks;                                                                            \
   }
 #define SKM(MTV) SKL(MTV, 1) SKL(MTV, 2) SKL(MTV, 3) SKL(MTV, 4) SKL(MTV, 5)
