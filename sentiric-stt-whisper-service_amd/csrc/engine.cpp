@@ -228,6 +228,10 @@ struct State {
   // kvown[row] are read from row kvmap[row][pos] (host copies in kvmap_h/kvown_h)
   DBuf kvmap, kvown;
   std::vector<int> kvmap_h, kvown_h;
+  // pinned mirrors of kvmap_h / kvown_h: the map uploads of a beam step are
+  // asynchronous DMAs (a pageable 287-KB upload per step blocked the host)
+  int* kvmap_pin = nullptr;
+  size_t kvmap_pin_n = 0;
   int cross_cap = 0;  // cross cache slots
   int row_cap = 0;    // self cache rows
   std::vector<Segment> result_all;
@@ -1017,24 +1021,50 @@ struct Driver {
     HIPC(hipStreamSynchronize(st));  // no map upload may still read the host arrays
     S.kvmap_h.assign((size_t)R * Tctx, 0);
     S.kvown_h.assign(R, 0);
+    const size_t need = (size_t)R * Tctx + R;  // [kvmap | kvown]
+    if (S.kvmap_pin_n < need) {
+      std::lock_guard<std::recursive_mutex> lock(capture_mutex());
+      if (S.kvmap_pin) (void)hipHostFree(S.kvmap_pin);
+      S.kvmap_pin = nullptr;
+      S.kvmap_pin_n = 0;
+      HIPC(hipHostMalloc((void**)&S.kvmap_pin, need * 4, hipHostMallocDefault));
+      S.kvmap_pin_n = need;
+    }
+    memset(S.kvmap_pin, 0, need * 4);
     HIPC(hipMemsetAsync(S.kvown.p, 0, (size_t)R * 4, st));
   }
   void copy_kv_rows(const std::vector<int>& triples) {
     const int n = (int)triples.size() / 3;
     if (n == 0) return;
-    const std::vector<int> map0 = S.kvmap_h, own0 = S.kvown_h;
+    // pre-move state of the source rows (any permutation of moves is safe)
+    std::vector<int> srow(S.kvown_h.size(), -1), snap;
+    std::vector<int> own_src;
+    for (int i = 0; i < n; ++i) {
+      const int src = triples[3 * i + 1];
+      if (srow[src] >= 0) continue;
+      srow[src] = (int)own_src.size();
+      own_src.push_back(S.kvown_h[src]);
+      snap.insert(snap.end(), S.kvmap_h.begin() + (size_t)src * Tctx,
+                  S.kvmap_h.begin() + (size_t)(src + 1) * Tctx);
+    }
     int lo = 1 << 30, hi = -1;
+    const size_t R = S.kvown_h.size();
+    int* pmap = S.kvmap_pin;
+    int* pown = S.kvmap_pin + R * Tctx;
     for (int i = 0; i < n; ++i) {
       const int dst = triples[3 * i], src = triples[3 * i + 1], npos = triples[3 * i + 2];
-      for (int j = 0; j < npos; ++j)
-        S.kvmap_h[(size_t)dst * Tctx + j] = j < own0[src] ? map0[(size_t)src * Tctx + j] : src;
+      const int si = srow[src];
+      int* row = S.kvmap_h.data() + (size_t)dst * Tctx;
+      for (int j = 0; j < npos; ++j) row[j] = j < own_src[si] ? snap[(size_t)si * Tctx + j] : src;
       S.kvown_h[dst] = npos;
+      memcpy(pmap + (size_t)dst * Tctx, row, (size_t)Tctx * 4);
+      pown[dst] = npos;
       lo = std::min(lo, dst);
       hi = std::max(hi, dst);
     }
-    HIPC(hipMemcpyAsync((int*)S.kvmap.p + (size_t)lo * Tctx, S.kvmap_h.data() + (size_t)lo * Tctx,
+    HIPC(hipMemcpyAsync((int*)S.kvmap.p + (size_t)lo * Tctx, pmap + (size_t)lo * Tctx,
                         (size_t)(hi - lo + 1) * Tctx * 4, hipMemcpyHostToDevice, st));
-    HIPC(hipMemcpyAsync((int*)S.kvown.p + lo, S.kvown_h.data() + lo, (size_t)(hi - lo + 1) * 4,
+    HIPC(hipMemcpyAsync((int*)S.kvown.p + lo, pown + lo, (size_t)(hi - lo + 1) * 4,
                         hipMemcpyHostToDevice, st));
     // (ordered before the next step on this stream; the host arrays are next
     // written after that step's synchronize, or in reset_kv_maps)
