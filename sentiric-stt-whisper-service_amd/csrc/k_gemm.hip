@@ -784,9 +784,11 @@ static bool skinny_split(int K, int& nw, int& kch) {
 }
 
 // decode GEMMs with several row blocks: group them per weight tile on one XCD
-// (decode_tile_of; MWX_DEC_GROUP_ROWS=0: the grid.y / grid.z layout, A/B)
+// (decode_tile_of) with MWX_DEC_GROUP_ROWS=1. Off by default: measured slower
+// (beam 5 one lane 742.9 -> 703.7, C3 one lane 1207.7 -> 1179.9 audio-s/s,
+// same box)
 static bool decode_group_rows() {
-  static const bool on = !(getenv("MWX_DEC_GROUP_ROWS") && atoi(getenv("MWX_DEC_GROUP_ROWS")) == 0);
+  static const bool on = getenv("MWX_DEC_GROUP_ROWS") && atoi(getenv("MWX_DEC_GROUP_ROWS")) != 0;
   return on;
 }
 
