@@ -798,7 +798,10 @@ def main():
         """(dominant-kernel roofline, encoder-GEMM roofline) from live timings"""
         span = args.timing == "span"
         tot, launches = tm[args.perf_class + (".span" if span else "")]
-        launches = max(1, launches)
+        if launches == 0 or tot <= 0.0:
+            # (a class without span stamps: --timing events times it)
+            return ({"kernel": args.perf_class, "error": f"no {args.timing} timings for this class"},
+                    None)
         avg_raw = tot / 1e3 / launches
         ev_s = None
         if not span and tm.get("event_bracket", (0, 0))[1] > 0:
