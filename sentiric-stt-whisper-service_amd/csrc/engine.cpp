@@ -232,6 +232,11 @@ struct State {
   // asynchronous DMAs (a pageable 287-KB upload per step blocked the host)
   int* kvmap_pin = nullptr;
   size_t kvmap_pin_n = 0;
+  // pinned host staging of the batch's signal energy (token timestamps): the
+  // per-clip D2H copies are async DMAs, not pageable copies that block the
+  // host before the encoder is queued
+  float* energy_pin = nullptr;
+  size_t energy_pin_n = 0;
   int cross_cap = 0;  // cross cache slots
   int row_cap = 0;    // self cache rows
   std::vector<Segment> result_all;
@@ -731,7 +736,11 @@ static const std::vector<std::string>& non_speech_tokens() {
 struct TsState {
   int64_t t_beg = 0, t_last = 0;
   int tid_last = 0;
-  std::vector<float> energy;
+  // the clip's signal energy (get_signal_energy), in the batch state's pinned
+  // staging (State::energy_pin): written by an async copy queued before the
+  // decode steps, read after them
+  const float* energy = nullptr;
+  int n_energy = 0;
 };
 
 struct ClipRun {
