@@ -278,6 +278,18 @@ __device__ __forceinline__ float dpp_sum8(float d) {
 // written to the cache and taken from LDS (its cache line may be stale in L1).
 // The loop body is straight-line (two batches per trip, no early exit), so the
 // compiler keeps exactly one batch in flight with counted vmcnt waits.
+// Cross-attention scores of one 16-key tile on MFMA for f16 caches (MFC; the
+// single-row and the grouped kernel both call this, so a row's scores do not
+// depend on the kernel or the group size): the tile is the A operand (lane l:
+// key l&15, e = 32h + 8(l>>4) .. +7 for the two halves h), the queries the B
+// operand (lane l: query l&15, the same e; rows >= the query count zero);
+// lane l receives query l&15's dot products with keys 4(l>>4) .. +3.
+__device__ __forceinline__ f32x4 xscore16(f16x8 k0, f16x8 k1, f16x8 q0, f16x8 q1) {
+  const f32x4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+  const f32x4 a = __builtin_amdgcn_mfma_f32_16x16x32_f16(k0, q0, z, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(k1, q1, a, 0, 0, 0);
+}
+
 // PF > 0 (cross, small grids: one request): the grid carries PF helper
 // workgroups per (row, head) on the same XCD as the one that attends
 // (blockIdx.y >= R; H % 8 == 0, so linear id % 8 -- the XCD under the
@@ -286,7 +298,8 @@ __device__ __forceinline__ float dpp_sum8(float d) {
 // policy and discards them: the rows land in that XCD's L2 while the attending
 // workgroup streams the batches before them, so its later batches are L2 hits.
 // The attending workgroup's arithmetic is unchanged (bit-identical).
-template <typename T, bool SELF, int UBX = 8, bool NTL = !SELF, int NBC = 0, int PF = 0>
+template <typename T, bool SELF, int UBX = 8, bool NTL = !SELF, int NBC = 0, int PF = 0,
+          bool MFC = false>
 __global__ __launch_bounds__(256) void dec_attn_kernel(
     const float* __restrict__ P, int KS, int pcols, const float* __restrict__ bias, float qscale,
     float kscale, _Float16* __restrict__ kbase, _Float16* __restrict__ vbase,
@@ -428,10 +441,30 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
     // would make the query wait for all of them)
     if (part != 1) bcol = bias[col];
   }
-  LOADROWS0(ka, K)
-  // NBC: the second key batch is requested before the query is formed too,
-  // so two batches are in flight from the start
-  if constexpr (NBC > 0) LOADROWS(kb2, K, 1)
+  // MFC (cross, NBC): scores on MFMA (xscore16); wave w streams the 16-key
+  // tiles w, w + 4, ... four at a time, two groups in flight
+  constexpr int TDC = 4;
+  const int ntc = (n + 15) >> 4, ngc = ((ntc + 3) / 4 + TDC - 1) / TDC;
+  const int mln = lane & 15, gq = lane >> 4;
+  f16x8 kt[MFC ? 2 : 1][MFC ? TDC : 1][2];
+  auto mfc_load = [&](int buf, int grp) {
+#pragma unroll
+    for (int i = 0; i < TDC; ++i) {
+      const int t = min(wid + 4 * (TDC * grp + i), ntc - 1);
+      const _Float16* r = K + (long)min(t * 16 + mln, jmax) * 64 + 8 * gq;
+      kt[buf][i][0] = ld_stream<NTL>(reinterpret_cast<const f16x8*>(r));
+      kt[buf][i][1] = ld_stream<NTL>(reinterpret_cast<const f16x8*>(r + 32));
+    }
+  };
+  if constexpr (MFC) {
+    mfc_load(0, 0);
+    if (ngc > 1) mfc_load(1, 1);
+  } else {
+    LOADROWS0(ka, K)
+    // NBC: the second key batch is requested before the query is formed too,
+    // so two batches are in flight from the start
+    if constexpr (NBC > 0) LOADROWS(kb2, K, 1)
+  }
   if (red) {
     float acc = pk[0];
 #pragma unroll
@@ -532,6 +565,45 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
       if (b > 0) LOADROWS(ka, V, b)
       pv_batch(ka, b);
     }
+  } else if constexpr (NBC > 0 && MFC) {
+    f16x8 qb0, qb1;  // B operand: the query in column 0, zero elsewhere
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      qb0[j] = mln == 0 ? (_Float16)sq[8 * gq + j] : (_Float16)0.0f;
+      qb1[j] = mln == 0 ? (_Float16)sq[32 + 8 * gq + j] : (_Float16)0.0f;
+    }
+    auto tile = [&](int buf, int i, int t) {
+      const f32x4 d = xscore16(kt[buf][i][0], kt[buf][i][1], qb0, qb1);
+      if (mln == 0 && t < ntc) {
+        f32x4 out;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[r] = d[r] * scale;
+        *reinterpret_cast<f32x4*>(&sc[t * 16 + 4 * gq]) = out;
+      }
+    };
+#pragma unroll 1
+    for (int grp = 0; grp < ngc; grp += 2) {
+#pragma unroll
+      for (int i = 0; i < TDC; ++i) tile(0, i, wid + 4 * (TDC * grp + i));
+      if (grp + 2 < ngc) mfc_load(0, grp + 2);
+      if (grp + 1 < ngc) {
+#pragma unroll
+        for (int i = 0; i < TDC; ++i) tile(1, i, wid + 4 * (TDC * (grp + 1) + i));
+        if (grp + 3 < ngc) mfc_load(1, grp + 3);
+      }
+    }
+    LOADROWS(ka, V, 0)
+    LOADROWS(kb2, V, 1)
+    softmax();
+#pragma unroll 1
+    for (int b = 0; b < NBC - 2; b += 2) {
+      pv_batch(ka, b);
+      LOADROWS(ka, V, b + 2)
+      pv_batch(kb2, b + 1);
+      LOADROWS(kb2, V, b + 3)
+    }
+    pv_batch(ka, NBC - 2);
+    pv_batch(kb2, NBC - 1);
   } else if constexpr (NBC > 0) {
     // cross with a compile-time even batch count (n = 1500: 6): the K batches
     // and then the V batches form one load stream through the two register
@@ -720,12 +792,19 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
   constexpr int TD = 4;
   const int ntile = (n + 15) >> 4;
   const int mrow = lane & 15, gq = lane >> 4;
-  uint2 kr[MFS ? 2 : 1][MFS ? TD : 1][2];
-  uint32_t ksr[MFS ? 2 : 1][MFS ? TD : 1][2];
+  uint2 kr[MFS && KV8 ? 2 : 1][MFS && KV8 ? TD : 1][2];
+  uint32_t ksr[MFS && KV8 ? 2 : 1][MFS && KV8 ? TD : 1][2];
+  f16x8 kf[MFS && !KV8 ? 2 : 1][MFS && !KV8 ? TD : 1][2];  // (f16 cache: xscore16 tiles)
   auto mfs_load = [&](int buf, int grp) {  // tiles wid + 4 * (TD * grp + i)
 #pragma unroll
     for (int i = 0; i < TD; ++i) {
       const int t = min(wid + 4 * (TD * grp + i), ntile - 1);
+      if constexpr (!KV8) {
+        const _Float16* r = K + (long)min(t * 16 + mrow, jmax) * 64 + 8 * gq;
+        kf[buf][i][0] = ld_stream<NTL>(reinterpret_cast<const f16x8*>(r));
+        kf[buf][i][1] = ld_stream<NTL>(reinterpret_cast<const f16x8*>(r + 32));
+        continue;
+      }
       const uint8_t* row = K8 + (long)min(t * 16 + mrow, jmax) * 64 + 8 * gq;
       const u32x2 a = ld_stream<NTL>(reinterpret_cast<const u32x2*>(row));
       const u32x2 b = ld_stream<NTL>(reinterpret_cast<const u32x2*>(row + 32));
@@ -818,7 +897,7 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
   // half's byte reads hit distinct banks) and reads each lane's B operand
   // (8 keys at one e) from there; the A operand is the query's P times the V
   // scale of each key (per scale half), so the codes enter the MFMA unscaled
-  __shared__ __attribute__((aligned(16))) uint8_t vtile[MFS ? 4 : 1][MFS ? 32 * 64 : 16];
+  __shared__ __attribute__((aligned(16))) uint8_t vtile[MFS && KV8 ? 4 : 1][MFS && KV8 ? 32 * 64 : 16];
   const int nt32 = (n + 31) >> 5;
   const int vrow = lane >> 1, vch = 2 * (lane & 1);
   u32x4 vr0, vr1, vsr;  // the next tile's bytes (rows vrow, chunks vch, vch + 1) and V scales
@@ -848,19 +927,24 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
     }
     auto e8m0 = [](uint32_t e) { return e ? __uint_as_float(e << 23) : __uint_as_float(0x00400000u); };
     auto score_tile = [&](int buf, int i, int t) {
-      const f16x8 a0 = dequant_h8(kr[buf][i][0], 127u), a1 = dequant_h8(kr[buf][i][1], 127u);
-      const f32x4 z = {0.0f, 0.0f, 0.0f, 0.0f};
-      const f32x4 d0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, qb0, z, 0, 0, 0);
-      const f32x4 d1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, qb1, z, 0, 0, 0);
-      if (mrow < NQ && t < ntile) {
-        f32x4 out;
+      f32x4 out;
+      if constexpr (KV8) {
+        const f16x8 a0 = dequant_h8(kr[buf][i][0], 127u), a1 = dequant_h8(kr[buf][i][1], 127u);
+        const f32x4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+        const f32x4 d0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, qb0, z, 0, 0, 0);
+        const f32x4 d1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, qb1, z, 0, 0, 0);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const uint32_t sp = (ksr[buf][i][r >> 1] >> (16 * (r & 1))) & 0xffffu;
           out[r] = (e8m0(sp & 0xffu) * d0[r] + e8m0(sp >> 8) * d1[r]) * scale;
         }
-        *reinterpret_cast<f32x4*>(&sc[min(mrow, NQ - 1)][t * 16 + 4 * gq]) = out;
+      } else {  // (f16: dec_attn_kernel MFC's arithmetic)
+        const f32x4 d = xscore16(kf[buf][i][0], kf[buf][i][1], qb0, qb1);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[r] = d[r] * scale;
       }
+      if (mrow < NQ && t < ntile)
+        *reinterpret_cast<f32x4*>(&sc[min(mrow, NQ - 1)][t * 16 + 4 * gq]) = out;
     };
 #pragma unroll 1
     for (int grp = 0; grp < ngrp; grp += 2) {
@@ -873,7 +957,11 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
         for (int i = 0; i < TD; ++i) score_tile(1, i, wid + 4 * (TD * (grp + 1) + i));
       }
     }
-    if (wid < nt32) v_load(wid);  // (in flight across the softmax)
+    if constexpr (KV8) {
+      if (wid < nt32) v_load(wid);  // (in flight across the softmax)
+    } else {
+      LOADROWS16(ka, V, 0, 0)
+    }
   } else if constexpr (NBC > 0) {
 #pragma unroll 1
     for (int b = 0; b < NBC - 1; ++b) k_trip(b, false);
@@ -924,7 +1012,7 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
     for (int j = tid; j < n; j += 256) sc[q][j] = (float)f16r(sc[q][j] * inv);
   }
   __syncthreads();
-  if constexpr (MFS) {
+  if constexpr (MFS && KV8) {
     auto e8m0 = [](uint32_t e) { return e ? __uint_as_float(e << 23) : __uint_as_float(0x00400000u); };
     uint8_t* vw = &vtile[0][0] + wid * (32 * 64);
     f32x4 oacc[4];
@@ -1275,6 +1363,13 @@ __global__ __launch_bounds__(256) void dec_xattn8_kernel(
   }
 }
 
+// f16 cross K/V caches: scores on MFMA in the single-row and the grouped
+// kernels together (xscore16; MWX_XATTN_MFC=1, A/B)
+static bool xattn_mfc() {
+  static const bool on = getenv("MWX_XATTN_MFC") && atoi(getenv("MWX_XATTN_MFC")) != 0;
+  return on;
+}
+
 template <typename T>
 bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float* bias,
                                  const void* kbase, const void* vbase, const int* kv_index,
@@ -1331,6 +1426,9 @@ bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float*
     if (kv8 && mfs)                            \
       dec_xattn_kernel<T, N, true, true, 0, true><<<g, 256, 0, st>>>(P, KS, pcols, bias, kbase, \
           vbase, kscale8, vscale8, kv_index, active, n_keys, cap, R, o, H, scale, span);       \
+    else if (!kv8 && xattn_mfc())              \
+      dec_xattn_kernel<T, N, false, true, 0, true><<<g, 256, 0, st>>>(P, KS, pcols, bias,   \
+          kbase, vbase, kscale8, vscale8, kv_index, active, n_keys, cap, R, o, H, scale, span); \
     else if (kv8 && nt)                        \
       XL(N, true, true);                       \
     else if (kv8)                              \
@@ -1456,6 +1554,15 @@ void dec_attention(const float* P, int KS, int pcols, const float* bias, float q
           kv_len_cap, o, H, scale, nullptr, nullptr, 0, nq, R, 1, span);
     else
       dec_attn_kernel<T, false, 8, false, 6, 7><<<gp, 256, 0, st>>>(
+          P, KS, pcols, bias, qscale, kscale, kbase, vbase, kv_index, pos, active, fixed_len,
+          kv_len_cap, o, H, scale, nullptr, nullptr, 0, nq, R, 1, span);
+  } else if (xattn_mfc() && fixed_len == 1500 && xattn_nbc) {
+    if (xattn_nt)
+      dec_attn_kernel<T, false, 8, true, 6, 0, true><<<g, 256, 0, st>>>(
+          P, KS, pcols, bias, qscale, kscale, kbase, vbase, kv_index, pos, active, fixed_len,
+          kv_len_cap, o, H, scale, nullptr, nullptr, 0, nq, R, 1, span);
+    else
+      dec_attn_kernel<T, false, 8, false, 6, 0, true><<<g, 256, 0, st>>>(
           P, KS, pcols, bias, qscale, kscale, kbase, vbase, kv_index, pos, active, fixed_len,
           kv_len_cap, o, H, scale, nullptr, nullptr, 0, nq, R, 1, span);
   } else if (xattn_nt && fixed_len == 1500 && xattn_nbc)  // (every Whisper model: 1500 frames)
