@@ -20,6 +20,7 @@
 #   b5one / b5nr / bench1nr  beam 5 one lane with / without decode row-block grouping; C3 one lane without
 #   bench1g16 / bench1g32 / pmcg32  encoder tile-order group of 16 / 32 row tiles (one lane; FETCH pass)
 #   testsmfc / b5mfc / bench1mfc / benchqmfc  the same with the f16 cross-attention scores on MFMA (MWX_XATTN_MFC=1)
+#   benchqnp / bench1np8  the instrumented (span) step graph replayed only once (A/B of the live timing's cost)
 #   pairtest   the paired-decode parity tests only
 #   b5         beam 5 (service default decode), C3 shape
 #   c5         C5: MX-fp8, beam 5, 600-s long-form clips
@@ -84,6 +85,8 @@ for s in "$@"; do
     b5mfc) run b5mfc 500 env MWX_XATTN_MFC=1 python -u bench.py --beam 5 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
     bench1mfc) run bench1mfc 400 env MWX_XATTN_MFC=1 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
     benchqmfc) run benchqmfc 400 env MWX_XATTN_MFC=1 python -u bench.py --steps 8 --warmup 2 --no-cpu-baseline ;;
+    benchqnp) run benchqnp 400 env MWX_PERF_PERIOD=1000000 python -u bench.py --steps 8 --warmup 2 --no-cpu-baseline ;;
+    bench1np8) run bench1np8 400 env MWX_PERF_PERIOD=1000000 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
     pairtest) run pairtest 600 python -u -m pytest tests/test_gpu_pair.py -m gpu -x -v -s -rf --timeout 300 --timeout-method thread ;;
     b5) run b5 500 python -u bench.py --beam 5 --steps 4 --warmup 1 --no-cpu-baseline ;;
     c5) run c5 700 python -u bench.py --fp8 --beam 5 --clip-seconds 600 --steps 2 --warmup 1 --no-cpu-baseline ;;
