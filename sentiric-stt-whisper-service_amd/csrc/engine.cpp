@@ -310,12 +310,11 @@ static void harvest_spans(State& S, bool graph, hipStream_t zs = nullptr) {
     S.perf_acc_ms[c] += (double)(t1 - t0) * S.span_tick_ms;
     S.perf_acc_n[c] += 1;
   }
-  if (!graph) {
-    // (re-zeroed for the next launches, ordered before them on the state's stream)
-    HIPC(hipMemsetAsync((unsigned long long*)S.perf_span.p + su * base, 0, n * su * 8,
-                        zs ? zs : S.stream));
-    S.span_eused = 0;
-  }
+  // re-zeroed for the next launches, ordered before them on the state's
+  // stream (graph slots: the next instrumented replay is queued after this)
+  HIPC(hipMemsetAsync((unsigned long long*)S.perf_span.p + su * base, 0, n * su * 8,
+                      zs ? zs : S.stream));
+  if (!graph) S.span_eused = 0;
 }
 
 static int perf_class_index(const State& S, const char* cls) {
@@ -332,18 +331,19 @@ static bool perf_on(const State& s, const char* cls) {
 
 // The stamp pair a launch of class `cls` writes its span to (kcommon.h
 // span_start / span_end) when "<cls>.span" is an enabled perf class, else
-// nullptr. In an instrumented graph capture the first slot adds one memset
-// node zeroing every graph slot; eager slots are used once each between two
-// harvests, which re-zero them.
+// nullptr. Slots are used once between two harvests, which re-zero them on
+// the state's stream (no memset node in the instrumented graph: a blit node
+// there lengthened the instrumented replays).
 static unsigned long long* span_slot(State& S, const char* cls, hipStream_t s) {
   if (S.perf_class.empty() || (S.capturing && !S.capture_perf) || !S.perf_span.p) return nullptr;
   const int ci = perf_class_index(S, (std::string(cls) + ".span").c_str());
   if (ci < 0) return nullptr;
   unsigned long long* base = (unsigned long long*)S.perf_span.p;
   if (S.capturing) {
+    // (graph slots are zero when the instrumented graph replays: zeroed at
+    // allocation and re-zeroed on the state's stream by each harvest, which
+    // follows every instrumented replay)
     if (S.span_gused >= (size_t)State::SPAN_G) return nullptr;
-    if (S.span_gused == 0)
-      HIPC(hipMemsetAsync(base, 0, (size_t)State::SPAN_G * SPAN_SLOT_U64 * 8, s));
     if (S.span_gtag.size() <= S.span_gused) S.span_gtag.resize(S.span_gused + 1);
     S.span_gtag[S.span_gused] = ci;
     return base + SPAN_SLOT_U64 * S.span_gused++;
