@@ -291,7 +291,7 @@ static int perf_class_index(const State& S, const char* cls);
 // eager: after the state's stream has drained)
 static void harvest_spans(State& S, bool graph, hipStream_t zs = nullptr) {
   const size_t n = graph ? S.span_gused : S.span_eused;
-  if (n == 0 || !S.span_host) return;
+  if (n == 0 || !S.span_host || !S.span_stream) return;
   const size_t base = graph ? 0 : State::SPAN_G;
   const size_t su = SPAN_SLOT_U64;
   HIPC(hipMemcpyAsync(S.span_host, (unsigned long long*)S.perf_span.p + su * base, n * su * 8,
