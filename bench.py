@@ -586,10 +586,6 @@ def main():
     ap.add_argument("--lanes", type=int, default=2,
                     help="concurrent batches (host threads, each with its own states and HIP "
                          "stream), as the SttEngine's parallel_requests batchers run them")
-    ap.add_argument("--pair", action="store_true",
-                    help="each lane's state decodes two batches of --clips clips as one step "
-                         "graph with the two row sets' cross-attentions interleaved "
-                         "(MWX_DECODE_PAIR, engine.cpp decode_group_pair)")
     ap.add_argument("--lane-stagger", type=float, default=0.0,
                     help="seconds lane i waits (x i) before its first timed batch")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -612,11 +608,6 @@ def main():
     args = ap.parse_args()
     if args.prompt_leg:
         args.rich, args.decode_steps, args.clip_seconds = True, 0, 600.0
-    if args.pair:
-        # (read by the engine at its first decode step)
-        os.environ["MWX_DECODE_PAIR"] = "1"
-        args.batch_clips = args.clips
-        args.clips *= 2
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return launch_ranks(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -809,15 +800,10 @@ def main():
             # the two event nodes' own cost (+ the empty kernel)
             ev_s = tm["event_bracket"][0] / 1e3 / tm["event_bracket"][1]
         avg_s = avg_raw - ev_s if ev_s is not None and ev_s < 0.5 * avg_raw else avg_raw
-        # decode kernels run per row group (MWX_DECODE_GROUPS chains on their
-        # own streams, default 1); the engine times every 8th decode step's
-        # launches (MWX_PERF_PERIOD), all inside the timed region
+        # the engine times every 8th decode step's launches (MWX_PERF_PERIOD),
+        # all inside the timed region
         rows = args.clips * max(1, args.beam)
-        if args.perf_class.startswith("dec_attn"):
-            rows = rows / max(1, int(os.environ.get("MWX_DECODE_GROUPS", "1")))
-            if os.environ.get("MWX_DECODE_PAIR", "0") not in ("", "0"):
-                rows = rows / 2  # two interleaved row sets per step (engine.cpp)
-        clips_per_launch = args.clips * (rows / (args.clips * max(1, args.beam)))
+        clips_per_launch = args.clips
         bound, work, desc = kernel_model(args.arch, args.perf_class, clips_per_launch, rows,
                                          launches // max(1, nsteps), prompt_len,
                                          args.decode_steps, n_windows, kv8=args.fp8)
@@ -903,12 +889,9 @@ def main():
                      + "; seeded weights in the ggml .bin layout)"),
             "config": {
                 "workload": (f"whisper-{args.arch}{' (-rich weights)' if args.rich else ''} "
-                             f"{args.wtype}: batches of {args.batch_clips if args.pair else args.clips} x "
-                             f"{args.clip_seconds:g} s clips per GPU "
-                             + (f"({2 * lanes} in flight: {lanes} lane(s), each decoding two batches "
-                                f"as interleaved row sets of one step graph), mel + "
-                                if args.pair else f"({lanes} in flight), mel + ")
-                             + f"encoder + cross-KV + {args.decode_steps or 'until-EOT'} "
+                             f"{args.wtype}: batches of {args.clips} x "
+                             f"{args.clip_seconds:g} s clips per GPU ({lanes} in flight), mel + "
+                             f"encoder + cross-KV + {args.decode_steps or 'until-EOT'} "
                              f"{'beam-%d' % args.beam if args.beam > 1 else 'greedy'} KV-cached "
                              f"decode steps per 30-s window, token timestamps on (as the service), RCCL "
                              f"token gather to rank 0"),
@@ -916,7 +899,6 @@ def main():
                 "seq_len": 1500,
                 "parallelism": f"dp{world}",
                 "lanes": lanes,
-                "row_sets_per_lane": 2 if args.pair else 1,
             },
             "audio_sec_per_s_per_gpu": round(value / world, 2),
             "rtf": round(elapsed / audio_s * world, 6),

@@ -930,8 +930,10 @@ static void compute_probs(const std::vector<float>& logits, int n, const std::ve
   for (int i = 0; i < n; ++i) pr[i] = logits[i] == -INFINITY ? 0.0f : expf(lp[i]);
 }
 
+// ts_mass_rule = false leaves out the last step (the timestamp-mass rule), a
+// test hook of orc_process_logits
 static void process_logits(const Model& m, const Params& P, Decoder& dec, const float* raw,
-                           float temperature) {
+                           float temperature, bool ts_mass_rule = true) {
   const int n = m.n_vocab;
   const auto& toks = dec.seq.tokens;
   const bool is_initial = toks.empty();
@@ -993,7 +995,7 @@ static void process_logits(const Model& m, const Params& P, Decoder& dec, const 
     for (int i = m.beg; i < m.beg + tid0; ++i) logits[i] = -INFINITY;
   }
   compute_logprobs(logits, n, dec.logprobs);
-  {
+  if (ts_mass_rule) {
     float ts_logprob = -INFINITY;
     {
       float lse = 0.0f;
@@ -1839,6 +1841,48 @@ void orc_full_token(void* r, int i, int j, int* ids, float* f, int64_t* t) {
   f[3] = tk.ptsum;
   t[0] = tk.t0;
   t[1] = tk.t1;
+}
+// whisper_process_logits + whisper_sample_token(best = true) on ONE raw logits
+// row for a decoder whose sampled tokens so far are hist[0..n_hist) (the
+// token-loop rules pinned against HF's Whisper logits processors,
+// tests/test_oracle_golden.py). has_ts / seek_delta are the decoder state the
+// loop derives from hist (full() above). ip: [suppress_blank, suppress_nst,
+// no_timestamps, tdrz, bench_fixed_steps, skip_ts_mass]; skip_ts_mass = 1
+// returns the logits before the "sum p(timestamps) > max p(text)" rule (a
+// test hook: that rule is the last step of process_logits). fp: [temperature,
+// max_initial_ts]. out_logits / out_logprobs / out_probs: [n_vocab];
+// tok_i = {id, tid}, tok_f = {p, plog, pt, ptsum}.
+void orc_process_logits(void* h, const float* raw, const int* hist, int n_hist, int has_ts,
+                        int seek_delta, const int* ip, const float* fp, float* out_logits,
+                        float* out_logprobs, float* out_probs, int* tok_i, float* tok_f) {
+  const Model& m = *(const Model*)h;
+  Params P;
+  P.suppress_blank = ip[0];
+  P.suppress_nst = ip[1];
+  P.no_timestamps = ip[2];
+  P.tdrz_enable = ip[3];
+  P.bench_fixed_steps = ip[4];
+  P.max_initial_ts = fp[1];
+  Decoder d;
+  for (int i = 0; i < n_hist; ++i) {
+    TokenData t;
+    t.id = hist[i];
+    d.seq.tokens.push_back(t);
+  }
+  d.has_ts = has_ts != 0;
+  d.seek_delta = seek_delta;
+  const int n = m.n_vocab;
+  process_logits(m, P, d, raw, fp[0], ip[5] == 0);
+  memcpy(out_logits, d.logits.data(), (size_t)n * 4);
+  memcpy(out_logprobs, d.logprobs.data(), (size_t)n * 4);
+  memcpy(out_probs, d.probs.data(), (size_t)n * 4);
+  const TokenData t = sample_token(m, d, true);
+  tok_i[0] = t.id;
+  tok_i[1] = t.tid;
+  tok_f[0] = t.p;
+  tok_f[1] = t.plog;
+  tok_f[2] = t.pt;
+  tok_f[3] = t.ptsum;
 }
 int orc_full_lang_id(void* r) { return ((OrcFull*)r)->r.lang_id; }
 int orc_full_n_windows(void* r) { return (int)((OrcFull*)r)->r.window_tokens.size(); }

@@ -80,6 +80,9 @@ def lib() -> C.CDLL:
     L.orc_full_n_windows.argtypes = [P]
     L.orc_full_window_tokens.restype = C.c_int
     L.orc_full_window_tokens.argtypes = [P, C.c_int, C.POINTER(C.c_int), C.c_int]
+    L.orc_process_logits.restype = None
+    L.orc_process_logits.argtypes = [P, fp, C.POINTER(C.c_int), C.c_int, C.c_int, C.c_int,
+                                     C.POINTER(C.c_int), fp, fp, fp, fp, C.POINTER(C.c_int), fp]
     L.orc_prosody.restype = None
     L.orc_prosody.argtypes = [fp, C.c_int64, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, P]
     L.orc_resample.restype = C.c_long
@@ -244,6 +247,28 @@ class Oracle:
         lib().orc_decode_seq(self.h, _fp(np.ascontiguousarray(k)), _fp(np.ascontiguousarray(v)),
                              toks.ctypes.data_as(C.POINTER(C.c_int)), len(toks), _fp(out))
         return out
+
+    def process_logits(self, raw, history, has_ts: bool, seek_delta: int, *,
+                       suppress_blank=True, suppress_nst=False, no_timestamps=False, tdrz=False,
+                       bench_fixed_steps=0, ts_mass_rule=True, temperature=0.0,
+                       max_initial_ts=1.0):
+        """whisper_process_logits + greedy whisper_sample_token on one raw
+        logits row for a decoder whose sampled tokens are `history`; returns
+        (logits, logprobs, probs, (id, tid, p, plog, pt, ptsum))."""
+        V = self.n_vocab
+        raw = np.ascontiguousarray(raw, np.float32)
+        assert raw.shape == (V,)
+        hist = np.ascontiguousarray(history, np.int32)
+        ip = (C.c_int * 6)(int(suppress_blank), int(suppress_nst), int(no_timestamps), int(tdrz),
+                           int(bench_fixed_steps), 0 if ts_mass_rule else 1)
+        fpv = (C.c_float * 2)(temperature, max_initial_ts)
+        lg, lp, pr = (np.empty(V, np.float32) for _ in range(3))
+        ti = (C.c_int * 2)()
+        tf = (C.c_float * 4)()
+        lib().orc_process_logits(self.h, _fp(raw), hist.ctypes.data_as(C.POINTER(C.c_int)),
+                                 len(hist), int(has_ts), int(seek_delta), ip, fpv, _fp(lg),
+                                 _fp(lp), _fp(pr), ti, tf)
+        return lg, lp, pr, (ti[0], ti[1], tf[0], tf[1], tf[2], tf[3])
 
     def full_external(self, pcm: np.ndarray, opt: FullOptions, encode_fn, logits_fn):
         """full() with every decode answered by callbacks: encode_fn(seek) and

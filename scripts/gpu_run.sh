@@ -8,20 +8,15 @@
 #   benchq     default bench without the CPU baseline (quick)
 #   bench1     C3 on one lane
 #   c2         C2: base f16, one clip per request
-#   c2pf       C2 with L2-prefetch helper workgroups in the cross-attention (MWX_XATTN_PF)
 #   c2nt       C2 with the cross K/V streamed non-temporally (A/B of the MALL-resident default)
-#   x64 / g2x64  64 clips in one state, one decode chain / two row groups on two streams
-#   pair64     64 clips in one state, decoded as two interleaved 32-row sets (MWX_DECODE_PAIR)
-#   pair64x2   the same on two lanes
-#   pair32 / pair32x2  one 32-clip batch per lane split into two interleaved 16-row sets
+#   b5one      beam 5 on one lane
+#   bench1nc / benchqnc  C3 one lane / 2 lanes with the chained decode seams off (MWX_CHAIN=0, A/B)
+#   probe      the decode-chain probe (scripts/probe/dec_chain_probe): seams bit-exact + per-layer times
 #   mfstest    the MX-fp8 tests with the MFMA-score cross-attention (MWX_XATTN_MFS=1)
 #   c5mfs / c5one  C5 on one lane with / without the MFMA scores
 #   bench1np / bench1g0  one lane without the prompt prefill / with row-major encoder tile order
-#   b5one / b5nr / bench1nr  beam 5 one lane with / without decode row-block grouping; C3 one lane without
 #   bench1g16 / bench1g32 / pmcg32  encoder tile-order group of 16 / 32 row tiles (one lane; FETCH pass)
-#   testsmfc / b5mfc / bench1mfc / benchqmfc  the same with the f16 cross-attention scores on MFMA (MWX_XATTN_MFC=1)
 #   benchqnp / bench1np8  the instrumented (span) step graph replayed only once (A/B of the live timing's cost)
-#   pairtest   the paired-decode parity tests only
 #   b5         beam 5 (service default decode), C3 shape
 #   c5         C5: MX-fp8, beam 5, 600-s long-form clips
 #   prompt     long-form leg with previous-window text carried as the prompt
@@ -62,32 +57,21 @@ for s in "$@"; do
     benchq) run benchq 400 python -u bench.py --steps 8 --warmup 2 --no-cpu-baseline ;;
     bench1) run bench1 400 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
     c2) run c2 300 python -u bench.py --arch base --wtype f16 --clips 1 --lanes 1 --steps 20 --warmup 3 --no-cpu-baseline ;;
-    c2pf) run c2pf 300 env MWX_XATTN_PF=7 python -u bench.py --arch base --wtype f16 --clips 1 --lanes 1 --steps 20 --warmup 3 --no-cpu-baseline ;;
     c2nt) run c2nt 300 env MWX_XATTN_NT=1 python -u bench.py --arch base --wtype f16 --clips 1 --lanes 1 --steps 20 --warmup 3 --no-cpu-baseline ;;
-    x64) run x64 500 python -u bench.py --clips 64 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
-    g2x64) run g2x64 500 env MWX_DECODE_GROUPS=2 python -u bench.py --clips 64 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
-    pair64) run pair64 500 python -u bench.py --pair --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
-    pair64x2) run pair64x2 600 python -u bench.py --pair --lanes 2 --steps 4 --warmup 1 --no-cpu-baseline ;;
-    pair32) run pair32 500 env MWX_DECODE_PAIR=1 python -u bench.py --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
-    pair32x2) run pair32x2 500 env MWX_DECODE_PAIR=1 python -u bench.py --lanes 2 --steps 4 --warmup 1 --no-cpu-baseline ;;
     mfstest) run mfstest 600 env MWX_XATTN_MFS=1 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shapes.py -k "mxfp8" -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
     c5mfs) run c5mfs 700 env MWX_XATTN_MFS=1 python -u bench.py --fp8 --beam 5 --clip-seconds 600 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline ;;
     c5one) run c5one 700 python -u bench.py --fp8 --beam 5 --clip-seconds 600 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline ;;
     bench1np) run bench1np 400 env MWX_PREFILL_MIN=0 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
     bench1g0) run bench1g0 400 env MWX_GEMM_GROUP=0 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
     b5one) run b5one 500 python -u bench.py --beam 5 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
-    b5nr) run b5nr 500 env MWX_DEC_GROUP_ROWS=0 python -u bench.py --beam 5 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
-    bench1nr) run bench1nr 400 env MWX_DEC_GROUP_ROWS=0 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
     bench1g16) run bench1g16 400 env MWX_GEMM_GROUP=16 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
     bench1g32) run bench1g32 400 env MWX_GEMM_GROUP=32 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
     pmcg32) (export MWX_GEMM_GROUP=32; cd /tmp && run pmcg32_FETCH_SIZE 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/${TAG}_pmcg32_FETCH_SIZE" -o pmc -- $B --lanes 1 --steps 1 --warmup 0 --decode-steps 8 --no-cpu-baseline) || exit 5 ;;
-    testsmfc) run testsmfc 1150 env MWX_XATTN_MFC=1 python -u -m pytest tests -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
-    b5mfc) run b5mfc 500 env MWX_XATTN_MFC=1 python -u bench.py --beam 5 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
-    bench1mfc) run bench1mfc 400 env MWX_XATTN_MFC=1 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
-    benchqmfc) run benchqmfc 400 env MWX_XATTN_MFC=1 python -u bench.py --steps 8 --warmup 2 --no-cpu-baseline ;;
+    bench1nc) run bench1nc 400 env MWX_CHAIN=0 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
+    benchqnc) run benchqnc 400 env MWX_CHAIN=0 python -u bench.py --steps 8 --warmup 2 --no-cpu-baseline ;;
+    probe) run probe 200 env PROBE_ONLY=seam ./scripts/probe/dec_chain_probe 32 10 && run probel 200 env PROBE_ONLY=layer ./scripts/probe/dec_chain_probe 32 10 ;;
     benchqnp) run benchqnp 400 env MWX_PERF_PERIOD=1000000 python -u bench.py --steps 8 --warmup 2 --no-cpu-baseline ;;
     bench1np8) run bench1np8 400 env MWX_PERF_PERIOD=1000000 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
-    pairtest) run pairtest 600 python -u -m pytest tests/test_gpu_pair.py -m gpu -x -v -s -rf --timeout 300 --timeout-method thread ;;
     b5) run b5 500 python -u bench.py --beam 5 --steps 4 --warmup 1 --no-cpu-baseline ;;
     c5) run c5 700 python -u bench.py --fp8 --beam 5 --clip-seconds 600 --steps 2 --warmup 1 --no-cpu-baseline ;;
     prompt) run prompt 700 python -u bench.py --prompt-leg --steps 2 --warmup 1 --no-cpu-baseline ;;

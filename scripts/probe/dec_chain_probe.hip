@@ -9,6 +9,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <functional>
 #include <string>
 #include <vector>
@@ -232,6 +233,120 @@ int main(int argc, char** argv) {
       CK(hipStreamWaitEvent(s, jn, 0));
     }
   };
+  // fused seams (k_chain.hip): counters [L][3][8], zeroed at the head of each
+  // replay by a memset node (the engine zeroes them in the step's embedding)
+  unsigned *ctrs, *cerr;
+  CK(hipMalloc(&ctrs, (size_t)L * 3 * chain_slot_words() * 4));
+  CK(hipMalloc(&cerr, 4));
+  CK(hipMemset(ctrs, 0, (size_t)L * 3 * chain_slot_words() * 4));
+  CK(hipMemset(cerr, 0, 4));
+  float* slab2;
+  CK(hipMalloc(&slab2, (size_t)8 * R * 3 * d * 4));
+  auto chain = [&](int l, int site, const T* pA, const T* pW, int pK, const T* cW, int cN,
+                   bool skinny, float* cP) {
+    ChainArgs a;
+    a.M = R;
+    a.d = d;
+    a.p_A = pA;
+    a.p_W = pW;
+    a.p_K = pK;
+    a.ln.x = x;
+    a.ln.w = lnw;
+    a.ln.b = lnb;
+    a.ln.P = slab;
+    a.ln.pbias = bias;
+    a.ln.y = hd;
+    a.ln.active = act;
+    a.c_W = cW;
+    a.c_N = cN;
+    a.c_skinny = skinny;
+    a.c_P = cP;
+    a.c_epi = ep_gelu();
+    a.ctr = ctrs + ((size_t)l * 3 + site) * chain_slot_words();
+    a.err = cerr;
+    if (!chain_launch<T>(a, s)) {
+      fprintf(stderr, "chain_launch unsupported\n");
+      exit(1);
+    }
+  };
+  auto chain_layer = [&](int l) {
+    if (l == 0) CK(hipMemsetAsync(ctrs, 0, (size_t)L * 3 * chain_slot_words() * 4, s));
+    dec_attention<T>(slab2, 5, 3 * d, bias, kqs, kqs, (_Float16*)kself + (l & 1) * self_elems,
+                     (_Float16*)vself + (l & 1) * self_elems, nullptr, pos, act, 0, Tctx, od, R, H,
+                     1.0f, s, kvmap, kvown, 0, 1);
+    chain(l, 0, od, wl(l, 1), d, wl(l, 2), d, false, slab2);  // out -> LN2 -> cross-Q
+    dec_attention<T>(slab2, 5, d, bias, 1.0f, 1.0f, (_Float16*)ck + (l & 1) * cross_elems,
+                     (_Float16*)cv + (l & 1) * cross_elems, xidx, pos, act, Lc, Lc, od, R, H, kqs, s);
+    chain(l, 1, od, wl(l, 3), d, wl(l, 4), 4 * d, true, nullptr);  // cross-out -> LN3 -> FFN1
+    chain(l, 2, ffd, wl(l, 5), 4 * d, wl((l + 1) % L, 0), 3 * d, false, slab2);  // FFN2 -> LN1 -> QKV
+  };
+  // ---- bit-exactness: each fused seam == its three launches (same inputs) ----
+  {
+    fill_kernel<<<1024, 256>>>((uint16_t*)od, R64 * d, 21);
+    fill_kernel<<<1024, 256>>>((uint16_t*)ffd, R64 * 4 * d, 22);
+    // slab rows of the producer must be finite garbage-free: the producers write them
+    CK(hipDeviceSynchronize());
+    std::vector<float> x0((size_t)R * d);
+    CK(hipMemcpy(x0.data(), x, x0.size() * 4, hipMemcpyDeviceToHost));
+    const size_t hdn = R64 * d, ffn = R64 * 4 * d, sln = (size_t)8 * R * 3 * d;
+    auto snap = [&](std::vector<float>& hx, std::vector<uint16_t>& hh, std::vector<uint16_t>& hf,
+                    std::vector<float>& hs) {
+      CK(hipDeviceSynchronize());
+      hx.resize((size_t)R * d);
+      hh.resize(hdn);
+      hf.resize(ffn);
+      hs.resize(sln);
+      CK(hipMemcpy(hx.data(), x, hx.size() * 4, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(hh.data(), hd, hdn * 2, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(hf.data(), ffd, ffn * 2, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(hs.data(), slab2, sln * 4, hipMemcpyDeviceToHost));
+    };
+    auto reset = [&]() {
+      CK(hipMemcpy(x, x0.data(), x0.size() * 4, hipMemcpyHostToDevice));
+      CK(hipMemset(hd, 0, hdn * 2));
+      CK(hipMemset(slab2, 0, sln * 4));
+      CK(hipMemset(ctrs, 0, (size_t)L * 3 * chain_slot_words() * 4));
+      fill_kernel<<<1024, 256>>>((uint16_t*)ffd, ffn, 22);
+      CK(hipDeviceSynchronize());
+    };
+    const char* names[3] = {"o+ln+cq", "co+ln+fc1", "fc2+ln+qkv"};
+    for (int site = 0; site < 3; ++site) {
+      std::vector<float> ax, as, bx, bs;
+      std::vector<uint16_t> ah, af, bh, bf;
+      reset();
+      if (site == 0) {
+        gemm_splitk_partials<T>(od, wl(0, 1), R, d, d, slab, s);
+        layer_norm_dec<T>(x, lnw, lnb, hd, R, d, act, s, slab, 5, bias);
+        gemm_splitk_partials<T>(hd, wl(0, 2), R, d, d, slab2, s);
+      } else if (site == 1) {
+        gemm_splitk_partials<T>(od, wl(0, 3), R, d, d, slab, s);
+        layer_norm_dec<T>(x, lnw, lnb, hd, R, d, act, s, slab, 5, bias);
+        EpiParams e = ep_gelu();
+        e.nw = 4;
+        gemm_decode<T>(EPI_GELU, hd, wl(0, 4), R, 4 * d, d, e, s);
+      } else {
+        gemm_splitk_partials<T>(ffd, wl(0, 5), R, d, 4 * d, slab, s);
+        layer_norm_dec<T>(x, lnw, lnb, hd, R, d, act, s, slab, 8, bias);
+        gemm_splitk_partials<T>(hd, wl(1, 0), R, 3 * d, d, slab2, s);
+      }
+      snap(ax, ah, af, as);
+      reset();
+      if (site == 0) chain(0, 0, od, wl(0, 1), d, wl(0, 2), d, false, slab2);
+      if (site == 1) chain(0, 1, od, wl(0, 3), d, wl(0, 4), 4 * d, true, nullptr);
+      if (site == 2) chain(0, 2, ffd, wl(0, 5), 4 * d, wl(1, 0), 3 * d, false, slab2);
+      snap(bx, bh, bf, bs);
+      unsigned herr = 0;
+      CK(hipMemcpy(&herr, cerr, 4, hipMemcpyDeviceToHost));
+      const bool ok = ax == bx && ah == bh && af == bf && memcmp(as.data(), bs.data(), as.size() * 4) == 0;
+      size_t dx = 0, dh = 0, df = 0, ds = 0;
+      for (size_t i = 0; i < ax.size(); ++i) dx += memcmp(&ax[i], &bx[i], 4) != 0;
+      for (size_t i = 0; i < ah.size(); ++i) dh += ah[i] != bh[i];
+      for (size_t i = 0; i < af.size(); ++i) df += af[i] != bf[i];
+      for (size_t i = 0; i < as.size(); ++i) ds += memcmp(&as[i], &bs[i], 4) != 0;
+      printf("verify seam %-12s %s (diff x %zu, hd %zu, ffd %zu, slabs %zu; err %u)\n", names[site],
+             ok ? "BIT-EXACT" : "MISMATCH", dx, dh, df, ds, herr);
+    }
+  }
   struct Op {
     std::string name;
     int launches_per_layer;
@@ -285,6 +400,42 @@ int main(int argc, char** argv) {
          logits_process(logits, smask, ctl, tout, nullptr, nullptr, LCo, R, LPScratch{flt, parts, lres}, s);
        }},
       {"FULL layer (11 launches)", 11, [&](int l) { full_layer(l, 0); }},
+      {"CHAIN layer (5 launches)", 5, [&](int l) { chain_layer(l); }},
+      {"seam o+ln+cq (3 launches)", 3,
+       [&](int l) {
+         gemm_splitk_partials<T>(od, wl(l, 1), R, d, d, slab, s);
+         layer_norm_dec<T>(x, lnw, lnb, hd, R, d, act, s, slab, 5, bias);
+         gemm_splitk_partials<T>(hd, wl(l, 2), R, d, d, slab2, s);
+       }},
+      {"CHAIN seam o+ln+cq (1 launch)", 1,
+       [&](int l) {
+         if (l == 0) CK(hipMemsetAsync(ctrs, 0, (size_t)L * 3 * chain_slot_words() * 4, s));
+         chain(l, 0, od, wl(l, 1), d, wl(l, 2), d, false, slab2);
+       }},
+      {"seam fc2+ln+qkv (3 launches)", 3,
+       [&](int l) {
+         gemm_splitk_partials<T>(ffd, wl(l, 5), R, d, 4 * d, slab, s);
+         layer_norm_dec<T>(x, lnw, lnb, hd, R, d, act, s, slab, 8, bias);
+         gemm_splitk_partials<T>(hd, wl((l + 1) % L, 0), R, 3 * d, d, slab2, s);
+       }},
+      {"CHAIN seam fc2+ln+qkv (1 launch)", 1,
+       [&](int l) {
+         if (l == 0) CK(hipMemsetAsync(ctrs, 0, (size_t)L * 3 * chain_slot_words() * 4, s));
+         chain(l, 2, ffd, wl(l, 5), 4 * d, wl((l + 1) % L, 0), 3 * d, false, slab2);
+       }},
+      {"seam co+ln+fc1 (3 launches)", 3,
+       [&](int l) {
+         gemm_splitk_partials<T>(od, wl(l, 3), R, d, d, slab, s);
+         layer_norm_dec<T>(x, lnw, lnb, hd, R, d, act, s, slab, 5, bias);
+         EpiParams e = ep_gelu();
+         e.nw = 4;
+         gemm_decode<T>(EPI_GELU, hd, wl(l, 4), R, 4 * d, d, e, s);
+       }},
+      {"CHAIN seam co+ln+fc1 (1 launch)", 1,
+       [&](int l) {
+         if (l == 0) CK(hipMemsetAsync(ctrs, 0, (size_t)L * 3 * chain_slot_words() * 4, s));
+         chain(l, 1, od, wl(l, 3), d, wl(l, 4), 4 * d, true, nullptr);
+       }},
       {"FULL layer + prefetch next at start", 11, [&](int l) { full_layer(l, 1); }},
       {"FULL layer + prefetch next after xattn", 11, [&](int l) { full_layer(l, 2); }},
       {"touch one layer's weights", 1,
@@ -326,6 +477,12 @@ int main(int argc, char** argv) {
     CK(hipEventElapsedTime(&ms, a, b));
     const double per_layer = ms * 1e3 / reps / L;
     printf("%-38s %10.2f %12.2f\n", op.name.c_str(), per_layer / op.launches_per_layer, per_layer);
+    unsigned herr = 0;
+    CK(hipMemcpy(&herr, cerr, 4, hipMemcpyDeviceToHost));
+    if (herr) {
+      printf("  !! chain hand-off wait timed out\n");
+      CK(hipMemset(cerr, 0, 4));
+    }
     CK(hipGraphExecDestroy(ge));
     CK(hipGraphDestroy(g));
   }

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -40,6 +41,13 @@
 namespace mwx {
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// chained decode seams on (1) / off (0) / from MWX_CHAIN (-1, the default);
+// mwx_test_set_chain sets it for the A/B tests
+inline std::atomic<int>& chain_mode() {
+  static std::atomic<int> m{-1};
+  return m;
+}
 
 // Process-wide order between graph capture and (de)allocation: while any
 // thread captures a stream, HIP rejects legacy-stream operations such as
@@ -141,19 +149,9 @@ struct Segment {
   bool speaker_turn_next;
 };
 
-constexpr int MWX_MAX_GROUPS = 4;
-
 struct State {
   Context* ctx = nullptr;
   hipStream_t stream = nullptr;
-  // decode row groups: group g > 0 runs on gstream[g] (group 0 on `stream`);
-  // ev_in orders the groups after the step inputs, ev_done joins them
-  hipStream_t gstream[MWX_MAX_GROUPS] = {};
-  hipEvent_t ev_in = nullptr, ev_done[MWX_MAX_GROUPS] = {};
-  // paired decode (MWX_DECODE_PAIR): the second row set's stream and the
-  // events of its interleave with the first
-  hipStream_t pstream = nullptr;
-  hipEvent_t pev_fork = nullptr, pev_a = nullptr, pev_b = nullptr, pev_join = nullptr;
   // encoder stream (MWX_STREAM_PRIO=enc_low / both): the encoder of a batch runs
   // on a low-priority stream, ordered after / before `stream` by two events,
   // so a concurrent batch's latency-bound decode chain is dispatched first
@@ -211,8 +209,10 @@ struct State {
   }
   // decoder workspace (row-batched)
   DBuf xd, hd, qd, od, ffd, logits, kself, vself, stepin, ctl, tokout, probs, logprobs, smask;
-  DBuf xd2;  // second residual buffer (LayerNorm-fused GEMMs: ping-pong)
   DBuf pqkv, pres, pq;  // split-K partial slabs of the decode GEMMs
+  // chained decode seams (k_chain.hip): hand-off counters of a step (zeroed
+  // by the step's embedding kernel) and the time-out flag
+  DBuf chain_ctr, chain_err;
   // batched prompt prefill: virtual-row inputs [tok|pos|act|xidx|crow] and the
   // layer stack's activations / slabs for up to MWX_PREFILL_ROWS virtual rows
   DBuf pf_in, pf_x, pf_h, pf_o, pf_ff, pf_pqkv, pf_pres, pf_pq;
@@ -1001,10 +1001,8 @@ struct Driver {
     S.pres.get((size_t)8 * R * d * 4);
     S.pq.get((size_t)8 * R * d * 4);
     S.xd.get((size_t)R * d * 4, true);
-    S.xd2.get((size_t)R * d * 4, true);
     // decode-GEMM A operands (fragment tiles), rows padded to the 64-row block
-    // (+ one 64-row block per decode group: each group's region is padded)
-    const size_t R64 = (size_t)(R + 63) / 64 * 64 + 64 * MWX_MAX_GROUPS;
+    const size_t R64 = (size_t)(R + 63) / 64 * 64;
     S.hd.get(R64 * d * sizeof(T), true);
     S.od.get(R64 * d * sizeof(T), true);
     S.ffd.get(R64 * 4 * d * sizeof(T), true);
@@ -1019,6 +1017,7 @@ struct Driver {
     HIPC(hipMemsetAsync(S.kvown.p, 0, (size_t)R * 4, st));
     S.ctl.get((size_t)R * sizeof(RowCtl));
     S.tokout.get((size_t)R * sizeof(TokOut));
+    chain_prepare();
   }
 
   // beam search: rows take over other rows' self-attention histories
@@ -1081,36 +1080,7 @@ struct Driver {
 
   // one decoder step for all R rows on the state's stream; inputs already in
   // S.stepin / S.ctl
-  void decode_step(int R, bool want_probs) { decode_group(R, 0, R, 0, want_probs, st); }
-
-  // Row groups of a step: with MWX_DECODE_GROUPS=G > 1 the rows are split into
-  // G groups that run as independent launch chains (one hipGraph each) on
-  // their own streams, so the latency-bound projections / LayerNorms of one
-  // group can overlap the HBM-bound cross-attention of another. Every kernel
-  // is row-blocked, so a row's arithmetic is the same in any group. Measured
-  // on MI355X (large-v3, 32 rows): G=2 is 8% slower than G=1 (the split
-  // doubles the weight stream and a stream beside a chain keeps only part of
-  // its rate), so the default is one group.
-  struct Group {
-    int r0, n;
-    size_t prow;  // first row of the group's region in the packed A buffers
-  };
-  std::vector<Group> groups_for(int R) const {
-    int G = 1;
-    if (const char* e = getenv("MWX_DECODE_GROUPS")) G = atoi(e);
-    G = std::max(1, std::min(G, MWX_MAX_GROUPS));
-    if (R < 16 * G) G = std::max(1, R / 16);
-    std::vector<Group> gs;
-    size_t prow = 0;
-    const int xg = std::max(1, xgroup);
-    for (int g = 0; g < G; ++g) {
-      const int r0 = (int)((long)R * g / G) / xg * xg;
-      const int r1 = g == G - 1 ? R : (int)((long)R * (g + 1) / G) / xg * xg;
-      gs.push_back(Group{r0, r1 - r0, prow});
-      prow += (size_t)(r1 - r0 + 63) / 64 * 64;
-    }
-    return gs;
-  }
+  void decode_step(int R, bool want_probs) { decode_rows(R, want_probs, st); }
 
   // The rows one pass of the decoder layer stack runs on: a decode step's
   // rows (one position each), or the virtual rows of a prompt prefill (one
@@ -1121,7 +1091,6 @@ struct Driver {
     // prefill: the self-cache row of each virtual row (nullptr: row = its own)
     const int* crow = nullptr;
     float* xd = nullptr;
-    float* xd2 = nullptr;  // the other residual buffer (LayerNorm-fused GEMMs)
     T *hd = nullptr, *od = nullptr, *ffd = nullptr;
     float *Pqkv = nullptr, *Pres = nullptr, *Pq = nullptr;
     _Float16 *kself = nullptr, *vself = nullptr;  // layer-0 self cache of row 0
@@ -1136,55 +1105,103 @@ struct Driver {
     bool prefill = false;
   };
 
-  // MWX_LN_FUSE=1 folds the decode LayerNorms of <= LNF_MAX_ROWS rows (one
-  // request, streaming) into the consumer GEMMs (kernels.h LnFuse): three
-  // launches per layer fewer, the same bits. Off by default: every workgroup
-  // of the consumer repeats the row statistics before its first MFMA, and on
-  // C2 that serial prologue costs more than the launches it saves (87.7 vs
-  // 73.0 ms per request).
-  static bool ln_fuse_on() {
-    static const bool on = getenv("MWX_LN_FUSE") && atoi(getenv("MWX_LN_FUSE")) != 0;
-    return on;
-  }
-
   // One pass of the decoder layer stack over a set of rows, in parts: the
   // embedding, and per layer the chain up to the cross-attention's query
   // projection (pre), the cross-attention (cross) and the chain after it
-  // (post). run_layers runs them in order on one stream; decode_group_pair
-  // interleaves the parts of two row sets on two streams.
+  // (post); run_layers runs them in order on one stream.
   struct LayerRun {
     float* xd = nullptr;    // the residual stream's buffer
-    float* xalt = nullptr;  // the other buffer (LayerNorm-fused sites)
-    bool fuse = false;
+    bool chain = false;
+    int chain_prev = -1;    // counter slot of the previous seam launch     // GEMM -> LayerNorm -> GEMM seams as one launch each
     int k1 = 0, k2 = 0, k3 = 0, k4 = 0;
     bool k5 = false;
     int ks_prev = 0;  // the last FFN2's split-K factor and bias (folded into
     const float* bias_prev = nullptr;  // the next consumer)
   };
-  // the LayerNorm of a fused site: the consumer reads xd (+ the producer's
-  // slabs) and its workgroup 0 writes the completed rows to the other buffer
-  LnFuse lnf(LayerRun& c, const LayerRows& rw, const float* w, const float* b, const float* P,
-             int KS, const float* pb) {
-    LnFuse L;
-    L.x = c.xd;
-    L.w = w;
-    L.b = b;
-    L.P = P;
-    L.KS = KS;
-    L.pbias = pb;
-    L.active = rw.act;
-    if (P) {
-      L.xout = c.xalt;
-      std::swap(c.xd, c.xalt);
+  // Chained seams (MWX_CHAIN=1; off by default until measured faster): out-proj -> LN2 -> cross-Q,
+  // cross-out -> LN3 -> FFN1 and FFN2 -> LN1 -> QKV each run as one launch
+  // (k_chain.hip; the same arithmetic as the separate launches), so a decode
+  // layer is 5 launches instead of 11. Decode steps of <= 64 rows with 16-bit
+  // weights; the prompt prefill, beam-sized steps and MX-fp8 weights keep the
+  // separate launches (bit-identical results).
+  static bool chain_on() {
+    int v = chain_mode().load();
+    if (v < 0) {
+      v = (getenv("MWX_CHAIN") && atoi(getenv("MWX_CHAIN")) != 0) ? 1 : 0;
+      chain_mode().store(v);
     }
-    return L;
+    return v != 0;
+  }
+  // counter slots: seam (l, site) at 3 l + site, layer 0's LN1 + QKV at 3 L
+  int chain_slots() const { return 3 * L_dec + 1; }
+  unsigned* chain_ctr(int slot) {
+    return (unsigned*)S.chain_ctr.p + (size_t)slot * chain_slot_words();
+  }
+  // (outside any capture: before a decode loop) the counter slots, zeroed
+  void chain_prepare() {
+    S.chain_ctr.get((size_t)chain_slots() * chain_slot_words() * 4);
+    S.chain_err.get(4, true);
+    HIPC(hipMemsetAsync(S.chain_ctr.p, 0, (size_t)chain_slots() * chain_slot_words() * 4, st));
   }
   void layers_begin(const LayerRows& rw, LayerRun& c, hipStream_t s) {
-    embed<T>(Wt(C.tok_emb), C.dec_pe, rw.tok, rw.pos, rw.act, rw.xd, rw.n, d, s);
     c = LayerRun{};
     c.xd = rw.xd;
-    c.xalt = rw.xd2;
-    c.fuse = !rw.prefill && rw.xd2 && rw.n <= LNF_MAX_ROWS && d <= 2048 && ln_fuse_on();
+    c.chain = !rw.prefill && rw.n <= 64 && !C.dec8 && d % 128 == 0 && d <= 2048 &&
+              chain_on() && S.chain_ctr.p != nullptr;
+    // a step's seams run in the order 3L, 0, 1, 2, 3, ..., 3(L-1) + 1: each
+    // launch zeroes its predecessor's slot (the first, the step's last)
+    c.chain_prev = 3 * (L_dec - 1) + 1;
+    embed<T>(Wt(C.tok_emb), C.dec_pe, rw.tok, rw.pos, rw.act, rw.xd, rw.n, d, s);
+  }
+  // a chained seam's hand-off wait timed out since the last check (results
+  // of that step are wrong): 0, or -12 (after an error message)
+  int chain_check() {
+    if (!S.chain_err.p) return 0;
+    unsigned e = 0;
+    HIPC(hipMemcpyAsync(&e, S.chain_err.p, 4, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    if (!e) return 0;
+    HIPC(hipMemsetAsync(S.chain_err.p, 0, 4, st));
+    MWX_LOG_ERROR("mwx: a chained decode seam timed out waiting for its producer\n");
+    return -12;
+  }
+  // one chained seam: [producer pA x pW (K = pK) -> slabs Pres] -> LayerNorm
+  // (lw, lb; producer bias pb) of the residual into hd -> consumer cW:
+  // split-K slabs cP (returns their KS) or the FFN1 GELU GEMM (cP == nullptr)
+  int chain_seam(const LayerRows& rw, LayerRun& c, int slot, const T* pA, const DecWeight* pW,
+                 int pK, const float* pb, const float* lw, const float* lb, const DecWeight& cW,
+                 int cN, float* cP, const float* cbias, hipStream_t s) {
+    ChainArgs a;
+    a.M = rw.n;
+    a.d = d;
+    a.p_A = pA;
+    a.p_W = pW ? pW->w : nullptr;
+    a.p_K = pK;
+    a.ln.x = c.xd;
+    a.ln.w = lw;
+    a.ln.b = lb;
+    a.ln.P = rw.Pres;
+    a.ln.pbias = pb;
+    a.ln.y = rw.hd;
+    a.ln.active = rw.act;
+    a.c_W = cW.w;
+    a.c_N = cN;
+    a.c_skinny = cP == nullptr;
+    a.c_P = cP;
+    if (!cP) {
+      a.c_epi.bias = cbias;
+      a.c_epi.c16 = rw.ffd;
+      a.c_epi.ldc = 4 * d;
+      a.c_epi.pack_out = true;
+    }
+    a.ctr = chain_ctr(slot);
+    a.zero = c.chain_prev >= 0 ? chain_ctr(c.chain_prev) : nullptr;
+    a.nzero = chain_slot_words();
+    c.chain_prev = slot;
+    a.err = (unsigned*)S.chain_err.p;
+    PerfScope ps(S, "dec_gemm", s);
+    if (!chain_launch<T>(a, s)) throw std::runtime_error("mwx: unsupported chained seam");
+    return cP ? splitk_factor(d) : 1;
   }
   // The d- and 3d-wide projections run as split-K GEMMs writing f32 partial
   // slabs; each consumer (LN: bias + residual, attention: bias/scale/f16 and
@@ -1197,11 +1214,11 @@ struct Driver {
     _Float16* ks = rw.kself + l * layer_self;
     _Float16* vs = rw.vself + l * layer_self;
     T* hd = rw.hd;
-    if (c.fuse) {
-      const LnFuse L = lnf(c, rw, W.ln1_w, W.ln1_b, c.ks_prev ? rw.Pres : nullptr, c.ks_prev,
-                           c.bias_prev);
-      PerfScope ps(S, "dec_gemm", s);
-      c.k1 = gemm_splitk_partials<T>(hd, Dw(W.qkv), n, 3 * d, d, rw.Pqkv, s, &L);
+    if (c.chain) {
+      // (layers > 0: LN1 + QKV ran in the previous layer's FFN2 seam)
+      if (l == 0)
+        c.k1 = chain_seam(rw, c, 3 * L_dec, nullptr, nullptr, 0, nullptr, W.ln1_w, W.ln1_b, W.qkv,
+                          3 * d, rw.Pqkv, nullptr, s);
     } else {
       layer_norm_dec<T>(c.xd, W.ln1_w, W.ln1_b, hd, n, d, rw.act, s, c.ks_prev ? rw.Pres : nullptr,
                         c.ks_prev, c.bias_prev);
@@ -1217,17 +1234,17 @@ struct Driver {
       dec_attention<T>(rw.Pqkv, c.k1, 3 * d, W.qkv_b, kqs, kqs, ks, vs, rw.crow, rw.pos, rw.act, 0,
                        Tctx, rw.od, n, H, 1.0f, s, rw.kvmap, rw.kvown, rw.map_row0,
                        rw.prefill ? 1 : rw.xgroup, pf_selfwrite || !rw.prefill); }
+    if (c.chain) {
+      c.k2 = splitk_factor(d);
+      c.k3 = chain_seam(rw, c, 3 * l, rw.od, &W.o, d, W.o_b, W.lnc_w, W.lnc_b, W.cq, d, rw.Pq,
+                        nullptr, s);
+      return;
+    }
     { PerfScope ps(S, "dec_gemm", s);
       c.k2 = gemm_splitk_partials<T>(rw.od, Dw(W.o), n, d, d, rw.Pres, s); }
-    if (c.fuse) {
-      const LnFuse L = lnf(c, rw, W.lnc_w, W.lnc_b, rw.Pres, c.k2, W.o_b);
-      PerfScope ps(S, "dec_gemm", s);
-      c.k3 = gemm_splitk_partials<T>(hd, Dw(W.cq), n, d, d, rw.Pq, s, &L);
-    } else {
-      layer_norm_dec<T>(c.xd, W.lnc_w, W.lnc_b, hd, n, d, rw.act, s, rw.Pres, c.k2, W.o_b);
-      PerfScope ps(S, "dec_gemm", s);
-      c.k3 = gemm_splitk_partials<T>(hd, Dw(W.cq), n, d, d, rw.Pq, s);
-    }
+    layer_norm_dec<T>(c.xd, W.lnc_w, W.lnc_b, hd, n, d, rw.act, s, rw.Pres, c.k2, W.o_b);
+    PerfScope ps(S, "dec_gemm", s);
+    c.k3 = gemm_splitk_partials<T>(hd, Dw(W.cq), n, d, d, rw.Pq, s);
   }
   void layer_cross(const LayerRows& rw, LayerRun& c, int l, hipStream_t s) {
     const int n = rw.n;
@@ -1272,6 +1289,24 @@ struct Driver {
   void layer_post(const LayerRows& rw, LayerRun& c, int l, hipStream_t s) {
     const int n = rw.n;
     const DecLayerW& W = C.dec[l];
+    if (c.chain) {
+      c.k4 = splitk_factor(d);
+      c.k5 = chain_seam(rw, c, 3 * l + 1, rw.od, &W.co, d, W.co_b, W.ln2_w, W.ln2_b, W.fc1, 4 * d,
+                        nullptr, W.fc1_b, s) > 0;
+      if (l + 1 < L_dec) {
+        const DecLayerW& Wn = C.dec[l + 1];
+        c.k1 = chain_seam(rw, c, 3 * l + 2, rw.ffd, &W.fc2, 4 * d, W.fc2_b, Wn.ln1_w, Wn.ln1_b,
+                          Wn.qkv, 3 * d, rw.Pqkv, nullptr, s);
+        c.ks_prev = splitk_factor(4 * d);
+      } else {
+        PerfScope ps(S, "dec_gemm", s);
+        c.ks_prev = gemm_splitk_partials<T>(rw.ffd, Dw(W.fc2), n, d, 4 * d, rw.Pres, s);
+      }
+      c.bias_prev = W.fc2_b;
+      if (!c.k1 || !c.k3 || !c.k4 || !c.k5 || !c.ks_prev)
+        throw std::runtime_error("mwx: unsupported split-K shape");
+      return;
+    }
     { PerfScope ps(S, "dec_gemm", s);
       c.k4 = gemm_splitk_partials<T>(rw.od, Dw(W.co), n, d, d, rw.Pres, s); }
     EpiParams e;
@@ -1279,15 +1314,10 @@ struct Driver {
     e.c16 = rw.ffd;
     e.ldc = 4 * d;
     e.pack_out = true;
-    if (c.fuse) {
-      const LnFuse L = lnf(c, rw, W.ln2_w, W.ln2_b, rw.Pres, c.k4, W.co_b);
-      PerfScope ps(S, "dec_gemm", s);
-      c.k5 = gemm_decode<T>(EPI_GELU, rw.hd, Dw(W.fc1), n, 4 * d, d, e, s, &L);
-    } else {
-      layer_norm_dec<T>(c.xd, W.ln2_w, W.ln2_b, rw.hd, n, d, rw.act, s, rw.Pres, c.k4, W.co_b);
-      PerfScope ps(S, "dec_gemm", s);
-      c.k5 = gemm_decode<T>(EPI_GELU, rw.hd, Dw(W.fc1), n, 4 * d, d, e, s);
-    }
+    e.nw = 4;  // (4 waves split K: the chained seam's FFN1 arithmetic)
+    layer_norm_dec<T>(c.xd, W.ln2_w, W.ln2_b, rw.hd, n, d, rw.act, s, rw.Pres, c.k4, W.co_b);
+    { PerfScope ps(S, "dec_gemm", s);
+      c.k5 = gemm_decode<T>(EPI_GELU, rw.hd, Dw(W.fc1), n, 4 * d, d, e, s); }
     { PerfScope ps(S, "dec_gemm", s);
       c.ks_prev = gemm_splitk_partials<T>(rw.ffd, Dw(W.fc2), n, d, 4 * d, rw.Pres, s); }
     c.bias_prev = W.fc2_b;
@@ -1298,8 +1328,7 @@ struct Driver {
   // embedding + all decoder layers; returns the last FFN2's split-K factor
   // and bias (folded into the consumer: the final LayerNorm) and the buffer
   // holding the residual stream
-  void run_layers(const LayerRows& rw, hipStream_t s, int& ks_prev, const float*& bias_prev,
-                  float** x_final = nullptr) {
+  void run_layers(const LayerRows& rw, hipStream_t s, int& ks_prev, const float*& bias_prev) {
     LayerRun c;
     layers_begin(rw, c, s);
     for (int l = 0; l < L_dec; ++l) {
@@ -1309,7 +1338,6 @@ struct Driver {
     }
     ks_prev = c.ks_prev;
     bias_prev = c.bias_prev;
-    if (x_final) *x_final = c.fuse ? c.xd : nullptr;
   }
 
   // Batched prompt prefill (whisper.cpp decodes a window's prompt in one
@@ -1431,118 +1459,50 @@ struct Driver {
     }
   }
 
-  // decoder step for rows [r0, r0+n) of an R-row step, launched on `s`
-  // the decode-step rows [r0, r0 + n) of R (packed A operands from row prow)
-  LayerRows step_rows(int R, int r0, int n, size_t prow) {
+  // the decode-step rows (all R) and their buffers
+  LayerRows step_rows(int R) {
     int* si = (int*)S.stepin.p;
     LayerRows rw;
-    rw.n = n;
-    rw.tok = si + r0;
-    rw.pos = si + R + r0;
-    rw.act = si + 2 * R + r0;
-    rw.xidx = si + 3 * R + r0;
-    rw.xd = (float*)S.xd.p + (size_t)r0 * d;
-    rw.xd2 = (float*)S.xd2.p + (size_t)r0 * d;
-    rw.hd = (T*)S.hd.p + prow * d;
-    rw.od = (T*)S.od.p + prow * d;
-    rw.ffd = (T*)S.ffd.p + prow * 4 * d;
-    // the group's split-K slabs [KS][n][N] live inside the R-row slab buffers
-    rw.Pqkv = (float*)S.pqkv.p + (size_t)8 * r0 * 3 * d;
-    rw.Pres = (float*)S.pres.p + (size_t)8 * r0 * d;
-    rw.Pq = (float*)S.pq.p + (size_t)8 * r0 * d;
-    rw.kself = (_Float16*)S.kself.p + (size_t)r0 * H * Tctx * 64;
-    rw.vself = (_Float16*)S.vself.p + (size_t)r0 * H * Tctx * 64;
-    rw.kvmap = (const int*)S.kvmap.p + (size_t)r0 * Tctx;
-    rw.kvown = (const int*)S.kvown.p + r0;
-    rw.map_row0 = r0;
+    rw.n = R;
+    rw.tok = si;
+    rw.pos = si + R;
+    rw.act = si + 2 * R;
+    rw.xidx = si + 3 * R;
+    rw.xd = (float*)S.xd.p;
+    rw.hd = (T*)S.hd.p;
+    rw.od = (T*)S.od.p;
+    rw.ffd = (T*)S.ffd.p;
+    rw.Pqkv = (float*)S.pqkv.p;
+    rw.Pres = (float*)S.pres.p;
+    rw.Pq = (float*)S.pq.p;
+    rw.kself = (_Float16*)S.kself.p;
+    rw.vself = (_Float16*)S.vself.p;
+    rw.kvmap = (const int*)S.kvmap.p;
+    rw.kvown = (const int*)S.kvown.p;
+    rw.map_row0 = 0;
     rw.xgroup = xgroup;
     return rw;
   }
 
-  // Two row sets decoded as one step graph on two streams, their layers
-  // interleaved: the cross-attention of set B at layer l starts after set A's
-  // (layer l) has ended and set A's at layer l + 1 after set B's at layer l,
-  // so the two HBM-bound cross K/V streams never run at the same time and
-  // each runs beside the other set's latency-bound projection / LayerNorm
-  // chain (two independent chains on two streams have no such phase: their
-  // cross-attentions collide about as often as their chains do). Each set's
-  // kernels and arithmetic are those of a decode step of that set alone.
-  // MWX_DECODE_PAIR=1 enables it for steps of >= 2 x MWX_PAIR_MIN rows
-  // (default 16); the sets split at a clip boundary.
-  static bool pair_on() {
-    static const bool on = getenv("MWX_DECODE_PAIR") && atoi(getenv("MWX_DECODE_PAIR")) != 0;
-    return on;
-  }
-  bool pair_rows(int n) const {
-    static const int pmin = getenv("MWX_PAIR_MIN") ? std::max(1, atoi(getenv("MWX_PAIR_MIN"))) : 16;
-    return pair_on() && n >= 2 * pmin * std::max(1, xgroup);
-  }
-  // (outside any capture) the second stream and the interleave's events
-  void pair_prepare() {
-    if (!S.pstream) HIPC(hipStreamCreateWithFlags(&S.pstream, hipStreamNonBlocking));
-    for (auto* e : {&S.pev_fork, &S.pev_a, &S.pev_b, &S.pev_join})
-      if (!*e) HIPC(hipEventCreateWithFlags(e, hipEventDisableTiming));
-  }
-  void decode_group_pair(int R, int r0, int n, size_t prow, bool want_probs, hipStream_t s) {
-    const int xg = std::max(1, xgroup);
-    const int na = (n / 2) / xg * xg, nb = n - na;
-    const LayerRows ra = step_rows(R, r0, na, prow);
-    const LayerRows rb = step_rows(R, r0 + na, nb, prow + (size_t)(na + 63) / 64 * 64);
-    hipStream_t s2 = S.pstream;
-    HIPC(hipEventRecord(S.pev_fork, s));
-    HIPC(hipStreamWaitEvent(s2, S.pev_fork, 0));
-    LayerRun ca, cb;
-    layers_begin(ra, ca, s);
-    layers_begin(rb, cb, s2);
-    for (int l = 0; l < L_dec; ++l) {
-      layer_pre(ra, ca, l, s);
-      if (l > 0) HIPC(hipStreamWaitEvent(s, S.pev_b, 0));
-      layer_cross(ra, ca, l, s);
-      HIPC(hipEventRecord(S.pev_a, s));
-      layer_post(ra, ca, l, s);
-      layer_pre(rb, cb, l, s2);
-      HIPC(hipStreamWaitEvent(s2, S.pev_a, 0));
-      layer_cross(rb, cb, l, s2);
-      HIPC(hipEventRecord(S.pev_b, s2));
-      layer_post(rb, cb, l, s2);
-    }
-    step_tail(R, ra, ca.ks_prev, ca.bias_prev, ca.fuse ? ca.xd : nullptr, want_probs, s);
-    step_tail(R, rb, cb.ks_prev, cb.bias_prev, cb.fuse ? cb.xd : nullptr, want_probs, s2);
-    HIPC(hipEventRecord(S.pev_join, s2));
-    HIPC(hipStreamWaitEvent(s, S.pev_join, 0));
-  }
-
-  void decode_group(int R, int r0, int n, size_t prow, bool want_probs, hipStream_t s) {
-    if (pair_rows(n)) return decode_group_pair(R, r0, n, prow, want_probs, s);
-    const LayerRows rw = step_rows(R, r0, n, prow);
+  // one decode step of all R rows on stream s
+  void decode_rows(int R, bool want_probs, hipStream_t s) {
+    const LayerRows rw = step_rows(R);
     int ks_prev = 0;
     const float* bias_prev = nullptr;
-    float* xfin = nullptr;  // (LayerNorm-fused layers: the residual's buffer)
-    run_layers(rw, s, ks_prev, bias_prev, &xfin);
-    step_tail(R, rw, ks_prev, bias_prev, xfin, want_probs, s);
+    run_layers(rw, s, ks_prev, bias_prev);
+    step_tail(R, rw, ks_prev, bias_prev, want_probs, s);
   }
 
   // final LayerNorm, logits and logits processing of a step's row set
-  void step_tail(int R, const LayerRows& rw, int ks_prev, const float* bias_prev, float* xfin,
-                 bool want_probs, hipStream_t s) {
+  void step_tail(int R, const LayerRows& rw, int ks_prev, const float* bias_prev, bool want_probs,
+                 hipStream_t s) {
     const int n = rw.n;
     const int r0 = rw.map_row0;
     const int* act = rw.act;
     float* xd = rw.xd;
     T* hd = rw.hd;
     float* Pres = rw.Pres;
-    LnFuse Lfin;
-    if (xfin) {
-      Lfin.x = xfin;
-      Lfin.w = C.dec_ln_w;
-      Lfin.b = C.dec_ln_b;
-      Lfin.P = Pres;
-      Lfin.KS = ks_prev;
-      Lfin.pbias = bias_prev;
-      Lfin.active = act;  // (xout: the completed residual is not read again)
-    } else {
-      layer_norm_dec<T>(xd, C.dec_ln_w, C.dec_ln_b, hd, n, d, act, s, Pres, ks_prev, bias_prev);
-    }
+    layer_norm_dec<T>(xd, C.dec_ln_w, C.dec_ln_b, hd, n, d, act, s, Pres, ks_prev, bias_prev);
     EpiParams e;
     e.c32 = (float*)S.logits.p + (size_t)r0 * V;
     e.ldc = V;
@@ -1553,7 +1513,7 @@ struct Driver {
     // launch at 32 rows, scripts/probe/dec_chain_probe.hip).
     e.mt = n <= 64 ? std::max(1, (n + 15) / 16) : 2;
     { PerfScope ps(S, "logits_gemm", s);
-    if (!gemm_decode<T>(EPI_F32, hd, Dw(C.tok_p), n, V, d, e, s, xfin ? &Lfin : nullptr))
+    if (!gemm_decode<T>(EPI_F32, hd, Dw(C.tok_p), n, V, d, e, s))
       throw std::runtime_error("mwx: unsupported logits GEMM shape"); }
     float* pr = nullptr;
     float* lp = nullptr;

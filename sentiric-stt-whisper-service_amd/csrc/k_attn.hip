@@ -19,6 +19,8 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include <atomic>
+
 #include "kcommon.h"
 #include "kernels.h"
 
@@ -278,28 +280,7 @@ __device__ __forceinline__ float dpp_sum8(float d) {
 // written to the cache and taken from LDS (its cache line may be stale in L1).
 // The loop body is straight-line (two batches per trip, no early exit), so the
 // compiler keeps exactly one batch in flight with counted vmcnt waits.
-// Cross-attention scores of one 16-key tile on MFMA for f16 caches (MFC; the
-// single-row and the grouped kernel both call this, so a row's scores do not
-// depend on the kernel or the group size): the tile is the A operand (lane l:
-// key l&15, e = 32h + 8(l>>4) .. +7 for the two halves h), the queries the B
-// operand (lane l: query l&15, the same e; rows >= the query count zero);
-// lane l receives query l&15's dot products with keys 4(l>>4) .. +3.
-__device__ __forceinline__ f32x4 xscore16(f16x8 k0, f16x8 k1, f16x8 q0, f16x8 q1) {
-  const f32x4 z = {0.0f, 0.0f, 0.0f, 0.0f};
-  const f32x4 a = __builtin_amdgcn_mfma_f32_16x16x32_f16(k0, q0, z, 0, 0, 0);
-  return __builtin_amdgcn_mfma_f32_16x16x32_f16(k1, q1, a, 0, 0, 0);
-}
-
-// PF > 0 (cross, small grids: one request): the grid carries PF helper
-// workgroups per (row, head) on the same XCD as the one that attends
-// (blockIdx.y >= R; H % 8 == 0, so linear id % 8 -- the XCD under the
-// round-robin placement -- equals the attending workgroup's). Helper p loads
-// its share of the (row, head)'s K rows then V rows with the default cache
-// policy and discards them: the rows land in that XCD's L2 while the attending
-// workgroup streams the batches before them, so its later batches are L2 hits.
-// The attending workgroup's arithmetic is unchanged (bit-identical).
-template <typename T, bool SELF, int UBX = 8, bool NTL = !SELF, int NBC = 0, int PF = 0,
-          bool MFC = false>
+template <typename T, bool SELF, int UBX = 8, bool NTL = !SELF, int NBC = 0>
 __global__ __launch_bounds__(256) void dec_attn_kernel(
     const float* __restrict__ P, int KS, int pcols, const float* __restrict__ bias, float qscale,
     float kscale, _Float16* __restrict__ kbase, _Float16* __restrict__ vbase,
@@ -314,35 +295,6 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
   __shared__ float sq[64], snk[64], snv[64];
   span_start(span);
   int row = blockIdx.y, h = blockIdx.x;
-  if constexpr (PF > 0) {
-    if (row >= R) {
-      const int r = (row - R) % R, p = (row - R) / R;
-      const int hslot = kv_index ? kv_index[r] : r;
-      if (active[r]) {
-        const _Float16* K = kbase + (((long)hslot * H + h) * cap) * 64;
-        const _Float16* V = vbase + (((long)hslot * H + h) * cap) * 64;
-        // 16-B chunks of the K rows then the V rows; helper p takes chunks
-        // [p*per, (p+1)*per): the later ones (the attending workgroup reads
-        // K first, its own first batches itself)
-        const long chunks = (long)fixed_len * 8;  // per matrix
-        const long per = (2 * chunks + PF - 1) / PF;
-        const long c0 = min((long)p * per, 2 * chunks), c1 = min(c0 + per, 2 * chunks);
-        for (long c = c0 + threadIdx.x; c < c1; c += 256 * 4) {
-          f16x8 x[4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const long ci = min(c + 256 * i, c1 - 1);
-            const _Float16* src = ci < chunks ? K + ci * 8 : V + (ci - chunks) * 8;
-            x[i] = *reinterpret_cast<const f16x8*>(src);
-          }
-#pragma unroll
-          for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(x[i]));
-        }
-      }
-      span_end(span);
-      return;
-    }
-  }
   if (nq > 1) {
     // nq rows per clip (beam / best-of decoders: cross, the same K/V; self,
     // histories taken over from each other): 1-D grid where the nq
@@ -441,30 +393,10 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
     // would make the query wait for all of them)
     if (part != 1) bcol = bias[col];
   }
-  // MFC (cross, NBC): scores on MFMA (xscore16); wave w streams the 16-key
-  // tiles w, w + 4, ... four at a time, two groups in flight
-  constexpr int TDC = 4;
-  const int ntc = (n + 15) >> 4, ngc = ((ntc + 3) / 4 + TDC - 1) / TDC;
-  const int mln = lane & 15, gq = lane >> 4;
-  f16x8 kt[MFC ? 2 : 1][MFC ? TDC : 1][2];
-  auto mfc_load = [&](int buf, int grp) {
-#pragma unroll
-    for (int i = 0; i < TDC; ++i) {
-      const int t = min(wid + 4 * (TDC * grp + i), ntc - 1);
-      const _Float16* r = K + (long)min(t * 16 + mln, jmax) * 64 + 8 * gq;
-      kt[buf][i][0] = ld_stream<NTL>(reinterpret_cast<const f16x8*>(r));
-      kt[buf][i][1] = ld_stream<NTL>(reinterpret_cast<const f16x8*>(r + 32));
-    }
-  };
-  if constexpr (MFC) {
-    mfc_load(0, 0);
-    if (ngc > 1) mfc_load(1, 1);
-  } else {
-    LOADROWS0(ka, K)
-    // NBC: the second key batch is requested before the query is formed too,
-    // so two batches are in flight from the start
-    if constexpr (NBC > 0) LOADROWS(kb2, K, 1)
-  }
+  LOADROWS0(ka, K)
+  // NBC: the second key batch is requested before the query is formed too,
+  // so two batches are in flight from the start
+  if constexpr (NBC > 0) LOADROWS(kb2, K, 1)
   if (red) {
     float acc = pk[0];
 #pragma unroll
@@ -565,45 +497,6 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
       if (b > 0) LOADROWS(ka, V, b)
       pv_batch(ka, b);
     }
-  } else if constexpr (NBC > 0 && MFC) {
-    f16x8 qb0, qb1;  // B operand: the query in column 0, zero elsewhere
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      qb0[j] = mln == 0 ? (_Float16)sq[8 * gq + j] : (_Float16)0.0f;
-      qb1[j] = mln == 0 ? (_Float16)sq[32 + 8 * gq + j] : (_Float16)0.0f;
-    }
-    auto tile = [&](int buf, int i, int t) {
-      const f32x4 d = xscore16(kt[buf][i][0], kt[buf][i][1], qb0, qb1);
-      if (mln == 0 && t < ntc) {
-        f32x4 out;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) out[r] = d[r] * scale;
-        *reinterpret_cast<f32x4*>(&sc[t * 16 + 4 * gq]) = out;
-      }
-    };
-#pragma unroll 1
-    for (int grp = 0; grp < ngc; grp += 2) {
-#pragma unroll
-      for (int i = 0; i < TDC; ++i) tile(0, i, wid + 4 * (TDC * grp + i));
-      if (grp + 2 < ngc) mfc_load(0, grp + 2);
-      if (grp + 1 < ngc) {
-#pragma unroll
-        for (int i = 0; i < TDC; ++i) tile(1, i, wid + 4 * (TDC * (grp + 1) + i));
-        if (grp + 3 < ngc) mfc_load(1, grp + 3);
-      }
-    }
-    LOADROWS(ka, V, 0)
-    LOADROWS(kb2, V, 1)
-    softmax();
-#pragma unroll 1
-    for (int b = 0; b < NBC - 2; b += 2) {
-      pv_batch(ka, b);
-      LOADROWS(ka, V, b + 2)
-      pv_batch(kb2, b + 1);
-      LOADROWS(kb2, V, b + 3)
-    }
-    pv_batch(ka, NBC - 2);
-    pv_batch(kb2, NBC - 1);
   } else if constexpr (NBC > 0) {
     // cross with a compile-time even batch count (n = 1500: 6): the K batches
     // and then the V batches form one load stream through the two register
@@ -794,17 +687,11 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
   const int mrow = lane & 15, gq = lane >> 4;
   uint2 kr[MFS && KV8 ? 2 : 1][MFS && KV8 ? TD : 1][2];
   uint32_t ksr[MFS && KV8 ? 2 : 1][MFS && KV8 ? TD : 1][2];
-  f16x8 kf[MFS && !KV8 ? 2 : 1][MFS && !KV8 ? TD : 1][2];  // (f16 cache: xscore16 tiles)
+  static_assert(!MFS || KV8, "MFMA scores: MX-fp8 caches only");
   auto mfs_load = [&](int buf, int grp) {  // tiles wid + 4 * (TD * grp + i)
 #pragma unroll
     for (int i = 0; i < TD; ++i) {
       const int t = min(wid + 4 * (TD * grp + i), ntile - 1);
-      if constexpr (!KV8) {
-        const _Float16* r = K + (long)min(t * 16 + mrow, jmax) * 64 + 8 * gq;
-        kf[buf][i][0] = ld_stream<NTL>(reinterpret_cast<const f16x8*>(r));
-        kf[buf][i][1] = ld_stream<NTL>(reinterpret_cast<const f16x8*>(r + 32));
-        continue;
-      }
       const uint8_t* row = K8 + (long)min(t * 16 + mrow, jmax) * 64 + 8 * gq;
       const u32x2 a = ld_stream<NTL>(reinterpret_cast<const u32x2*>(row));
       const u32x2 b = ld_stream<NTL>(reinterpret_cast<const u32x2*>(row + 32));
@@ -907,7 +794,11 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
     vr1 = ld_stream<NTL>(src + 1);
     const int k0 = t * 32 + 8 * gq;  // scales of the lane's 8 A-operand keys
     if (k0 + 7 <= jmax) {
-      vsr = *reinterpret_cast<const u32x4*>(VS8 + (long)k0 * 2);
+      // (two 8-B reads: a (slot, head)'s scale rows start 3000 B apart, so a
+      // 16-B read here is only 8-B aligned)
+      const u32x2 lo = *reinterpret_cast<const u32x2*>(VS8 + (long)k0 * 2);
+      const u32x2 hi = *reinterpret_cast<const u32x2*>(VS8 + (long)k0 * 2 + 8);
+      vsr = u32x4{lo[0], lo[1], hi[0], hi[1]};
     } else {
       uint32_t w[4];
 #pragma unroll
@@ -938,10 +829,6 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
           const uint32_t sp = (ksr[buf][i][r >> 1] >> (16 * (r & 1))) & 0xffffu;
           out[r] = (e8m0(sp & 0xffu) * d0[r] + e8m0(sp >> 8) * d1[r]) * scale;
         }
-      } else {  // (f16: dec_attn_kernel MFC's arithmetic)
-        const f32x4 d = xscore16(kf[buf][i][0], kf[buf][i][1], qb0, qb1);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) out[r] = d[r] * scale;
       }
       if (mrow < NQ && t < ntile)
         *reinterpret_cast<f32x4*>(&sc[min(mrow, NQ - 1)][t * 16 + 4 * gq]) = out;
@@ -957,11 +844,7 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
         for (int i = 0; i < TD; ++i) score_tile(1, i, wid + 4 * (TD * (grp + 1) + i));
       }
     }
-    if constexpr (KV8) {
-      if (wid < nt32) v_load(wid);  // (in flight across the softmax)
-    } else {
-      LOADROWS16(ka, V, 0, 0)
-    }
+    if (wid < nt32) v_load(wid);  // (in flight across the softmax)
   } else if constexpr (NBC > 0) {
 #pragma unroll 1
     for (int b = 0; b < NBC - 1; ++b) k_trip(b, false);
@@ -1028,17 +911,38 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
       }
       const u32x4 sv = vsr;
       if (t + 4 < nt32) v_load(t + 4);
-      // A operands: P'[q][key] = P x V scale of (key, half), keys t*32 + 8(l>>4) + j
+      // A operands: P'[q][key] = P x 2^(s(key, half) - smax(half)), keys
+      // t*32 + 8(l>>4) + j, with smax the largest V scale exponent of the
+      // tile's 32 keys in that half; the tile's product is scaled by
+      // 2^smax in f32 below. (Folding the whole scale into P, as before,
+      // pushed typical weights p ~ 1/1500 x 2^-8 into f16 subnormals.)
       const int kb = t * 32 + 8 * gq;
+      int smax0 = 0, smax1 = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t sp = (sv[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+        if (kb + j < n) {
+          smax0 = max(smax0, (int)(sp & 0xffu));
+          smax1 = max(smax1, (int)(sp >> 8));
+        }
+      }
+      smax0 = max(smax0, __shfl_xor(smax0, 16, 64));
+      smax0 = max(smax0, __shfl_xor(smax0, 32, 64));
+      smax1 = max(smax1, __shfl_xor(smax1, 16, 64));
+      smax1 = max(smax1, __shfl_xor(smax1, 32, 64));
+      auto pow2 = [](int d) {  // 2^d for d <= 0 (0 below 2^-126)
+        return d < -126 ? 0.0f : __uint_as_float((uint32_t)(127 + d) << 23);
+      };
       f16x8 pa[2];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float p = sc[qrow][min(kb + j, n - 1)];
         if (mrow >= NQ || kb + j >= n) p = 0.0f;
         const uint32_t sp = (sv[j >> 1] >> (16 * (j & 1))) & 0xffffu;
-        pa[0][j] = (_Float16)(p * e8m0(sp & 0xffu));
-        pa[1][j] = (_Float16)(p * e8m0(sp >> 8));
+        pa[0][j] = (_Float16)(p * pow2((int)(sp & 0xffu) - smax0));
+        pa[1][j] = (_Float16)(p * pow2((int)(sp >> 8) - smax1));
       }
+      const float tscale[2] = {e8m0((uint32_t)smax0), e8m0((uint32_t)smax1)};
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
         const int e = 16 * nt + mrow;
@@ -1050,7 +954,10 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
           if (j < 4) w0 |= b << (8 * j); else w1 |= b << (8 * (j - 4));
         }
         const f16x8 vb = dequant_h8(uint2{w0, w1}, 127u);
-        oacc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa[nt >> 1], vb, oacc[nt], 0, 0, 0);
+        const f32x4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+        const f32x4 tp = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa[nt >> 1], vb, z, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) oacc[nt][r] += tp[r] * tscale[nt >> 1];
       }
     }
     // the four waves' partial sums: (w0 + w1) + (w2 + w3)
@@ -1363,12 +1270,19 @@ __global__ __launch_bounds__(256) void dec_xattn8_kernel(
   }
 }
 
-// f16 cross K/V caches: scores on MFMA in the single-row and the grouped
-// kernels together (xscore16; MWX_XATTN_MFC=1, A/B)
-static bool xattn_mfc() {
-  static const bool on = getenv("MWX_XATTN_MFC") && atoi(getenv("MWX_XATTN_MFC")) != 0;
-  return on;
+static std::atomic<int>& xattn_mfs_mode() {
+  static std::atomic<int> m{-1};
+  return m;
 }
+static bool xattn_mfs_on() {
+  int v = xattn_mfs_mode().load();
+  if (v < 0) {
+    v = (getenv("MWX_XATTN_MFS") && atoi(getenv("MWX_XATTN_MFS")) == 0) ? 0 : 1;
+    xattn_mfs_mode().store(v);
+  }
+  return v != 0;
+}
+int xattn_mfs_set(int on) { return xattn_mfs_mode().exchange(on < 0 ? -1 : (on ? 1 : 0)); }
 
 template <typename T>
 bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float* bias,
@@ -1417,18 +1331,16 @@ bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float*
       default: return false;
     }
   }
-  // MX-fp8 cache: scores on MFMA (default; MWX_XATTN_MFS=0: the v_dot2 scores,
-  // the A/B: C5 one lane 735.8 -> 778.8 audio-s/s, 52.4 -> 44.6 us per launch)
-  static const bool mfs = !(getenv("MWX_XATTN_MFS") && atoi(getenv("MWX_XATTN_MFS")) == 0);
+  // MX-fp8 cache: scores on MFMA (default; MWX_XATTN_MFS=0 or
+  // xattn_mfs_set(0): the v_dot2 scores, the A/B: C5 one lane 735.8 -> 778.8
+  // audio-s/s, 52.4 -> 44.6 us per launch)
+  const bool mfs = xattn_mfs_on();
   switch (nq) {
 #define XQ(N)                                  \
   case N:                                      \
     if (kv8 && mfs)                            \
       dec_xattn_kernel<T, N, true, true, 0, true><<<g, 256, 0, st>>>(P, KS, pcols, bias, kbase, \
           vbase, kscale8, vscale8, kv_index, active, n_keys, cap, R, o, H, scale, span);       \
-    else if (!kv8 && xattn_mfc())              \
-      dec_xattn_kernel<T, N, false, true, 0, true><<<g, 256, 0, st>>>(P, KS, pcols, bias,   \
-          kbase, vbase, kscale8, vscale8, kv_index, active, n_keys, cap, R, o, H, scale, span); \
     else if (kv8 && nt)                        \
       XL(N, true, true);                       \
     else if (kv8)                              \
@@ -1531,9 +1443,6 @@ void dec_attention(const float* P, int KS, int pcols, const float* bias, float q
   // MWX_XATTN_NBC=0: the runtime-batch-count cross kernel (A/B of the
   // constant-count load stream)
   static const bool xattn_nbc = !(getenv("MWX_XATTN_NBC") && atoi(getenv("MWX_XATTN_NBC")) == 0);
-  // MWX_XATTN_PF=7: 7 L2-prefetch helper workgroups per (row, head) for small
-  // cross-attention grids (A/B; off by default)
-  static const int xattn_pf = getenv("MWX_XATTN_PF") ? (atoi(getenv("MWX_XATTN_PF")) > 0 ? 7 : 0) : 0;
   if (fixed_len == 0 && self_ub4)
     dec_attn_kernel<T, true, 4><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale, kbase,
                                                    vbase, kv_index, pos, active, fixed_len,
@@ -1544,28 +1453,7 @@ void dec_attention(const float* P, int KS, int pcols, const float* bias, float q
                                                 kv_index, pos, active, fixed_len, kv_len_cap, o,
                                                 H, scale, kvmap, own_from, map_row0, nq, R,
                                                 write_new);
-  else if (xattn_pf > 0 && nq == 1 && H % 8 == 0 && (long)R * H * (1 + xattn_pf) <= 256 &&
-           fixed_len == 1500 && xattn_nbc) {
-    // (one request: helper workgroups pull the K / V rows into L2)
-    const dim3 gp(H, R * (1 + xattn_pf));
-    if (xattn_nt)
-      dec_attn_kernel<T, false, 8, true, 6, 7><<<gp, 256, 0, st>>>(
-          P, KS, pcols, bias, qscale, kscale, kbase, vbase, kv_index, pos, active, fixed_len,
-          kv_len_cap, o, H, scale, nullptr, nullptr, 0, nq, R, 1, span);
-    else
-      dec_attn_kernel<T, false, 8, false, 6, 7><<<gp, 256, 0, st>>>(
-          P, KS, pcols, bias, qscale, kscale, kbase, vbase, kv_index, pos, active, fixed_len,
-          kv_len_cap, o, H, scale, nullptr, nullptr, 0, nq, R, 1, span);
-  } else if (xattn_mfc() && fixed_len == 1500 && xattn_nbc) {
-    if (xattn_nt)
-      dec_attn_kernel<T, false, 8, true, 6, 0, true><<<g, 256, 0, st>>>(
-          P, KS, pcols, bias, qscale, kscale, kbase, vbase, kv_index, pos, active, fixed_len,
-          kv_len_cap, o, H, scale, nullptr, nullptr, 0, nq, R, 1, span);
-    else
-      dec_attn_kernel<T, false, 8, false, 6, 0, true><<<g, 256, 0, st>>>(
-          P, KS, pcols, bias, qscale, kscale, kbase, vbase, kv_index, pos, active, fixed_len,
-          kv_len_cap, o, H, scale, nullptr, nullptr, 0, nq, R, 1, span);
-  } else if (xattn_nt && fixed_len == 1500 && xattn_nbc)  // (every Whisper model: 1500 frames)
+  else if (xattn_nt && fixed_len == 1500 && xattn_nbc)  // (every Whisper model: 1500 frames)
     dec_attn_kernel<T, false, 8, true, 6><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale,
                                                              kbase, vbase, kv_index, pos, active,
                                                              fixed_len, kv_len_cap, o, H, scale,

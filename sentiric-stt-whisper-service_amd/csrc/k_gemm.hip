@@ -541,120 +541,6 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
 }
 
 // ---------------------------------------------------------------------------
-// LayerNorm prologue of the LN-fused decode GEMMs (kernels.h LnFuse): rows
-// 0..M-1 (M <= LNF_MAX_ROWS) normalised into LDS exactly as ln_dec_kernel
-// does it (threads 0..255, thread t owning elements 8t..8t+7, the same slab
-// sum, double sums, DPP wave reductions and workgroup combine); the caller's
-// lanes then form their A fragments with lnf_frag. Every thread of the
-// workgroup must call it (it holds workgroup barriers).
-// ---------------------------------------------------------------------------
-struct LnLds {
-  float v[LNF_MAX_ROWS][2048];  // completed residual rows
-  float mean[LNF_MAX_ROWS], scale[LNF_MAX_ROWS];
-  int act[LNF_MAX_ROWS];
-  double red[2][4];
-};
-__device__ __forceinline__ void lnf_prologue(const LnFuse& L, int M, int N, LnLds& sh,
-                                             bool write_x) {
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const bool par = tid < 256;
-  const bool own = par && tid * 8 < N;
-  const int i0 = own ? tid * 8 : 0;
-  for (int m = 0; m < M; ++m) {
-    const int act = L.active ? L.active[m] : 1;
-    float v[8];
-    if (own) {
-      const float* xr = L.x + (long)m * N + i0;
-      const f32x4 xa = *reinterpret_cast<const f32x4*>(xr);
-      const f32x4 xc = *reinterpret_cast<const f32x4*>(xr + 4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] = xa[e];
-        v[4 + e] = xc[e];
-      }
-      if (L.P) {
-        const long pstride = (long)M * N;
-        const float* pp = L.P + (long)m * N + i0;
-        f32x4 pk[8][2];
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (k < L.KS) {
-            pk[k][0] = *reinterpret_cast<const f32x4*>(pp + k * pstride);
-            pk[k][1] = *reinterpret_cast<const f32x4*>(pp + k * pstride + 4);
-          }
-        const f32x4 pb0 = *reinterpret_cast<const f32x4*>(L.pbias + i0);
-        const f32x4 pb1 = *reinterpret_cast<const f32x4*>(L.pbias + i0 + 4);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          float acc = pk[0][e >> 2][e & 3];
-#pragma unroll
-          for (int k = 1; k < 8; ++k)
-            if (k < L.KS) acc += pk[k][e >> 2][e & 3];
-          v[e] = (acc + (e < 4 ? pb0[e] : pb1[e - 4])) + v[e];
-        }
-        if (write_x && L.xout && act) {
-          float* xo = L.xout + (long)m * N + i0;
-          *reinterpret_cast<f32x4*>(xo) = f32x4{v[0], v[1], v[2], v[3]};
-          *reinterpret_cast<f32x4*>(xo + 4) = f32x4{v[4], v[5], v[6], v[7]};
-        }
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) sh.v[m][i0 + e] = v[e];
-    }
-    double s = 0.0;
-    if (own) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) s += (double)v[e];
-    }
-    if (par) {
-      s = wave_sum_d_dpp(s);
-      if (lane == 0) sh.red[0][wid] = s;
-    }
-    __syncthreads();
-    s = (sh.red[0][0] + sh.red[0][1]) + (sh.red[0][2] + sh.red[0][3]);
-    const float mean = (float)(s / N);
-    double s2 = 0.0;
-    if (own) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float d = v[e] - mean;
-        s2 += (double)(d * d);
-      }
-    }
-    if (par) {
-      s2 = wave_sum_d_dpp(s2);
-      if (lane == 0) sh.red[1][wid] = s2;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      s2 = (sh.red[1][0] + sh.red[1][1]) + (sh.red[1][2] + sh.red[1][3]);
-      const float variance = (float)(s2 / N);
-      sh.mean[m] = mean;
-      sh.scale[m] = 1.0f / sqrtf(variance + 1e-5f);
-      sh.act[m] = act;
-    }
-    __syncthreads();  // (red reused by the next row; v / stats visible to every lane)
-  }
-}
-// A fragment (8 consecutive k of row m) of the normalised rows: ln_dec's
-// ((v - mean) * scale) * w + b, rounded to T; rows >= M / inactive: zeros
-template <typename T>
-__device__ __forceinline__ typename Elt<T>::v8 lnf_frag(const LnFuse& L, const LnLds& sh, int M,
-                                                         int m, int k) {
-  typename Elt<T>::v8 o;
-  if (m < M && sh.act[m]) {
-    const float mean = sh.mean[m], scale = sh.scale[m];
-#pragma unroll
-    for (int e = 0; e < 8; ++e)
-      o[e] = to_t<T>(((sh.v[m][k + e] - mean) * scale) * L.w[k + e] + L.b[k + e]);
-  } else {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = to_t<T>(0.0f);
-  }
-  return o;
-}
-
-// ---------------------------------------------------------------------------
 // skinny (decode) GEMM: M <= 16*MT rows. One workgroup = one 16-column strip;
 // its NW waves split K, each wave owns KCH consecutive 32-deep k-steps and
 // issues all of its W and A fragment loads before the first MFMA (one memory
@@ -665,31 +551,15 @@ __device__ __forceinline__ void skinny_store(const EpiParams& P, int m, int n, f
   epi_store<EPI, T, OUT16>(P, 0, m, n, v);
 }
 
-// Row-block grouping (zrb = row blocks > 1, decode_tile_of): a 1-D grid where
-// the zrb row blocks of one weight tile are consecutive ids of one residue
-// mod 8 -- one XCD under the round-robin placement -- so the tile is read from
-// HBM about once and served to the other row blocks from that XCD's L2 (with
-// the row blocks as grid.z / grid.y, a beam step's 5 row blocks of 32 rows
-// re-read every weight tile from HBM 5 times). Which rows and columns a
-// workgroup computes, and how, is unchanged: results are bit-identical.
-__device__ __forceinline__ bool decode_tile_of(int zrb, int ntiles, int& t, int& z) {
-  const int L = blockIdx.x, W = 8 * zrb, w = L / W, j = L - w * W;
-  t = w * 8 + (j & 7);
-  z = j >> 3;
-  return t < ntiles;
-}
-
-template <typename T, int MT, int KCH, bool W8 = false, bool LNA = false>
+template <typename T, int MT, int KCH, bool W8 = false>
 __global__ __launch_bounds__(1024) void gemm_skinny(int epi, const T* __restrict__ Ap,
                                                     const void* __restrict__ Wv,
                                                     const uint8_t* __restrict__ Ws, int KT, int M,
-                                                    int N, EpiParams P, LnFuse LN, int zrb = 0) {
+                                                    int N, EpiParams P) {
   using V8 = typename Elt<T>::v8;
   __shared__ f32x4 red[16][MT][64];
-  __shared__ typename std::conditional<LNA, LnLds, int>::type lnsh;  // (LNA only)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, NW = blockDim.x >> 6;
-  int bx = blockIdx.x, by = blockIdx.y;
-  if (zrb > 0 && !decode_tile_of(zrb, (N + 15) / 16, bx, by)) return;
+  const int bx = blockIdx.x, by = blockIdx.y;
   const int n0 = bx * 16;
   // row block of 16*MT rows (grid.y): per-row arithmetic does not depend on M
   // nor on the block size (each output is the same MFMA chain over k)
@@ -714,18 +584,10 @@ __global__ __launch_bounds__(1024) void gemm_skinny(int epi, const T* __restrict
 #pragma unroll
     for (int c = 0; c < KCH; ++c) bfr[c] = ld8(wt + c * 512);
   }
-  if constexpr (LNA) {
-    // (MT = 1, M <= LNF_MAX_ROWS: the rows' LayerNorm is formed here)
-    lnf_prologue(LN, M, KT * 32, lnsh, blockIdx.x == 0 && blockIdx.y == 0);
 #pragma unroll
-    for (int c = 0; c < KCH; ++c)
-      afr[0][c] = lnf_frag<T>(LN, lnsh, M, lane & 15, (kt0 + c) * 32 + (lane >> 4) * 8);
-  } else {
+  for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int c = 0; c < KCH; ++c) afr[mt][c] = ld8(at + ((long)mt * KT + c) * 512);
-  }
+    for (int c = 0; c < KCH; ++c) afr[mt][c] = ld8(at + ((long)mt * KT + c) * 512);
   if constexpr (W8) {
 #pragma unroll
     for (int c = 0; c < KCH; ++c) bfr[c] = dequant8<T>(wraw[c], e8m0_to_f32(wsc[c]));
@@ -766,12 +628,14 @@ __global__ __launch_bounds__(1024) void gemm_skinny(int epi, const T* __restrict
 }
 
 // (waves, k-steps per wave) for a K: all 32-deep k-steps split evenly over at
-// most 16 waves with at most 10 k-steps each.
-static bool skinny_split(int K, int& nw, int& kch) {
+// most 16 waves with at most 10 k-steps each. want_nw > 0: exactly that many
+// waves (FFN1 runs 4, as the chained seam's skinny consumer does, k_chain.hip)
+static bool skinny_split(int K, int& nw, int& kch, int want_nw = 0) {
   if (K % 32) return false;
   const int S = K / 32;
   static const int wmax = getenv("MWX_SKINNY_NW") ? atoi(getenv("MWX_SKINNY_NW")) : 16;
-  for (int w = std::min(16, std::max(1, wmax)); w >= 1; --w) {
+  const int wtop = want_nw > 0 ? want_nw : std::min(16, std::max(1, wmax));
+  for (int w = wtop; w >= (want_nw > 0 ? want_nw : 1); --w) {
     if (S % w) continue;
     const int c = S / w;
     if (c == 1 || c == 2 || c == 3 || c == 4 || c == 6 || c == 8 || c == 10) {
@@ -783,27 +647,16 @@ static bool skinny_split(int K, int& nw, int& kch) {
   return false;
 }
 
-// decode GEMMs with several row blocks: group them per weight tile on one XCD
-// (decode_tile_of) with MWX_DEC_GROUP_ROWS=1. Off by default: measured slower
-// (beam 5 one lane 742.9 -> 703.7, C3 one lane 1207.7 -> 1179.9 audio-s/s,
-// same box)
-static bool decode_group_rows() {
-  static const bool on = getenv("MWX_DEC_GROUP_ROWS") && atoi(getenv("MWX_DEC_GROUP_ROWS")) != 0;
-  return on;
-}
-
-template <typename T, int MT, bool W8, bool LNA = false>
+template <typename T, int MT, bool W8>
 static bool skinny_launch(int epi, const T* Ap, const void* Wp, const uint8_t* Ws, int M, int N,
-                          int K, const EpiParams& P, hipStream_t st, const LnFuse& ln = LnFuse()) {
+                          int K, const EpiParams& P, hipStream_t st) {
   int nw = 0, kch = 0;
-  if (!skinny_split(K, nw, kch)) return false;
-  if (LNA && (nw < 4 || K > 2048 || M > LNF_MAX_ROWS)) return false;  // (256 LayerNorm threads)
+  if (!skinny_split(K, nw, kch, P.nw)) return false;
   const int nrb = (M + 16 * MT - 1) / (16 * MT), nx = (N + 15) / 16;
-  const int zrb = nrb > 1 && decode_group_rows() ? nrb : 0;
-  const dim3 g = zrb ? dim3((nx + 7) / 8 * 8 * zrb) : dim3(nx, nrb), b(64 * nw);
+  const dim3 g(nx, nrb), b(64 * nw);
   switch (kch) {
 #define SK(C) \
-  case C: gemm_skinny<T, MT, C, W8, LNA><<<g, b, 0, st>>>(epi, Ap, Wp, Ws, K / 32, M, N, P, ln, zrb); return true;
+  case C: gemm_skinny<T, MT, C, W8><<<g, b, 0, st>>>(epi, Ap, Wp, Ws, K / 32, M, N, P); return true;
     SK(1) SK(2) SK(3) SK(4) SK(6) SK(8) SK(10)
 #undef SK
     default: return false;
@@ -818,24 +671,15 @@ static bool skinny_launch(int epi, const T* Ap, const void* Wp, const uint8_t* W
 // order) by the consumer kernel together with the epilogue ggml applies
 // (bias, residual, scale, f16 rounding), so the reduction costs no launch.
 // ---------------------------------------------------------------------------
-template <typename T, int MT, int KCH, bool W8 = false, bool LNA = false>
+template <typename T, int MT, int KCH, bool W8 = false>
 __global__ __launch_bounds__(256) void gemm_splitk(const T* __restrict__ Ap,
                                                    const void* __restrict__ Wv,
                                                    const uint8_t* __restrict__ Ws, int KT, int M,
-                                                   int N, int kslice, float* __restrict__ P,
-                                                   LnFuse LN, int zrb = 0) {
+                                                   int N, int kslice, float* __restrict__ P) {
   using V8 = typename Elt<T>::v8;
   __shared__ f32x4 red[4][MT][64];
-  __shared__ typename std::conditional<LNA, LnLds, int>::type lnsh;  // (LNA only)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  int bx = blockIdx.x, ks = blockIdx.y, bz = blockIdx.z;
-  if (zrb > 0) {  // (row-block grouping, gemm_skinny's note)
-    const int nx = (N + 15) / 16, nks = KT * 32 / kslice;
-    int t;
-    if (!decode_tile_of(zrb, nx * nks, t, bz)) return;
-    bx = t % nx;
-    ks = t / nx;
-  }
+  const int bx = blockIdx.x, ks = blockIdx.y, bz = blockIdx.z;
   const int n0 = bx * 16;
   const int m_base = bz * 16 * MT;  // row block (16*MT rows per grid.z slice)
   const int Mb = min(16 * MT, M - m_base);
@@ -858,18 +702,10 @@ __global__ __launch_bounds__(256) void gemm_splitk(const T* __restrict__ Ap,
 #pragma unroll
     for (int c = 0; c < KCH; ++c) bfr[c] = ld8(wt + c * 512);
   }
-  if constexpr (LNA) {
-    lnf_prologue(LN, M, KT * 32, lnsh,
-                 blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0);
 #pragma unroll
-    for (int c = 0; c < KCH; ++c)
-      afr[0][c] = lnf_frag<T>(LN, lnsh, M, lane & 15, (kt0 + c) * 32 + (lane >> 4) * 8);
-  } else {
+  for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int c = 0; c < KCH; ++c) afr[mt][c] = ld8(at + ((long)mt * KT + c) * 512);
-  }
+    for (int c = 0; c < KCH; ++c) afr[mt][c] = ld8(at + ((long)mt * KT + c) * 512);
   if constexpr (W8) {
 #pragma unroll
     for (int c = 0; c < KCH; ++c) bfr[c] = dequant8<T>(wraw[c], e8m0_to_f32(wsc[c]));
@@ -910,7 +746,7 @@ int splitk_factor(int K) {
 
 template <typename T>
 int gemm_splitk_partials(const T* Ap, const DecW<T>& Wd, int M, int N, int K, float* P,
-                         hipStream_t st, const LnFuse* ln) {
+                         hipStream_t st) {
   const void* Wp = Wd.q ? (const void*)Wd.q : (const void*)Wd.w;
   const uint8_t* Ws = Wd.s;
   const bool w8 = Wd.q != nullptr;
@@ -927,33 +763,14 @@ int gemm_splitk_partials(const T* Ap, const DecW<T>& Wd, int M, int N, int K, fl
   static const bool mt1 = !(getenv("MWX_DEC_MT1") && atoi(getenv("MWX_DEC_MT1")) == 0);
   if (mt1 && M <= 64) MT = 1;  // 16-row blocks (greedy +3%; MWX_DEC_MT1=0 for A/B)
   const int nrb = (M + 16 * MT - 1) / (16 * MT), nx = (N + 15) / 16;
-  const int zrb = nrb > 1 && !ln && decode_group_rows() ? nrb : 0;
-  const dim3 g = zrb ? dim3((nx * ks + 7) / 8 * 8 * zrb) : dim3(nx, ks, nrb);
-  if (ln) {  // LayerNorm-fused A operand (M <= LNF_MAX_ROWS, one 16-row block)
-    if (M > LNF_MAX_ROWS || K > 2048) return 0;
-#define SKF(C)                                                                                  \
-  if (kch == C) {                                                                               \
-    if (w8)                                                                                     \
-      gemm_splitk<T, 1, C, true, true><<<g, 256, 0, st>>>(Ap, Wp, Ws, K / 32, M, N, kslice, P,  \
-                                                          *ln);                                 \
-    else                                                                                        \
-      gemm_splitk<T, 1, C, false, true><<<g, 256, 0, st>>>(Ap, Wp, Ws, K / 32, M, N, kslice, P, \
-                                                           *ln);                                \
-    return ks;                                                                                  \
-  }
-    SKF(1) SKF(2) SKF(3) SKF(4) SKF(5)
-#undef SKF
-    return 0;
-  }
-#define SKL(MTV, C)                                                                       \
-  if (MT == MTV && kch == C) {                                                            \
-    if (w8)                                                                               \
-      gemm_splitk<T, MTV, C, true><<<g, 256, 0, st>>>(Ap, Wp, Ws, K / 32, M, N, kslice, P, \
-                                                      LnFuse(), zrb);                     \
-    else                                                                                  \
-      gemm_splitk<T, MTV, C, false><<<g, 256, 0, st>>>(Ap, Wp, Ws, K / 32, M, N, kslice, P, \
-                                                       LnFuse(), zrb);                    \
-    return ks;                                                                            \
+  const dim3 g(nx, ks, nrb);
+#define SKL(MTV, C)                                                                         \
+  if (MT == MTV && kch == C) {                                                              \
+    if (w8)                                                                                 \
+      gemm_splitk<T, MTV, C, true><<<g, 256, 0, st>>>(Ap, Wp, Ws, K / 32, M, N, kslice, P);  \
+    else                                                                                    \
+      gemm_splitk<T, MTV, C, false><<<g, 256, 0, st>>>(Ap, Wp, Ws, K / 32, M, N, kslice, P); \
+    return ks;                                                                              \
   }
 #define SKM(MTV) SKL(MTV, 1) SKL(MTV, 2) SKL(MTV, 3) SKL(MTV, 4) SKL(MTV, 5)
   SKM(1) SKM(2) SKM(3) SKM(4)
@@ -963,13 +780,13 @@ int gemm_splitk_partials(const T* Ap, const DecW<T>& Wd, int M, int N, int K, fl
 }
 
 template int gemm_splitk_partials<_Float16>(const _Float16*, const DecW<_Float16>&, int, int, int,
-                                            float*, hipStream_t, const LnFuse*);
+                                            float*, hipStream_t);
 template int gemm_splitk_partials<__bf16>(const __bf16*, const DecW<__bf16>&, int, int, int, float*,
-                                          hipStream_t, const LnFuse*);
+                                          hipStream_t);
 
 template <typename T>
 bool gemm_decode(int epi, const T* Ap, const DecW<T>& Wd, int M, int N, int K, const EpiParams& P,
-                 hipStream_t st, const LnFuse* ln) {
+                 hipStream_t st) {
   const void* Wp = Wd.q ? (const void*)Wd.q : (const void*)Wd.w;
   const uint8_t* Ws = Wd.s;
   int MT = (std::min(M, 64) + 15) / 16;
@@ -981,11 +798,6 @@ bool gemm_decode(int epi, const T* Ap, const DecW<T>& Wd, int M, int N, int K, c
   static const bool mt1 = !(getenv("MWX_DEC_MT1") && atoi(getenv("MWX_DEC_MT1")) == 0);
   if (mt1 && M <= 64) MT = 1;  // 16-row blocks (greedy +3%; MWX_DEC_MT1=0 for A/B)
   if (P.mt >= 1 && P.mt <= 4) MT = P.mt;
-  if (ln) {  // LayerNorm-fused A operand (M <= LNF_MAX_ROWS, one 16-row block)
-    if (M > LNF_MAX_ROWS) return false;
-    return Wd.q ? skinny_launch<T, 1, true, true>(epi, Ap, Wp, Ws, M, N, K, P, st, *ln)
-                : skinny_launch<T, 1, false, true>(epi, Ap, Wp, Ws, M, N, K, P, st, *ln);
-  }
 #define SKM(MTV)                                                                          \
   if (MT == MTV)                                                                          \
     return Wd.q ? skinny_launch<T, MTV, true>(epi, Ap, Wp, Ws, M, N, K, P, st)            \
@@ -995,9 +807,9 @@ bool gemm_decode(int epi, const T* Ap, const DecW<T>& Wd, int M, int N, int K, c
   return false;
 }
 template bool gemm_decode<_Float16>(int, const _Float16*, const DecW<_Float16>&, int, int, int,
-                                    const EpiParams&, hipStream_t, const LnFuse*);
+                                    const EpiParams&, hipStream_t);
 template bool gemm_decode<__bf16>(int, const __bf16*, const DecW<__bf16>&, int, int, int,
-                                  const EpiParams&, hipStream_t, const LnFuse*);
+                                  const EpiParams&, hipStream_t);
 
 // ---------------------------------------------------------------------------
 // dispatch

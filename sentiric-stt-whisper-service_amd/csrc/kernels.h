@@ -54,6 +54,7 @@ struct EpiParams {
   bool xcd_remap = true;  // gemm_big: XCD-aware tile order
   int group_m = 0;        // gemm_big: row tiles per group of the grouped tile order (0: row-major)
   int mt = 0;             // gemm_decode: rows per block = 16 * mt (0: the default rule)
+  int nw = 0;             // gemm_decode (skinny): waves splitting K (0: the default rule)
   // EPI_CROSS_KV with an MX-fp8 cache: k / v hold e4m3 codes, ks8 / vs8 the
   // E8M0 scales (two per (time, head) row of 64)
   uint8_t* ks8 = nullptr;
@@ -106,34 +107,16 @@ struct DecW {
   DecW(const T* w_) : w(w_) {}
   DecW(const uint8_t* q_, const uint8_t* s_) : q(q_), s(s_) {}
 };
-// Decode LayerNorm folded into the consumer GEMM (rows <= LNF_MAX_ROWS, the
-// single-request / streaming case): every workgroup of the GEMM recomputes
-// the LayerNorm of its rows exactly as layer_norm_dec does (same element
-// ownership, slab sum, double sums and roundings) and forms its A fragments
-// from it; the one workgroup with blockIdx == 0 writes the completed
-// residual x + (sum P + pbias) to xout (the other buffer of a ping-pong pair:
-// the other workgroups are still reading x). The LayerNorm launch goes away.
-constexpr int LNF_MAX_ROWS = 4;
-struct LnFuse {
-  const float* x = nullptr;      // [M][K] residual rows
-  const float* w = nullptr;      // LayerNorm weight / bias [K]
-  const float* b = nullptr;
-  const float* P = nullptr;      // producer's split-K slabs [KS][M][K] (nullptr: x is complete)
-  int KS = 0;
-  const float* pbias = nullptr;  // producer's bias [K]
-  float* xout = nullptr;         // completed residual (nullptr: not written)
-  const int* active = nullptr;   // row flags
-};
 template <typename T>
 int gemm_splitk_partials(const T* Ap, const DecW<T>& W, int M, int N, int K, float* P,
-                         hipStream_t st, const LnFuse* ln = nullptr);
+                         hipStream_t st);
 // Decode full-K GEMM over fragment-tiled weights with a fused epilogue
 // (EPI_GELU / EPI_RES / EPI_F32 / EPI_STORE16 / EPI_DEC_QKV), rows in blocks of
 // 64 so a row's arithmetic does not depend on the batch. Returns false if K is
 // unsupported.
 template <typename T>
 bool gemm_decode(int epi, const T* Ap, const DecW<T>& W, int M, int N, int K, const EpiParams& P,
-                 hipStream_t st, const LnFuse* ln = nullptr);
+                 hipStream_t st);
 // Log-mel of a batch of clips in one pass (three launches): clip c's samples
 // at pcm_base + desc[c].pcm_off (n), its mel [n_mels][n_len] at mel_base +
 // desc[c].mel_off, normalised in place; mx[c] = the clip's raw max; part:
@@ -181,6 +164,46 @@ template <typename T>
 void embed(const T* te, const float* pe, const int* tok, const int* pos, const int* active,
            float* x, int R, int d, hipStream_t st);
 
+// Decoder-layer seam in one launch (k_chain.hip): [producer split-K GEMM
+// p_A x p_W -> slabs ln.P] -> LayerNorm of the M rows (x completed in place
+// from the slabs + ln.pbias when there is a producer) into ln.y (packed A
+// tiles) -> consumer GEMM ln.y x c_W: split-K slabs c_P [c_ks][M][c_N], or
+// (c_skinny) the full-K 4-wave GEMM with c_epi's EPI_GELU packed epilogue.
+// Same per-element arithmetic as gemm_splitk_partials + layer_norm_dec +
+// gemm_splitk_partials / gemm_decode(EPI_GELU, nw = 4). M <= 64, d % 128 == 0,
+// 16-bit weights. err: set if a hand-off wait timed out. Returns false if the
+// shape is unsupported.
+struct ChainLn {
+  float* x = nullptr;
+  const float* w = nullptr;
+  const float* b = nullptr;
+  const float* P = nullptr;  // the producer's slab buffer [KS][M][d] (KS set by chain_launch)
+  int KS = 0;
+  const float* pbias = nullptr;
+  void* y = nullptr;
+  const int* active = nullptr;
+};
+struct ChainArgs {
+  int M = 0, d = 0;
+  const void* p_A = nullptr;
+  const void* p_W = nullptr;  // nullptr: no producer (x complete)
+  int p_K = 0, p_ks = 0, p_kch = 0;
+  ChainLn ln;
+  const void* c_W = nullptr;
+  int c_N = 0;
+  bool c_skinny = false;
+  int c_ks = 0, c_kch = 0;
+  float* c_P = nullptr;
+  EpiParams c_epi;
+  unsigned* ctr = nullptr;   // this seam's counter slot (chain_slot_words(), zero at launch)
+  unsigned* zero = nullptr;  // a slot to zero (the previous seam launch's), or nullptr
+  int nzero = 0;
+  unsigned* err = nullptr;
+};
+int chain_slot_words();
+template <typename T>
+bool chain_launch(const ChainArgs& a, hipStream_t st);
+
 // encoder self-attention: q,k [B][H][L][64], vt [B][H][64][L] f16 -> o [B*L][H*64] (T)
 template <typename T>
 void enc_attention(const _Float16* q, const _Float16* k, const _Float16* vt, T* o, int B,
@@ -221,6 +244,9 @@ void kv_append(const float* P, int KS, int pcols, const float* bias, float kscal
 // dec_attention. Returns false if nq is not supported (1..8; f16 caches: 2..8).
 // kscale8 / vscale8 != nullptr: the cache is MX-fp8 (kbase / vbase hold e4m3
 // codes [slot][H][cap][64], the scales [slot][H][cap][2] E8M0), any nq >= 1.
+// MX-fp8 grouped cross-attention on MFMA (1, default) or v_dot2 (0); -1:
+// MWX_XATTN_MFS. Returns the previous setting (the A/B tests).
+int xattn_mfs_set(int on);
 template <typename T>
 bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float* bias,
                                  const void* kbase, const void* vbase, const int* kv_index,

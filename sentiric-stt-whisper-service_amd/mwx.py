@@ -212,6 +212,10 @@ def lib() -> C.CDLL:
     L.mwx_test_dequantize.argtypes = [C.c_int, C.c_void_p, C.c_long, C.POINTER(C.c_float)]
     L.mwx_test_decode_counters.restype = C.c_int
     L.mwx_test_decode_counters.argtypes = [P, C.POINTER(C.c_long), C.POINTER(C.c_long), C.c_int]
+    L.mwx_test_set_xattn_mfs.restype = C.c_int
+    L.mwx_test_set_xattn_mfs.argtypes = [C.c_int]
+    L.mwx_test_set_chain.restype = C.c_int
+    L.mwx_test_set_chain.argtypes = [C.c_int]
     L.mwx_test_sample_draws.restype = C.c_int
     L.mwx_test_sample_draws.argtypes = [P, fpp, fpp, C.c_int, C.c_int, C.POINTER(C.c_double),
                                         C.POINTER(C.c_int), C.c_int, C.c_int, C.c_int,
@@ -259,6 +263,18 @@ def write_synthetic_model(path: str, arch: str, wtype: int = GGML_F16, seed: int
     rc = lib().mwx_write_synthetic_model(path.encode(), arch.encode(), wtype, seed)
     if rc != 0:
         raise RuntimeError(f"mwx_write_synthetic_model failed ({rc})")
+
+
+def set_chain(on: Optional[bool]) -> int:
+    """mwx_test_set_chain: chained decode seams on / off (None: the MWX_CHAIN
+    default); returns the previous setting (-1 default, 0 off, 1 on)."""
+    return lib().mwx_test_set_chain(-1 if on is None else int(bool(on)))
+
+
+def set_xattn_mfs(on: Optional[bool]) -> int:
+    """mwx_test_set_xattn_mfs: the MX-fp8 grouped cross-attention on MFMA
+    (True) or v_dot2 (False); None: the MWX_XATTN_MFS default."""
+    return lib().mwx_test_set_xattn_mfs(-1 if on is None else int(bool(on)))
 
 
 def dequantize(qtype: int, raw: bytes, n: int) -> np.ndarray:

@@ -62,20 +62,25 @@ def run(path, beam, inc, secs, prompt, prefill_min):
     return json.loads(r.stdout.strip().splitlines()[-1])
 
 
-@pytest.mark.parametrize("arch,wtype", [("micro", mwx.GGML_F16), ("tiny.en", mwx.GGML_F16),
-                                        ("large-v3-l2", mwx.GGML_BF16)])
-def test_prefill_logits_equal_stepwise(make_model, arch, wtype):
+@pytest.mark.parametrize("arch,wtype,fp8", [("micro", mwx.GGML_F16, False),
+                                            ("tiny.en", mwx.GGML_F16, False),
+                                            ("large-v3-l2", mwx.GGML_BF16, False),
+                                            ("large-v3-l2", mwx.GGML_BF16, True)])
+def test_prefill_logits_equal_stepwise(make_model, arch, wtype, fp8):
     """Teacher-forced: tokens 0 .. n-2 through the prefill (one pass, virtual
-    rows in 16- / 32-row GEMM blocks, cross-attention in groups of 8) and the
-    last as a decode step give the stepwise logits bit for bit, for prompts
-    of 2 .. 226 positions (chunks of up to MWX_PREFILL_ROWS rows)."""
+    rows in 16- / 32-row GEMM blocks, cross-attention in groups of q = min(8,
+    n - 1): q = 2 .. 8, every grouped-kernel instantiation a short prompt
+    takes) and the last as a decode step (the chained seams) give the
+    stepwise logits bit for bit, for prompts of 3 .. 226 positions (chunks of
+    up to MWX_PREFILL_ROWS rows); also in the MX-fp8 compute mode, whose
+    cross-attention is the MFMA-score grouped kernel for every group size."""
     path = make_model(arch, wtype)
     import numpy as np
-    with mwx.Context.open(path) as ctx:
+    with mwx.Context.open(path, compute=mwx.COMPUTE_MXFP8 if fp8 else mwx.COMPUTE_MODEL) as ctx:
         ctx.test_encode(pcm_clip(1), cross=False, state_index=0)
         ctx.test_encode(pcm_clip(1), cross=False, state_index=1)
         rng = np.random.default_rng(7)
-        for n in (3, 9, 70, 226):
+        for n in (3, 4, 5, 6, 7, 8, 9, 70, 226):
             toks = [int(t) for t in rng.integers(0, 50000, n)]
             a = ctx.test_decode_last(toks, state_index=0)
             b = ctx.test_decode_last_prefill(toks, state_index=1)

@@ -277,3 +277,74 @@ def test_v3_geometry_concurrent_lanes_equal_sequential(v3):
         for i in range(len(pcms)):
             assert ctx.token_records(bases[j] + i) == [
                 (t.id, t.t0, t.t1, t.p) for s in ctx.segments(bases[j] + i) for t in s.tokens]
+
+
+def test_v3_geometry_mxfp8_teacher_forced_220_steps(v3):
+    """fp8 mode (C5's compute mode) at large-v3 geometry over a whole benched
+    window: 220 teacher-forced decode steps along the MX oracle's own greedy
+    stream (bench_fixed_steps), the device's decoder (fp8 weights, fp8 cross
+    cache through the MFMA grouped cross-attention) against the oracle's
+    ORC_MXFP8 decoder on the same (device) cross K/V: logits within the MX
+    tolerance at every step, argmax equal wherever the oracle's top-1 margin
+    exceeds 2 x that error. The same with the v_dot2 cross-attention
+    (mwx_test_set_xattn_mfs(0)), ADVICE r03: the MFMA P.V (V scales folded
+    relative to each 32-key tile's largest, kernel comment) is at least as
+    close to the oracle as the v_dot2 P.V."""
+    _, _, path = v3
+    omx = orc.Oracle(path, mxfp8=True)
+    pcm = pcm_clip(2)
+    opt = greedy_opt()
+    opt.bench_fixed_steps = 220
+    _, osegs, _, _ = omx.full(pcm, opt)
+    oids = [t.id for s in osegs for t in s.tokens]
+    assert len(oids) == 220
+    toks = [omx.sot, omx.sot + 1, omx.transcribe] + oids[:-1]
+    errs = {}
+    for mfs in (True, False):
+        prev = mwx.set_xattn_mfs(mfs)
+        try:
+            with mwx.Context.open(path, compute=mwx.COMPUTE_MXFP8) as ctx:
+                _, k, v = ctx.test_encode(pcm)
+                dev = ctx.test_decode(toks)[2:]
+        finally:
+            mwx.set_xattn_mfs(None if prev < 0 else bool(prev))
+        ref = omx.decode_seq(k, v, toks)[2:]
+        n_text = omx.eot
+        err = float(np.abs(dev[:, :n_text] - ref[:, :n_text]).max())
+        s = np.sort(ref[:, :n_text], axis=1)
+        m = s[:, -1] - s[:, -2]
+        sure = m > 2 * err
+        assert (dev[sure, :n_text].argmax(1) == ref[sure, :n_text].argmax(1)).all()
+        errs[mfs] = err
+        print(f"fp8 v3 teacher-forced 220 steps, {'MFMA' if mfs else 'v_dot2'} cross-attention: "
+              f"logits err {err:.4f}, argmax checked at {int(sure.sum())} steps")
+        assert err < 0.3, err
+    assert errs[True] <= 1.25 * errs[False] + 0.01, errs
+
+
+@pytest.mark.parametrize("beam,inc", [(7, 0.0), (1, 0.2)])
+def test_v3_geometry_mxfp8_group_of_7(v3, beam, inc):
+    """fp8 mode with groups of 7 decoders per clip (beam 7, and
+    best_of 7 under temperature fallback): the grouped MX-fp8 cross-attention
+    at NQ = 7 (XQ(7)); replay-exact against the MX oracle's token loop on the
+    device's logits, and a 2-clip batch == each clip alone."""
+    _, _, path = v3
+    pcm = [pcm_clip(7, 30.0), pcm_clip(8, 24.0)]
+    with mwx.Context.open(path, compute=mwx.COMPUTE_MXFP8) as ctx:
+        p = service_params(ctx, beam=beam, temperature_inc=inc, language=b"en")
+        p.greedy.best_of = 7
+        assert ctx.full_batch_states(pcm, p, range(2)) == 0
+        batched = [mwx.token_ids(ctx.segments(i)) for i in range(2)]
+        for i in range(2):
+            assert ctx.full(pcm[i], p, state_index=2) == 0
+            assert mwx.token_ids(ctx.segments(2)) == batched[i], i
+        assert ctx.full(pcm[0], p, state_index=3) == 0
+        segs = ctx.segments(3)
+        omx = orc.Oracle(path, mxfp8=True)
+        opt = orc.FullOptions.service_defaults(beam_size=beam)
+        opt.best_of = 7
+        opt.temperature_inc = inc
+        opt.language = "en"
+        osegs = replay(ctx, omx, pcm[0], opt)
+    assert len(segs) >= 1 and sum(len(s.tokens) for s in segs) > 5
+    assert_same(segs, osegs, p_tol=1e-4)
