@@ -73,12 +73,6 @@ int mwx_test_sample_draws(struct mwx_context* ctx, const float* probs, const flo
                           int R, int V, const double* u, const int* ndraw, int KD, int exact,
                           int reps, int* ids, double* us);
 
-/* Chained decode seams (k_chain.hip: out-proj -> LN2 -> cross-Q, cross-out ->
- * LN3 -> FFN1 and FFN2 -> LN1 -> QKV as one launch each) on (1) or off (0,
- * the separate launches); -1 restores the MWX_CHAIN default (on). Process
- * wide, read when a decode loop starts. Returns the previous setting. */
-int mwx_test_set_chain(int on);
-
 /* MX-fp8 grouped cross-attention scores and P.V on MFMA (1, the default) or
  * the v_dot2 kernel (0); -1 restores the MWX_XATTN_MFS default. Returns the
  * previous setting. */

@@ -5,6 +5,8 @@
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../include
 //        -I../../sentiric-stt-whisper-service_amd/csrc dec_chain_probe.hip
 //        -L../../sentiric-stt-whisper-service_amd -lmwx -o dec_chain_probe
+// (k_chain.hip, the fused GEMM -> LayerNorm -> GEMM seam, is compiled in:
+// `verify seam` checks it bit for bit against the three launches)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -15,6 +17,7 @@
 #include <vector>
 
 #include "kernels.h"
+#include "k_chain.hip"  // (the fused-seam probe kernel)
 
 using T = __bf16;
 using namespace mwx;

@@ -15,7 +15,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -41,13 +40,6 @@
 namespace mwx {
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
-
-// chained decode seams on (1) / off (0) / from MWX_CHAIN (-1, the default);
-// mwx_test_set_chain sets it for the A/B tests
-inline std::atomic<int>& chain_mode() {
-  static std::atomic<int> m{-1};
-  return m;
-}
 
 // Process-wide order between graph capture and (de)allocation: while any
 // thread captures a stream, HIP rejects legacy-stream operations such as
@@ -210,9 +202,6 @@ struct State {
   // decoder workspace (row-batched)
   DBuf xd, hd, qd, od, ffd, logits, kself, vself, stepin, ctl, tokout, probs, logprobs, smask;
   DBuf pqkv, pres, pq;  // split-K partial slabs of the decode GEMMs
-  // chained decode seams (k_chain.hip): hand-off counters of a step (zeroed
-  // by the step's embedding kernel) and the time-out flag
-  DBuf chain_ctr, chain_err;
   // batched prompt prefill: virtual-row inputs [tok|pos|act|xidx|crow] and the
   // layer stack's activations / slabs for up to MWX_PREFILL_ROWS virtual rows
   DBuf pf_in, pf_x, pf_h, pf_o, pf_ff, pf_pqkv, pf_pres, pf_pq;
@@ -1017,7 +1006,6 @@ struct Driver {
     HIPC(hipMemsetAsync(S.kvown.p, 0, (size_t)R * 4, st));
     S.ctl.get((size_t)R * sizeof(RowCtl));
     S.tokout.get((size_t)R * sizeof(TokOut));
-    chain_prepare();
   }
 
   // beam search: rows take over other rows' self-attention histories
@@ -1110,98 +1098,16 @@ struct Driver {
   // projection (pre), the cross-attention (cross) and the chain after it
   // (post); run_layers runs them in order on one stream.
   struct LayerRun {
-    float* xd = nullptr;    // the residual stream's buffer
-    bool chain = false;
-    int chain_prev = -1;    // counter slot of the previous seam launch     // GEMM -> LayerNorm -> GEMM seams as one launch each
+    float* xd = nullptr;  // the residual stream's buffer
     int k1 = 0, k2 = 0, k3 = 0, k4 = 0;
     bool k5 = false;
     int ks_prev = 0;  // the last FFN2's split-K factor and bias (folded into
     const float* bias_prev = nullptr;  // the next consumer)
   };
-  // Chained seams (MWX_CHAIN=1; off by default until measured faster): out-proj -> LN2 -> cross-Q,
-  // cross-out -> LN3 -> FFN1 and FFN2 -> LN1 -> QKV each run as one launch
-  // (k_chain.hip; the same arithmetic as the separate launches), so a decode
-  // layer is 5 launches instead of 11. Decode steps of <= 64 rows with 16-bit
-  // weights; the prompt prefill, beam-sized steps and MX-fp8 weights keep the
-  // separate launches (bit-identical results).
-  static bool chain_on() {
-    int v = chain_mode().load();
-    if (v < 0) {
-      v = (getenv("MWX_CHAIN") && atoi(getenv("MWX_CHAIN")) != 0) ? 1 : 0;
-      chain_mode().store(v);
-    }
-    return v != 0;
-  }
-  // counter slots: seam (l, site) at 3 l + site, layer 0's LN1 + QKV at 3 L
-  int chain_slots() const { return 3 * L_dec + 1; }
-  unsigned* chain_ctr(int slot) {
-    return (unsigned*)S.chain_ctr.p + (size_t)slot * chain_slot_words();
-  }
-  // (outside any capture: before a decode loop) the counter slots, zeroed
-  void chain_prepare() {
-    S.chain_ctr.get((size_t)chain_slots() * chain_slot_words() * 4);
-    S.chain_err.get(4, true);
-    HIPC(hipMemsetAsync(S.chain_ctr.p, 0, (size_t)chain_slots() * chain_slot_words() * 4, st));
-  }
   void layers_begin(const LayerRows& rw, LayerRun& c, hipStream_t s) {
     c = LayerRun{};
     c.xd = rw.xd;
-    c.chain = !rw.prefill && rw.n <= 64 && !C.dec8 && d % 128 == 0 && d <= 2048 &&
-              chain_on() && S.chain_ctr.p != nullptr;
-    // a step's seams run in the order 3L, 0, 1, 2, 3, ..., 3(L-1) + 1: each
-    // launch zeroes its predecessor's slot (the first, the step's last)
-    c.chain_prev = 3 * (L_dec - 1) + 1;
     embed<T>(Wt(C.tok_emb), C.dec_pe, rw.tok, rw.pos, rw.act, rw.xd, rw.n, d, s);
-  }
-  // a chained seam's hand-off wait timed out since the last check (results
-  // of that step are wrong): 0, or -12 (after an error message)
-  int chain_check() {
-    if (!S.chain_err.p) return 0;
-    unsigned e = 0;
-    HIPC(hipMemcpyAsync(&e, S.chain_err.p, 4, hipMemcpyDeviceToHost, st));
-    HIPC(hipStreamSynchronize(st));
-    if (!e) return 0;
-    HIPC(hipMemsetAsync(S.chain_err.p, 0, 4, st));
-    MWX_LOG_ERROR("mwx: a chained decode seam timed out waiting for its producer\n");
-    return -12;
-  }
-  // one chained seam: [producer pA x pW (K = pK) -> slabs Pres] -> LayerNorm
-  // (lw, lb; producer bias pb) of the residual into hd -> consumer cW:
-  // split-K slabs cP (returns their KS) or the FFN1 GELU GEMM (cP == nullptr)
-  int chain_seam(const LayerRows& rw, LayerRun& c, int slot, const T* pA, const DecWeight* pW,
-                 int pK, const float* pb, const float* lw, const float* lb, const DecWeight& cW,
-                 int cN, float* cP, const float* cbias, hipStream_t s) {
-    ChainArgs a;
-    a.M = rw.n;
-    a.d = d;
-    a.p_A = pA;
-    a.p_W = pW ? pW->w : nullptr;
-    a.p_K = pK;
-    a.ln.x = c.xd;
-    a.ln.w = lw;
-    a.ln.b = lb;
-    a.ln.P = rw.Pres;
-    a.ln.pbias = pb;
-    a.ln.y = rw.hd;
-    a.ln.active = rw.act;
-    a.c_W = cW.w;
-    a.c_N = cN;
-    a.c_skinny = cP == nullptr;
-    a.c_P = cP;
-    if (!cP) {
-      a.c_epi.bias = cbias;
-      a.c_epi.c16 = rw.ffd;
-      a.c_epi.ldc = 4 * d;
-      a.c_epi.pack_out = true;
-    }
-    a.ctr = chain_ctr(slot);
-    a.zero = c.chain_prev >= 0 ? chain_ctr(c.chain_prev) : nullptr;
-    a.nzero = chain_slot_words();
-    c.chain_prev = slot;
-    a.err = (unsigned*)S.chain_err.p;
-    PerfScope ps(S, "dec_gemm", s);
-    if (!chain_launch<T>(a, s)) throw std::runtime_error("mwx: unsupported chained seam");
-    return cP ? splitk_factor(d) : 1;
   }
   // The d- and 3d-wide projections run as split-K GEMMs writing f32 partial
   // slabs; each consumer (LN: bias + residual, attention: bias/scale/f16 and
@@ -1214,17 +1120,10 @@ struct Driver {
     _Float16* ks = rw.kself + l * layer_self;
     _Float16* vs = rw.vself + l * layer_self;
     T* hd = rw.hd;
-    if (c.chain) {
-      // (layers > 0: LN1 + QKV ran in the previous layer's FFN2 seam)
-      if (l == 0)
-        c.k1 = chain_seam(rw, c, 3 * L_dec, nullptr, nullptr, 0, nullptr, W.ln1_w, W.ln1_b, W.qkv,
-                          3 * d, rw.Pqkv, nullptr, s);
-    } else {
-      layer_norm_dec<T>(c.xd, W.ln1_w, W.ln1_b, hd, n, d, rw.act, s, c.ks_prev ? rw.Pres : nullptr,
-                        c.ks_prev, c.bias_prev);
-      PerfScope ps(S, "dec_gemm", s);
-      c.k1 = gemm_splitk_partials<T>(hd, Dw(W.qkv), n, 3 * d, d, rw.Pqkv, s);
-    }
+    layer_norm_dec<T>(c.xd, W.ln1_w, W.ln1_b, hd, n, d, rw.act, s, c.ks_prev ? rw.Pres : nullptr,
+                      c.ks_prev, c.bias_prev);
+    { PerfScope ps(S, "dec_gemm", s);
+      c.k1 = gemm_splitk_partials<T>(hd, Dw(W.qkv), n, 3 * d, d, rw.Pqkv, s); }
     static const int pf_selfwrite =
         getenv("MWX_PREFILL_SELFWRITE") ? atoi(getenv("MWX_PREFILL_SELFWRITE")) : 0;
     if (rw.prefill)
@@ -1234,12 +1133,6 @@ struct Driver {
       dec_attention<T>(rw.Pqkv, c.k1, 3 * d, W.qkv_b, kqs, kqs, ks, vs, rw.crow, rw.pos, rw.act, 0,
                        Tctx, rw.od, n, H, 1.0f, s, rw.kvmap, rw.kvown, rw.map_row0,
                        rw.prefill ? 1 : rw.xgroup, pf_selfwrite || !rw.prefill); }
-    if (c.chain) {
-      c.k2 = splitk_factor(d);
-      c.k3 = chain_seam(rw, c, 3 * l, rw.od, &W.o, d, W.o_b, W.lnc_w, W.lnc_b, W.cq, d, rw.Pq,
-                        nullptr, s);
-      return;
-    }
     { PerfScope ps(S, "dec_gemm", s);
       c.k2 = gemm_splitk_partials<T>(rw.od, Dw(W.o), n, d, d, rw.Pres, s); }
     layer_norm_dec<T>(c.xd, W.lnc_w, W.lnc_b, hd, n, d, rw.act, s, rw.Pres, c.k2, W.o_b);
@@ -1289,24 +1182,6 @@ struct Driver {
   void layer_post(const LayerRows& rw, LayerRun& c, int l, hipStream_t s) {
     const int n = rw.n;
     const DecLayerW& W = C.dec[l];
-    if (c.chain) {
-      c.k4 = splitk_factor(d);
-      c.k5 = chain_seam(rw, c, 3 * l + 1, rw.od, &W.co, d, W.co_b, W.ln2_w, W.ln2_b, W.fc1, 4 * d,
-                        nullptr, W.fc1_b, s) > 0;
-      if (l + 1 < L_dec) {
-        const DecLayerW& Wn = C.dec[l + 1];
-        c.k1 = chain_seam(rw, c, 3 * l + 2, rw.ffd, &W.fc2, 4 * d, W.fc2_b, Wn.ln1_w, Wn.ln1_b,
-                          Wn.qkv, 3 * d, rw.Pqkv, nullptr, s);
-        c.ks_prev = splitk_factor(4 * d);
-      } else {
-        PerfScope ps(S, "dec_gemm", s);
-        c.ks_prev = gemm_splitk_partials<T>(rw.ffd, Dw(W.fc2), n, d, 4 * d, rw.Pres, s);
-      }
-      c.bias_prev = W.fc2_b;
-      if (!c.k1 || !c.k3 || !c.k4 || !c.k5 || !c.ks_prev)
-        throw std::runtime_error("mwx: unsupported split-K shape");
-      return;
-    }
     { PerfScope ps(S, "dec_gemm", s);
       c.k4 = gemm_splitk_partials<T>(rw.od, Dw(W.co), n, d, d, rw.Pres, s); }
     EpiParams e;
@@ -1314,7 +1189,6 @@ struct Driver {
     e.c16 = rw.ffd;
     e.ldc = 4 * d;
     e.pack_out = true;
-    e.nw = 4;  // (4 waves split K: the chained seam's FFN1 arithmetic)
     layer_norm_dec<T>(c.xd, W.ln2_w, W.ln2_b, rw.hd, n, d, rw.act, s, rw.Pres, c.k4, W.co_b);
     { PerfScope ps(S, "dec_gemm", s);
       c.k5 = gemm_decode<T>(EPI_GELU, rw.hd, Dw(W.fc1), n, 4 * d, d, e, s); }
@@ -1326,8 +1200,7 @@ struct Driver {
   }
 
   // embedding + all decoder layers; returns the last FFN2's split-K factor
-  // and bias (folded into the consumer: the final LayerNorm) and the buffer
-  // holding the residual stream
+  // and bias (folded into the consumer: the final LayerNorm)
   void run_layers(const LayerRows& rw, hipStream_t s, int& ks_prev, const float*& bias_prev) {
     LayerRun c;
     layers_begin(rw, c, s);

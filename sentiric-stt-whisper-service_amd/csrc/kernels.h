@@ -164,45 +164,6 @@ template <typename T>
 void embed(const T* te, const float* pe, const int* tok, const int* pos, const int* active,
            float* x, int R, int d, hipStream_t st);
 
-// Decoder-layer seam in one launch (k_chain.hip): [producer split-K GEMM
-// p_A x p_W -> slabs ln.P] -> LayerNorm of the M rows (x completed in place
-// from the slabs + ln.pbias when there is a producer) into ln.y (packed A
-// tiles) -> consumer GEMM ln.y x c_W: split-K slabs c_P [c_ks][M][c_N], or
-// (c_skinny) the full-K 4-wave GEMM with c_epi's EPI_GELU packed epilogue.
-// Same per-element arithmetic as gemm_splitk_partials + layer_norm_dec +
-// gemm_splitk_partials / gemm_decode(EPI_GELU, nw = 4). M <= 64, d % 128 == 0,
-// 16-bit weights. err: set if a hand-off wait timed out. Returns false if the
-// shape is unsupported.
-struct ChainLn {
-  float* x = nullptr;
-  const float* w = nullptr;
-  const float* b = nullptr;
-  const float* P = nullptr;  // the producer's slab buffer [KS][M][d] (KS set by chain_launch)
-  int KS = 0;
-  const float* pbias = nullptr;
-  void* y = nullptr;
-  const int* active = nullptr;
-};
-struct ChainArgs {
-  int M = 0, d = 0;
-  const void* p_A = nullptr;
-  const void* p_W = nullptr;  // nullptr: no producer (x complete)
-  int p_K = 0, p_ks = 0, p_kch = 0;
-  ChainLn ln;
-  const void* c_W = nullptr;
-  int c_N = 0;
-  bool c_skinny = false;
-  int c_ks = 0, c_kch = 0;
-  float* c_P = nullptr;
-  EpiParams c_epi;
-  unsigned* ctr = nullptr;   // this seam's counter slot (chain_slot_words(), zero at launch)
-  unsigned* zero = nullptr;  // a slot to zero (the previous seam launch's), or nullptr
-  int nzero = 0;
-  unsigned* err = nullptr;
-};
-int chain_slot_words();
-template <typename T>
-bool chain_launch(const ChainArgs& a, hipStream_t st);
 
 // encoder self-attention: q,k [B][H][L][64], vt [B][H][64][L] f16 -> o [B*L][H*64] (T)
 template <typename T>

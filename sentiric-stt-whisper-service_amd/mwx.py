@@ -214,8 +214,6 @@ def lib() -> C.CDLL:
     L.mwx_test_decode_counters.argtypes = [P, C.POINTER(C.c_long), C.POINTER(C.c_long), C.c_int]
     L.mwx_test_set_xattn_mfs.restype = C.c_int
     L.mwx_test_set_xattn_mfs.argtypes = [C.c_int]
-    L.mwx_test_set_chain.restype = C.c_int
-    L.mwx_test_set_chain.argtypes = [C.c_int]
     L.mwx_test_sample_draws.restype = C.c_int
     L.mwx_test_sample_draws.argtypes = [P, fpp, fpp, C.c_int, C.c_int, C.POINTER(C.c_double),
                                         C.POINTER(C.c_int), C.c_int, C.c_int, C.c_int,
@@ -263,12 +261,6 @@ def write_synthetic_model(path: str, arch: str, wtype: int = GGML_F16, seed: int
     rc = lib().mwx_write_synthetic_model(path.encode(), arch.encode(), wtype, seed)
     if rc != 0:
         raise RuntimeError(f"mwx_write_synthetic_model failed ({rc})")
-
-
-def set_chain(on: Optional[bool]) -> int:
-    """mwx_test_set_chain: chained decode seams on / off (None: the MWX_CHAIN
-    default); returns the previous setting (-1 default, 0 off, 1 on)."""
-    return lib().mwx_test_set_chain(-1 if on is None else int(bool(on)))
 
 
 def set_xattn_mfs(on: Optional[bool]) -> int:
