@@ -589,6 +589,8 @@ def main():
     ap.add_argument("--lane-stagger", type=float, default=0.0,
                     help="seconds lane i waits (x i) before its first timed batch")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-token-timestamps", action="store_true",
+                    help="token_timestamps off (A/B only: the service sets it on)")
     ap.add_argument("--timing", choices=["span", "events"], default="span",
                     help="live kernel timing: device-clock launch spans (default) or HIP event "
                          "brackets")
@@ -650,7 +652,7 @@ def main():
     p.language = b"en"
     p.temperature = 0.0
     p.temperature_inc = 0.0
-    p.token_timestamps = True  # as the service sets it (src/stt_engine.cpp:225)
+    p.token_timestamps = not args.no_token_timestamps  # on, as the service sets it (src/stt_engine.cpp:225)
     p.suppress_nst = True
     p.bench_fixed_steps = args.decode_steps
     prompt_len = 3 if ARCH[args.arch][5] >= 51865 else 1
@@ -893,7 +895,8 @@ def main():
                              f"{args.clip_seconds:g} s clips per GPU ({lanes} in flight), mel + "
                              f"encoder + cross-KV + {args.decode_steps or 'until-EOT'} "
                              f"{'beam-%d' % args.beam if args.beam > 1 else 'greedy'} KV-cached "
-                             f"decode steps per 30-s window, token timestamps on (as the service), RCCL "
+                             f"decode steps per 30-s window, token timestamps "
+                             f"{'OFF (A/B)' if args.no_token_timestamps else 'on (as the service)'}, RCCL "
                              f"token gather to rank 0"),
                 "global_batch": world * args.clips,
                 "seq_len": 1500,

@@ -20,7 +20,8 @@ from typing import List, Optional, Sequence
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmwx.so")
+# MWX_LIB: an alternative build of the library (same ABI; A/B measurements)
+LIB_PATH = os.environ.get("MWX_LIB") or os.path.join(HERE, "libmwx.so")
 
 GGML_F16 = 1
 GGML_BF16 = 30
