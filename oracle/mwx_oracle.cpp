@@ -1483,7 +1483,9 @@ static int full(const Model& m, Params P, const float* samples, int n_samples, R
               cands.back().seq.sum_logprobs_all += tok.plog;
             }
           }
-          std::sort(cands.begin(), cands.end(), [](const BeamCand& a, const BeamCand& b) {
+          // (upstream std::sort leaves candidates tied on both keys in an
+          // unspecified order; stable keeps their draw order: DESIGN §2 D5)
+          std::stable_sort(cands.begin(), cands.end(), [](const BeamCand& a, const BeamCand& b) {
             if (a.seq.sum_logprobs_all != b.seq.sum_logprobs_all)
               return a.seq.sum_logprobs_all > b.seq.sum_logprobs_all;
             return a.decoder_idx < b.decoder_idx;

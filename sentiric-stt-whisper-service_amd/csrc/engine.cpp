@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -22,6 +23,7 @@
 #include <mutex>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "common.h"
@@ -986,9 +988,9 @@ struct Driver {
       S.vself.get(per * R);
       S.row_cap = R;
     }
-    S.pqkv.get((size_t)8 * R * 3 * d * 4);
-    S.pres.get((size_t)8 * R * d * 4);
-    S.pq.get((size_t)8 * R * d * 4);
+    S.pqkv.get((size_t)ks_d() * R * 3 * d * 4);
+    S.pres.get((size_t)ks_res() * R * d * 4);
+    S.pq.get((size_t)ks_d() * R * d * 4);
     S.xd.get((size_t)R * d * 4, true);
     // decode-GEMM A operands (fragment tiles), rows padded to the 64-row block
     const size_t R64 = (size_t)(R + 63) / 64 * 64;
@@ -1225,6 +1227,10 @@ struct Driver {
   // Rows in chunks of <= MWX_PREFILL_ROWS virtual rows (default 2048), each
   // row's positions padded to a multiple of the cross-attention group q
   // (min(8, prompt length)). Queued without a host synchronize.
+  // split-K slabs of the d-deep projections (QKV, out, cross Q, cross out)
+  // and of the residual-producing ones (out, cross out, FFN2: 4d deep)
+  int ks_d() const { return std::max(1, splitk_factor(d)); }
+  int ks_res() const { return std::max(ks_d(), splitk_factor(4 * d)); }
   struct PrefillRow {
     int row;                 // self-cache row
     int clip;                // cross slot
@@ -1259,9 +1265,11 @@ struct Driver {
     rw.hd = (T*)S.pf_h.get(m64 * d * sizeof(T), true);
     rw.od = (T*)S.pf_o.get(m64 * d * sizeof(T), true);
     rw.ffd = (T*)S.pf_ff.get(m64 * 4 * d * sizeof(T), true);
-    rw.Pqkv = (float*)S.pf_pqkv.get((size_t)8 * mcap * 3 * d * 4);
-    rw.Pres = (float*)S.pf_pres.get((size_t)8 * mcap * d * 4);
-    rw.Pq = (float*)S.pf_pq.get((size_t)8 * mcap * d * 4);
+    // (large-v3, 2048 virtual rows: slabs 5 x 31 + 8 x 10.5 + 5 x 10.5 MB, with
+    // the activations ~0.36 GB per state, held until mwx_free_state)
+    rw.Pqkv = (float*)S.pf_pqkv.get((size_t)ks_d() * mcap * 3 * d * 4);
+    rw.Pres = (float*)S.pf_pres.get((size_t)ks_res() * mcap * d * 4);
+    rw.Pq = (float*)S.pf_pq.get((size_t)ks_d() * mcap * d * 4);
     rw.kself = (_Float16*)S.kself.p;
     rw.vself = (_Float16*)S.vself.p;
     rw.prefill = true;

@@ -604,14 +604,21 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
     const void* __restrict__ kbase, const void* __restrict__ vbase,
     const uint8_t* __restrict__ kscale8, const uint8_t* __restrict__ vscale8,
     const int* __restrict__ kv_index, const int* __restrict__ active, int n, int cap, int R,
-    T* __restrict__ o, int H, float scale, unsigned long long* span = nullptr) {
+    T* __restrict__ o, int H, float scale, unsigned long long* span = nullptr, int gsz = 0,
+    int nsub = 1) {
   span_start(span);
   __shared__ float sc[NQ][DEC_MAX_KEYS];
   __shared__ float redf[4][NQ];
   __shared__ double redd[4][NQ];
   __shared__ float pv[4][64][9];
   __shared__ float sq[NQ][64];
-  const int g = blockIdx.y, h = blockIdx.x, row0 = g * NQ;
+  // nsub > 1: a group of gsz rows (one slot) is served by nsub workgroups of
+  // up to NQ queries each (part = blockIdx.y % nsub); every query's arithmetic
+  // is the same in any part, so results do not depend on the split
+  const int part = nsub > 1 ? (int)blockIdx.y % nsub : 0;
+  const int g = nsub > 1 ? (int)blockIdx.y / nsub : (int)blockIdx.y, h = blockIdx.x;
+  const int row0 = nsub > 1 ? g * gsz + part * NQ : g * NQ;
+  const int nq_eff = nsub > 1 ? min(NQ, gsz - part * NQ) : NQ;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int kg = lane >> 3, c = lane & 7;
   bool act[NQ];
@@ -621,7 +628,7 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
   const int slot = kv_index ? kv_index[row0] : row0;
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
-    act[q] = row0 + q < R && active[min(row0 + q, R - 1)];
+    act[q] = q < nq_eff && row0 + q < R && active[min(row0 + q, R - 1)];
     any |= act[q];
   }
   asm volatile("" ::"s"(slot));
@@ -1301,6 +1308,28 @@ bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float*
   // runtime count, so the grouped kernel keeps the runtime count by default
   static const bool nbc = getenv("MWX_XATTN_NBC") && atoi(getenv("MWX_XATTN_NBC")) == 1;
   const bool c6 = nbc && !kv8 && n_keys > 1280 && n_keys <= 1536;
+  // MWX_XATTN_SPLITQ=q (f16 caches, q < nq): each group's queries served by
+  // ceil(nq / q) workgroups of q queries (the K/V stream read once per part;
+  // the repeats meet in L2 / MALL)
+  static const int splitq = getenv("MWX_XATTN_SPLITQ") ? atoi(getenv("MWX_XATTN_SPLITQ")) : 0;
+  if (!kv8 && kv_index && splitq >= 2 && splitq <= 4 && splitq < nq) {
+    const int nsub = (nq + splitq - 1) / splitq;
+    const dim3 gs(H, ((R + nq - 1) / nq) * nsub);
+#define XS(N)                                                                                   \
+  case N:                                                                                       \
+    if (nt)                                                                                     \
+      dec_xattn_kernel<T, N, false, true><<<gs, 256, 0, st>>>(P, KS, pcols, bias, kbase, vbase, \
+          kscale8, vscale8, kv_index, active, n_keys, cap, R, o, H, scale, span, nq, nsub);     \
+    else                                                                                        \
+      dec_xattn_kernel<T, N, false, false><<<gs, 256, 0, st>>>(P, KS, pcols, bias, kbase, vbase,\
+          kscale8, vscale8, kv_index, active, n_keys, cap, R, o, H, scale, span, nq, nsub);     \
+    return true;
+    switch (splitq) {
+      XS(2) XS(3) XS(4)
+      default: break;
+    }
+#undef XS
+  }
 #define XL(N, K8, NT)                                                                          \
   do {                                                                                         \
     if (c6)                                                                                    \

@@ -590,12 +590,58 @@ void logits_process(float* logits, const float* static_mask, const RowCtl* ctl, 
   lp_pick_kernel<<<R, 64, 0, st>>>(logits, ws.flt, ws.parts, ws.res, ctl, out, C);
 }
 
-// Run-ahead greedy decoding: applies the token loop's per-row rules to the
-// step just run (whisper.cpp v1.8.2 whisper_full_with_state, the greedy
-// branch of its decoder loop; host restatement driver.inc, same order of
-// tests) and writes the next step's inputs. One workgroup; every row is
-// independent. The step's token records and the inputs chosen for the next
-// step go straight to the pinned host ring slot `*run_step % nslot`.
+// The token loop's per-row rules on the token a row generated this step
+// (whisper.cpp v1.8.2 whisper_full_with_state, its decoder loop after
+// sampling; host restatement driver.inc process_step, same order of tests).
+__device__ __forceinline__ void token_rules(RowRun& w, int id, const RunConst& C) {
+  const int i = w.ntok;
+  w.penult_id = w.last_id;
+  w.last_id = id;
+  w.ntok = i + 1;
+  bool stop = false;
+  if (id > C.beg) {
+    const int sd_new = 2 * (id - C.beg);
+    if (w.has_ts && w.seek_delta > sd_new && w.result_len < i) {
+      stop = true;  // (failed)
+    } else {
+      w.seek_delta = sd_new;
+      w.result_len = i + 1;
+      w.has_ts = 1;
+    }
+  }
+  if (!stop) {
+    if (id == C.eot || (C.max_tokens > 0 && i >= C.max_tokens) ||
+        (w.has_ts && w.seek + w.seek_delta + C.delta_min >= w.seek_end))
+      stop = true;
+    else if (i == C.n_max - 1)
+      stop = true;
+  }
+  if (stop) w.stopped = 1;
+}
+
+// The next step's inputs of a row (driver.inc fill_inputs).
+__device__ __forceinline__ RowCtl next_inputs(const RowRun& w, const RunConst& C,
+                                              const int* prompt_row, int& tok) {
+  tok = w.fed < w.p_len ? prompt_row[w.fed] : (w.ntok > 0 ? w.last_id : 0);
+  RowCtl n;
+  n.active = w.stopped ? 0 : 1;
+  n.sample = (!w.stopped && w.fed >= w.p_len - 1) ? 1 : 0;
+  n.is_initial = w.ntok == 0 ? 1 : 0;
+  n.last_ts = (w.ntok > 0 && w.last_id >= C.beg) ? 1 : 0;
+  n.penult_ts = (w.ntok < 2 || w.penult_id >= C.beg) ? 1 : 0;
+  n.has_ts = w.has_ts;
+  n.seek_delta = w.seek_delta;
+  n.want_probs = C.want_probs;
+  n.temperature = C.temperature;
+  n.want_nosp = (n.sample && n.is_initial) ? 1 : 0;
+  n.pad[0] = n.pad[1] = 0;
+  return n;
+}
+
+// Run-ahead greedy decoding: applies the token rules to the step just run and
+// writes the next step's inputs. One workgroup; every row is independent. The
+// step's token records and the inputs chosen for the next step go straight to
+// the pinned host ring slot `*run_step % nslot`.
 __global__ __launch_bounds__(256) void row_advance_kernel(RowRun* __restrict__ run,
                                                           int* __restrict__ run_step,
                                                           const int* __restrict__ prompt,
@@ -611,48 +657,11 @@ __global__ __launch_bounds__(256) void row_advance_kernel(RowRun* __restrict__ r
     const RowCtl k = ctl[r];
     const TokOut t = out[r];
     if (!w.stopped) {
-      if (k.sample) {
-        const int id = t.id;
-        const int i = w.ntok;
-        w.penult_id = w.last_id;
-        w.last_id = id;
-        w.ntok = i + 1;
-        bool stop = false;
-        if (id > C.beg) {
-          const int sd_new = 2 * (id - C.beg);
-          if (w.has_ts && w.seek_delta > sd_new && w.result_len < i) {
-            stop = true;  // (failed)
-          } else {
-            w.seek_delta = sd_new;
-            w.result_len = i + 1;
-            w.has_ts = 1;
-          }
-        }
-        if (!stop) {
-          if (id == C.eot || (C.max_tokens > 0 && i >= C.max_tokens) ||
-              (w.has_ts && w.seek + w.seek_delta + C.delta_min >= w.seek_end))
-            stop = true;
-          else if (i == C.n_max - 1)
-            stop = true;
-        }
-        if (stop) w.stopped = 1;
-      }
+      if (k.sample) token_rules(w, t.id, C);
       if (!w.stopped) w.fed++;
     }
-    const int tok = w.fed < w.p_len ? prompt[(long)r * C.prompt_stride + w.fed]
-                                    : (w.ntok > 0 ? w.last_id : 0);
-    RowCtl n;
-    n.active = w.stopped ? 0 : 1;
-    n.sample = (!w.stopped && w.fed >= w.p_len - 1) ? 1 : 0;
-    n.is_initial = w.ntok == 0 ? 1 : 0;
-    n.last_ts = (w.ntok > 0 && w.last_id >= C.beg) ? 1 : 0;
-    n.penult_ts = (w.ntok < 2 || w.penult_id >= C.beg) ? 1 : 0;
-    n.has_ts = w.has_ts;
-    n.seek_delta = w.seek_delta;
-    n.want_probs = 0;
-    n.temperature = C.temperature;
-    n.want_nosp = (n.sample && n.is_initial) ? 1 : 0;
-    n.pad[0] = n.pad[1] = 0;
+    int tok;
+    const RowCtl n = next_inputs(w, C, prompt + (long)r * C.prompt_stride, tok);
     si[r] = tok;
     si[R + r] = w.fed;
     si[2 * R + r] = n.active;
@@ -671,6 +680,182 @@ __global__ __launch_bounds__(256) void row_advance_kernel(RowRun* __restrict__ r
   if (threadIdx.x == 0) *run_step = step + 1;
 }
 
+// Run-ahead beam search, one workgroup per clip (its n decoders are rows
+// r0 .. r0+n-1, stepping in lockstep). The beam step of driver.inc beam_step
+// (whisper.cpp v1.8.2 WHISPER_SAMPLING_BEAM_SEARCH):
+//  * candidates: beam_size draws per live decoder, sum = decoder's
+//    sum_logprobs_all + plog;
+//  * ranking: by sum (desc), then decoder, then draw index — each candidate's
+//    rank counted in parallel against all others (a total order: the same
+//    permutation std::stable_sort gives the host);
+//  * hand-over: decoders in order take candidates in rank order, skipping the
+//    run of candidates equal to the one just taken (from the second token on).
+//    Equal token sequences are tracked as classes (cls): two candidates are
+//    equal iff their parents' classes and their tokens are equal, and a
+//    decoder's new class is the first decoder holding an equal sequence;
+//  * a decoder taking another decoder's candidate takes its state and its KV
+//    position map (the parent's maps as they were before the step).
+// Then the token rules and the next step's inputs as row_advance_kernel, and
+// the next step's uniforms copied from the host-filled ring.
+constexpr int BA_T = 256;
+constexpr int BA_MAXN = 16;
+__global__ __launch_bounds__(BA_T) void beam_advance_kernel(RowRun* __restrict__ run,
+                                                            int* __restrict__ run_step,
+                                                            const int* __restrict__ prompt,
+                                                            int* __restrict__ si,
+                                                            RowCtl* __restrict__ ctl,
+                                                            const TokOut* __restrict__ out,
+                                                            RunReport* __restrict__ rep, RunConst C,
+                                                            BeamRun B) {
+  extern __shared__ int smap[];  // [n][Tctx]: maps of the decoders others take over
+  __shared__ RowRun sw[BA_MAXN];
+  __shared__ int s_smp[BA_MAXN], s_src[BA_MAXN], s_tok[BA_MAXN], s_need[BA_MAXN],
+      s_own[BA_MAXN];
+  __shared__ double s_csum[BA_MAXN];
+  __shared__ double c_sum[BA_MAXN * 16];
+  __shared__ int c_id[BA_MAXN * 16], c_ord[BA_MAXN * 16], c_eq[BA_MAXN * 16];
+  const int n = B.n, KD = B.KD, tid = threadIdx.x;
+  const int r0 = blockIdx.x * n, R = C.R;
+  const int step = run_step[blockIdx.x];
+  if (tid < n) {
+    sw[tid] = run[r0 + tid];
+    s_smp[tid] = ctl[r0 + tid].sample;
+    s_src[tid] = tid;
+    s_need[tid] = 0;
+  }
+  __syncthreads();
+  int live = -1, nlive = 0;
+  for (int j = 0; j < n; ++j) {
+    if (sw[j].stopped) continue;
+    ++nlive;
+    if (live < 0 && s_smp[j]) live = j;
+  }
+  if (live >= 0) {
+    const int nc = n * KD;
+    for (int c = tid; c < nc; c += BA_T) {
+      const Draw dr = B.draws[(long)(r0 + c / KD) * KD + c % KD];
+      c_sum[c] = sw[c / KD].sum + (double)dr.plog;
+      c_id[c] = dr.id;
+    }
+    __syncthreads();
+    for (int c = tid; c < nc; c += BA_T) {
+      if (sw[c / KD].stopped) continue;
+      const double s = c_sum[c];
+      int rank = 0;
+      for (int u = 0; u < nc; ++u) {
+        if (sw[u / KD].stopped) continue;
+        const double t = c_sum[u];
+        rank += (t > s || (t == s && u < c)) ? 1 : 0;
+      }
+      c_ord[rank] = c;
+    }
+    __syncthreads();
+    const int ncand = nlive * KD;
+    for (int p = tid; p < ncand; p += BA_T) {
+      int eq = 0;
+      if (p > 0) {
+        const int a = c_ord[p], b = c_ord[p - 1];
+        eq = (c_id[a] == c_id[b] && sw[a / KD].cls == sw[b / KD].cls) ? 1 : 0;
+      }
+      c_eq[p] = eq;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const int i_step = sw[live].ntok;
+      int cur = 0;
+      for (int j = 0; j < n; ++j) {
+        if (sw[j].stopped) continue;
+        if (cur >= ncand) cur = 0;
+        const int c = c_ord[cur++];
+        while (cur < ncand && c_eq[cur] && i_step > 0) ++cur;
+        s_src[j] = c / KD;
+        s_tok[j] = c_id[c];
+        s_csum[j] = c_sum[c];
+        if (c / KD != j) s_need[c / KD] = 1;
+      }
+    }
+    __syncthreads();
+  }
+  // the decoders' new states (from their parents' pre-step states)
+  RowRun w;
+  if (tid < n) {
+    w = sw[tid];
+    if (!w.stopped) {
+      if (live >= 0) {
+        const RowRun& p = sw[s_src[tid]];
+        int cls = tid;  // the first decoder holding an equal sequence
+        for (int j = 0; j < tid; ++j)
+          if (!sw[j].stopped && sw[s_src[j]].cls == p.cls && s_tok[j] == s_tok[tid]) {
+            cls = j;
+            break;
+          }
+        w.ntok = p.ntok;
+        w.last_id = p.last_id;
+        w.penult_id = p.penult_id;
+        w.has_ts = p.has_ts;
+        w.seek_delta = p.seek_delta;
+        w.result_len = p.result_len;
+        w.cls = cls;
+        w.sum = s_csum[tid];
+        token_rules(w, s_tok[tid], C);
+      }
+      // (w.fed: the positions 0..fed of this window hold KV after this step)
+    }
+  }
+  // KV position maps: snapshot the taken-over decoders' maps, then rewrite
+  // the takers' (kvmap[dst][0..npos) = where src reads them, kvown = npos)
+  const int npos = live >= 0 ? sw[live].fed + 1 : 0;
+  if (live >= 0) {
+    if (tid < n && s_need[tid]) s_own[tid] = B.kvown[r0 + tid];
+    __syncthreads();
+    for (int j = 0; j < n; ++j) {
+      if (!s_need[j]) continue;
+      const int lim = min(s_own[j], npos);
+      for (int p = tid; p < lim; p += BA_T) smap[j * B.Tctx + p] = B.kvmap[(long)(r0 + j) * B.Tctx + p];
+    }
+    __syncthreads();
+    for (int j = 0; j < n; ++j) {
+      const int src = s_src[j];
+      if (src == j || sw[j].stopped) continue;
+      int* dm = B.kvmap + (long)(r0 + j) * B.Tctx;
+      for (int p = tid; p < npos; p += BA_T) dm[p] = p < s_own[src] ? smap[src * B.Tctx + p] : r0 + src;
+      if (tid == 0) B.kvown[r0 + j] = npos;
+    }
+  }
+  if (tid < n) {
+    const int r = r0 + tid;
+    if (!w.stopped) w.fed++;
+    int tok;
+    const RowCtl nx = next_inputs(w, C, prompt + (long)r * C.prompt_stride, tok);
+    const int nd = (!w.stopped && nx.sample) ? KD : 0;
+    for (int k = 0; k < nd; ++k) B.du[(long)r * KD + k] = B.uring[(long)r * B.ring_n + (w.used + k) % B.ring_n];
+    w.used += nd;
+    B.dnd[r] = nd;
+    si[r] = tok;
+    si[R + r] = w.fed;
+    si[2 * R + r] = nx.active;
+    ctl[r] = nx;
+    run[r] = w;
+    const int sl = step % C.nslot;
+    RunReport o;
+    o.out = out[r];
+    o.tok = tok;
+    o.pos = w.fed;
+    o.act = nx.active;
+    o.pad = 0;
+    o.next = nx;
+    rep[(long)sl * R + r] = o;
+    BeamReport b;
+    b.src = r0 + s_src[tid];
+    b.nd = nd;
+    b.pad[0] = b.pad[1] = 0;
+    B.brep[(long)sl * R + r] = b;
+    for (int k = 0; k < KD; ++k)
+      B.drep[((long)sl * R + r) * KD + k] = B.draws[(long)r * KD + k];
+    if (tid == 0) run_step[blockIdx.x] = step + 1;
+  }
+}
+
 // Event-bracket calibration (bench.py roofline): an empty kernel launched
 // between two timing events in the instrumented decode-step graph, so the
 // event nodes' own cost can be measured and removed from the kernel brackets.
@@ -680,6 +865,14 @@ void launch_perf_empty(hipStream_t st) { perf_empty_kernel<<<1, 64, 0, st>>>(); 
 void row_advance(RowRun* run, int* run_step, const int* prompt, int* stepin, RowCtl* ctl,
                  const TokOut* out, RunReport* rep, const RunConst& C, hipStream_t st) {
   row_advance_kernel<<<1, 256, 0, st>>>(run, run_step, prompt, stepin, ctl, out, rep, C);
+}
+
+void beam_advance(RowRun* run, int* run_step, const int* prompt, int* stepin, RowCtl* ctl,
+                  const TokOut* out, RunReport* rep, const RunConst& C, const BeamRun& B,
+                  hipStream_t st) {
+  const size_t lds = (size_t)B.n * B.Tctx * 4;
+  beam_advance_kernel<<<C.R / B.n, BA_T, lds, st>>>(run, run_step, prompt, stepin, ctl, out, rep,
+                                                   C, B);
 }
 
 

@@ -256,12 +256,16 @@ struct RowRun {
   int result_len;
   int stopped;
   int seek, seek_end;  // the clip's window position and end (centiseconds)
+  int cls;          // beam: token-sequence class (equal sequences <=> equal cls)
+  int used;         // beam: uniforms of the row's RNG consumed so far
   int pad;
+  double sum;       // beam: sum_logprobs_all
 };
 struct RunConst {
   int beg, eot, max_tokens, n_max, delta_min, R, nslot, prompt_stride;
   float temperature;
-  int pad[3];
+  int want_probs;
+  int pad[2];
 };
 // what the host reads back per row and step (written straight into pinned
 // host memory by the advance kernel: no copy launch per step)
@@ -274,6 +278,35 @@ struct RunReport {
 void launch_perf_empty(hipStream_t st);
 void row_advance(RowRun* run, int* run_step, const int* prompt, int* stepin, RowCtl* ctl,
                  const TokOut* out, RunReport* rep, const RunConst& C, hipStream_t st);
+
+struct Draw;
+// Run-ahead beam search: per clip (n decoders = rows r0 .. r0+n-1), the
+// beam step of whisper.cpp's decoder loop on the device (driver.inc
+// beam_step: candidate ranking, dedup, hand-over of state and KV maps), then
+// the token rules as row_advance, the next step's inputs and its uniforms
+// (from the host-filled ring uring[R][ring_n], the rows' RNG streams).
+struct BeamReport {
+  int src;      // decoder (row) whose candidate this row took (itself: no move)
+  int nd;       // uniforms the row's next step draws
+  int pad[2];
+};
+struct BeamRun {
+  const Draw* draws;  // [R][KD] this step's draws
+  int KD;             // = beam size
+  int n;              // decoders per clip
+  double* du;         // [R][KD] next step's uniforms
+  int* dnd;           // [R]
+  const double* uring;  // [R][ring_n] host-filled
+  int ring_n;
+  int* kvmap;         // [R][Tctx]
+  int* kvown;         // [R]
+  int Tctx;
+  BeamReport* brep;   // [nslot][R]
+  Draw* drep;         // [nslot][R][KD] the step's draws, for the host replay
+};
+void beam_advance(RowRun* run, int* run_step, const int* prompt, int* stepin, RowCtl* ctl,
+                  const TokOut* out, RunReport* rep, const RunConst& C, const BeamRun& B,
+                  hipStream_t st);
 
 struct LogitsConst {
   int n_vocab;

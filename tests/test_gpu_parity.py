@@ -759,3 +759,30 @@ def test_runahead_decode_equals_synchronous_loop(make_model, max_tokens, inc):
         res.append(json.loads(r.stdout.strip().splitlines()[-1]))
     assert res[0] == res[1]
     assert sum(len(s[3]) for c in res[0] for s in c) > 40
+
+
+@pytest.mark.parametrize("temperature_inc", [0.0, 0.2])
+def test_beam_runahead_equals_host_loop(rich, temperature_inc, monkeypatch):
+    """Beam search run ahead on the device (beam_advance_kernel: ranking,
+    dedup, decoder hand-over and KV maps, the next step's inputs and uniforms)
+    == the host loop (MWX_NO_RUNAHEAD: beam_step on the host, one round trip
+    per step): every clip's token records bit for bit, 4 clips in one batch.
+    With fallback, the sampled decoders after a beam pass draw from RNG
+    streams the run-ahead consumed from its uniform ring."""
+    ctx, _, _ = rich
+    p = beam_params(ctx, temperature_inc)
+    pcms = [pcm_clip(40 + k, 10.0 + 7 * k) for k in range(4)]
+
+    def run():
+        base = len(ctx.states)
+        for i in range(4):
+            ctx.state(base + i)
+        assert ctx.full_batch_states(pcms, p, range(base, base + 4)) == 0
+        return [ctx.token_records(base + i) for i in range(4)]
+
+    ra = run()
+    monkeypatch.setenv("MWX_NO_RUNAHEAD", "1")
+    host = run()
+    print("tokens per clip:", [len(x) for x in ra])
+    assert sum(len(x) for x in ra) > 20
+    assert ra == host
