@@ -68,11 +68,6 @@ for s in "$@"; do
     b5onenra) run b5onenra 500 env MWX_NO_RUNAHEAD=1 python -u bench.py --beam 5 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
     beamra) run beamra 400 python -u -m pytest tests/test_gpu_parity.py -k "runahead" -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
     tsfull) run tsfull 600 python -u -m pytest tests/test_gpu_fulldepth.py -k "bench_workload" -m gpu -v -s -rf --timeout 600 --timeout-method thread ;;
-    c2s256) run c2s256 300 env MWX_XATTN_SPLIT=256 python -u bench.py --arch base --wtype f16 --clips 1 --lanes 1 --steps 20 --warmup 3 --no-cpu-baseline ;;
-    c2s128) run c2s128 300 env MWX_XATTN_SPLIT=128 python -u bench.py --arch base --wtype f16 --clips 1 --lanes 1 --steps 20 --warmup 3 --no-cpu-baseline ;;
-    bench1s256) run bench1s256 400 env MWX_XATTN_SPLIT=256 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
-    bench1s128) run bench1s128 400 env MWX_XATTN_SPLIT=128 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
-    splittests) run splittests 1150 env MWX_XATTN_SPLIT=256 python -u -m pytest tests -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
     b5one) run b5one 500 python -u bench.py --beam 5 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
     bench1g16) run bench1g16 400 env MWX_GEMM_GROUP=16 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
     bench1g32) run bench1g32 400 env MWX_GEMM_GROUP=32 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;

@@ -207,7 +207,6 @@ struct State {
   // batched prompt prefill: virtual-row inputs [tok|pos|act|xidx|crow] and the
   // layer stack's activations / slabs for up to MWX_PREFILL_ROWS virtual rows
   DBuf pf_in, pf_x, pf_h, pf_o, pf_ff, pf_pqkv, pf_pres, pf_pq;
-  DBuf xpart;  // key-chunk cross-attention partials (MWX_XATTN_SPLIT)
   // the prefill's host-side inputs of all chunks: read by its stream-ordered
   // uploads, rewritten only by the next prefill (after that window's step
   // synchronizes)
@@ -1009,8 +1008,6 @@ struct Driver {
     HIPC(hipMemsetAsync(S.kvown.p, 0, (size_t)R * 4, st));
     S.ctl.get((size_t)R * sizeof(RowCtl));
     S.tokout.get((size_t)R * sizeof(TokOut));
-    // (allocated before any step graph is captured)
-    if (xattn_split_keys()) S.xpart.get(xattn_split_scratch(R, H, hp.n_audio_ctx));
   }
 
   // beam search: rows take over other rows' self-attention histories
@@ -1163,15 +1160,7 @@ struct Driver {
     // kernel for any group size
     const int nq = std::max(1, rw.xgroup);  // (prefill: Driver::prefill's q)
     unsigned long long* sp = rw.prefill ? nullptr : span_slot(S, "dec_attn_cross", s);
-    if (!C.kv8 && xattn_split_keys()) {
-      // key-chunk split, every row alike (the beam / prefill groups too)
-      void* xs = S.xpart.get(xattn_split_scratch(n, H, hp.n_audio_ctx));
-      dec_cross_attention_split<T>(rw.Pq, c.k3, d, W.cq_b, 1.0f,
-                                   (const _Float16*)S.cross_k.p + l * layer_cross,
-                                   (const _Float16*)S.cross_v.p + l * layer_cross, rw.xidx,
-                                   rw.act, hp.n_audio_ctx, hp.n_audio_ctx, rw.od, n, H, kqs, xs, s,
-                                   sp);
-    } else if (C.kv8) {
+    if (C.kv8) {
       if (!dec_cross_attention_grouped<T>(
               rw.Pq, c.k3, d, W.cq_b, (const uint8_t*)S.cross_k.p + l * layer_cross,
               (const uint8_t*)S.cross_v.p + l * layer_cross, rw.xidx, rw.act, hp.n_audio_ctx,

@@ -1401,194 +1401,6 @@ __global__ __launch_bounds__(128) void kv_append_kernel(const float* __restrict_
     vbase[dst] = f16r(acc + bias[col]);
 }
 
-// ---------------------------------------------------------------------------
-// Cross-attention with the encoder frames split into fixed chunks of 32*UB
-// keys (MWX_XATTN_SPLIT, every batch size alike): one workgroup per (row,
-// head, chunk) forms the query (as dec_attn_kernel), scores its chunk, and
-// writes the chunk's max m_c, sum l_c = sum exp(s - m_c) (double) and partial
-// P.V acc_c = sum f16(exp(s - m_c)) v (f32); a combine kernel merges the
-// chunks in index order: M = max m_c, w_c = exp(m_c - M),
-// o = (sum w_c acc_c) / (sum w_c l_c). A row's arithmetic depends only on the
-// fixed chunking, so batch == single and prefill == stepwise hold; a one-row
-// launch spreads over H x chunks workgroups instead of H.
-// ---------------------------------------------------------------------------
-struct XPart {
-  float acc[64];
-  float m, pad;
-  double l;
-};
-template <typename T, int UB, bool NTL>
-__global__ __launch_bounds__(256) void dec_xattn_chunk_kernel(
-    const float* __restrict__ P, int KS, int pcols, const float* __restrict__ bias, float qscale,
-    const _Float16* __restrict__ kbase, const _Float16* __restrict__ vbase,
-    const int* __restrict__ kv_index, const int* __restrict__ active, int n, int cap, int R, int H,
-    float scale, XPart* __restrict__ part, int nch, unsigned long long* span) {
-  constexpr int CK = 32 * UB;  // keys per chunk (4 waves x 8 lane groups x UB rows)
-  __shared__ float sc[CK];
-  __shared__ float redf[4];
-  __shared__ double redd[4];
-  __shared__ float pv[4][64][9];
-  __shared__ float sq[64];
-  span_start(span);
-  const int L = blockIdx.x;
-  const int ch = L % nch, rh = L / nch, h = rh % H, row = rh / H;
-  const int act_r = active[row];
-  const int slot = kv_index ? kv_index[row] : row;
-  asm volatile("" ::"s"(act_r), "s"(slot));
-  if (!act_r) {
-    span_end(span);
-    return;
-  }
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int kg = lane >> 3, c = lane & 7;
-  const _Float16* K = kbase + (((long)slot * H + h) * cap) * 64;
-  const _Float16* V = vbase + (((long)slot * H + h) * cap) * 64;
-  const int j0 = ch * CK, jmax = n - 1;
-  // the query's slab loads first, then the chunk's K and V rows (all in flight)
-  const long pstride = (long)R * pcols;
-  float pk[8];
-  float bcol = 0.0f;
-  if (tid < 64) {
-    const float* pp = P + (long)row * pcols + h * 64 + tid;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) pk[k] = pp[min(k, KS - 1) * pstride];
-    bcol = bias[h * 64 + tid];
-  }
-  f16x8 ka[UB], va[UB];
-#pragma unroll
-  for (int u = 0; u < UB; ++u) {
-    const int j = min(j0 + wid * (8 * UB) + u * 8 + kg, jmax);
-    ka[u] = ld_stream<NTL>(reinterpret_cast<const f16x8*>(K + (long)j * 64 + c * 8));
-  }
-#pragma unroll
-  for (int u = 0; u < UB; ++u) {
-    const int j = min(j0 + wid * (8 * UB) + u * 8 + kg, jmax);
-    va[u] = ld_stream<NTL>(reinterpret_cast<const f16x8*>(V + (long)j * 64 + c * 8));
-  }
-  if (tid < 64) {
-    float acc = pk[0];
-#pragma unroll
-    for (int k = 1; k < 8; ++k) acc += k < KS ? pk[k] : 0.0f;
-    sq[tid] = (float)f16r((acc + bcol) * qscale);
-  }
-  __syncthreads();
-  h2 qh[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) qh[e] = h2{(_Float16)sq[c * 8 + 2 * e], (_Float16)sq[c * 8 + 2 * e + 1]};
-#pragma unroll
-  for (int u = 0; u < UB; ++u) {
-    const int jl = wid * (8 * UB) + u * 8 + kg;
-    float d = dot8(qh, ka[u]);
-    d = dpp_sum8(d);
-    if (c == 0) sc[jl] = d * scale;
-  }
-  __syncthreads();
-  const int nk = min(CK, n - j0);
-  float mx = -INFINITY;
-  for (int j = tid; j < nk; j += 256) mx = fmaxf(mx, sc[j]);
-  mx = block_max_256(mx, redf);
-  double sum = 0.0;
-  for (int j = tid; j < CK; j += 256) {
-    const float e = j < nk ? expf(sc[j] - mx) : 0.0f;
-    sc[j] = (float)f16r(e);
-    sum += (double)e;
-  }
-  sum = block_sum_256d(sum, redd);  // (its barriers also publish sc)
-  float acc[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) acc[e] = 0.0f;
-#pragma unroll
-  for (int u = 0; u < UB; u += 2) {
-    h2 ph;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) ph[t] = (_Float16)sc[wid * (8 * UB) + (u + t) * 8 + kg];
-#pragma unroll
-    for (int e = 0; e < 8; ++e)
-      acc[e] = __builtin_amdgcn_fdot2(ph, h2{va[u][e], va[u + 1][e]}, acc[e], false);
-  }
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    acc[e] += __shfl_xor(acc[e], 8, 64);
-    acc[e] += __shfl_xor(acc[e], 16, 64);
-    acc[e] += __shfl_xor(acc[e], 32, 64);
-  }
-  if (kg == 0) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) pv[wid][c][e] = acc[e];
-  }
-  __syncthreads();
-  XPart* dst = part + L;
-  if (tid < 64) {
-    const int cc = tid >> 3, e = tid & 7;
-    dst->acc[tid] = (pv[0][cc][e] + pv[1][cc][e]) + (pv[2][cc][e] + pv[3][cc][e]);
-  } else if (tid == 64) {
-    dst->m = mx;
-    dst->pad = 0.0f;
-    dst->l = sum;
-  }
-  span_end(span);
-}
-
-template <typename T>
-__global__ __launch_bounds__(64) void dec_xattn_combine_kernel(const XPart* __restrict__ part,
-                                                               const int* __restrict__ active,
-                                                               int nch, int H, T* __restrict__ o) {
-  const int rh = blockIdx.x, row = rh / H, h = rh % H, e = threadIdx.x;
-  if (!active[row]) return;
-  const XPart* pp = part + (long)rh * nch;
-  float M = -INFINITY;
-  for (int c = 0; c < nch; ++c) M = fmaxf(M, pp[c].m);
-  double Ls = 0.0;
-  float acc = 0.0f;
-  for (int c = 0; c < nch; ++c) {
-    const float w = expf(pp[c].m - M);
-    Ls += (double)w * pp[c].l;
-    acc += w * pp[c].acc[e];
-  }
-  o[pack_index(row, h * 64 + e, H * 64)] = to_t<T>(acc * (float)(1.0 / Ls));
-}
-
-int xattn_split_keys() {
-  static const int k = getenv("MWX_XATTN_SPLIT") ? atoi(getenv("MWX_XATTN_SPLIT")) : 0;
-  return (k == 128 || k == 256) ? k : 0;
-}
-size_t xattn_split_scratch(int R, int H, int n) {
-  const int ck = xattn_split_keys();
-  return ck ? (size_t)R * H * ((n + ck - 1) / ck) * sizeof(XPart) : 0;
-}
-template <typename T>
-void dec_cross_attention_split(const float* P, int KS, int pcols, const float* bias, float qscale,
-                               const _Float16* kbase, const _Float16* vbase, const int* kv_index,
-                               const int* active, int n, int cap, T* o, int R, int H, float scale,
-                               void* scratch, hipStream_t st, unsigned long long* span) {
-  const int ck = xattn_split_keys();
-  const int nch = (n + ck - 1) / ck;
-  // (non-temporal K/V stream unless the launch's cross K/V is small: as
-  // dec_attention)
-  const bool nt = (long)R * H * n * 256 > (4l << 20);
-  XPart* part = reinterpret_cast<XPart*>(scratch);
-  const dim3 g(R * H * nch);
-#define XC(UB, NT)                                                                              \
-  dec_xattn_chunk_kernel<T, UB, NT><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kbase, vbase, \
-                                                      kv_index, active, n, cap, R, H, scale,   \
-                                                      part, nch, span)
-  if (ck == 256) {
-    if (nt) XC(8, true); else XC(8, false);
-  } else {
-    if (nt) XC(4, true); else XC(4, false);
-  }
-#undef XC
-  dec_xattn_combine_kernel<T><<<R * H, 64, 0, st>>>(part, active, nch, H, o);
-}
-template void dec_cross_attention_split<_Float16>(const float*, int, int, const float*, float,
-                                                  const _Float16*, const _Float16*, const int*,
-                                                  const int*, int, int, _Float16*, int, int, float,
-                                                  void*, hipStream_t, unsigned long long*);
-template void dec_cross_attention_split<__bf16>(const float*, int, int, const float*, float,
-                                                const _Float16*, const _Float16*, const int*,
-                                                const int*, int, int, __bf16*, int, int, float,
-                                                void*, hipStream_t, unsigned long long*);
-
 template <typename T>
 void kv_append(const float* P, int KS, int pcols, const float* bias, float kscale,
                _Float16* kbase, _Float16* vbase, const int* crow, const int* pos,

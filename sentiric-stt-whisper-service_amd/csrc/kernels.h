@@ -191,17 +191,6 @@ void dec_attention(const float* P, int KS, int pcols, const float* bias, float q
                    const int* own_from = nullptr, int map_row0 = 0, int nq = 1,
                    int write_new = 1, unsigned long long* span = nullptr);
 
-// Cross-attention over fixed key chunks + a combine launch (k_attn.hip;
-// MWX_XATTN_SPLIT = 128 / 256 keys per chunk, 0: off). scratch holds
-// xattn_split_scratch(R, H, n) bytes.
-int xattn_split_keys();
-size_t xattn_split_scratch(int R, int H, int n);
-template <typename T>
-void dec_cross_attention_split(const float* P, int KS, int pcols, const float* bias, float qscale,
-                               const _Float16* kbase, const _Float16* vbase, const int* kv_index,
-                               const int* active, int n, int cap, T* o, int R, int H, float scale,
-                               void* scratch, hipStream_t st, unsigned long long* span = nullptr);
-
 // Prompt prefill: K / V of every row (reduced from the QKV slabs exactly as
 // dec_attention's self kernel reduces its own position) appended to cache row
 // crow[row] (nullptr: row) at position pos[row].
