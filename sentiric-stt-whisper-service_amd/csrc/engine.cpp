@@ -1265,8 +1265,8 @@ struct Driver {
     rw.hd = (T*)S.pf_h.get(m64 * d * sizeof(T), true);
     rw.od = (T*)S.pf_o.get(m64 * d * sizeof(T), true);
     rw.ffd = (T*)S.pf_ff.get(m64 * 4 * d * sizeof(T), true);
-    // (large-v3, 2048 virtual rows: slabs 5 x 31 + 8 x 10.5 + 5 x 10.5 MB, with
-    // the activations ~0.36 GB per state, held until mwx_free_state)
+    // (large-v3, 2048 virtual rows: slabs 5 x 31.5 + 8 x 10.5 + 5 x 10.5 MB,
+    // with the activations ~0.33 GB per state, held until mwx_free_state)
     rw.Pqkv = (float*)S.pf_pqkv.get((size_t)ks_d() * mcap * 3 * d * 4);
     rw.Pres = (float*)S.pf_pres.get((size_t)ks_res() * mcap * d * 4);
     rw.Pq = (float*)S.pf_pq.get((size_t)ks_d() * mcap * d * 4);
