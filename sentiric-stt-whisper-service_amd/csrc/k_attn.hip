@@ -32,14 +32,25 @@ template <typename T>
 __global__ __launch_bounds__(256) void enc_attn_kernel(const _Float16* __restrict__ q,
                                                        const _Float16* __restrict__ k,
                                                        const _Float16* __restrict__ vt, T* __restrict__ o,
-                                                       int H, int L, int Lp, float scale_log2) {
+                                                       int H, int L, int Lp, float scale_log2,
+                                                       int nqb) {
   __shared__ __attribute__((aligned(16))) _Float16 ks[2][64 * 64];
   __shared__ __attribute__((aligned(16))) _Float16 vs[2][64 * VSTR];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int g = lane >> 4, c16 = lane & 15;
-  const int bh = blockIdx.y;
+  // 1-D grid, XCD-aware order: workgroups are placed round-robin over the 8
+  // XCDs (id % 8); each XCD gets a contiguous range of (clip, head, query
+  // block) ids, so the nqb query blocks of a (clip, head) run on one XCD and
+  // its K / V^T (384 KB at large-v3) are fetched from HBM into that XCD's L2
+  // once instead of once per XCD
+  int wgid = blockIdx.x;
+  {
+    const int nwg = gridDim.x, xcd = wgid % 8, qq = nwg / 8, rr = nwg % 8;
+    wgid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + wgid / 8;
+  }
+  const int bh = wgid / nqb;
   const int b = bh / H, h = bh - b * H;
-  const int q0 = blockIdx.x * 128 + wid * 32;
+  const int q0 = (wgid - bh * nqb) * 128 + wid * 32;
   const _Float16* Q = q + (long)bh * L * 64;
   const _Float16* Kh = k + (long)bh * L * 64;
   const _Float16* VT = vt + (long)bh * 64 * Lp;
@@ -223,8 +234,9 @@ template <typename T>
 void enc_attention(const _Float16* q, const _Float16* k, const _Float16* vt, T* o, int B, int H,
                    int L, float scale, hipStream_t st) {
   const int Lp = (L + 7) & ~7;
-  dim3 g((L + 127) / 128, B * H);
-  enc_attn_kernel<T><<<g, 256, 0, st>>>(q, k, vt, o, H, L, Lp, scale * 1.4426950408889634f);
+  const int nqb = (L + 127) / 128;
+  enc_attn_kernel<T><<<nqb * B * H, 256, 0, st>>>(q, k, vt, o, H, L, Lp,
+                                                  scale * 1.4426950408889634f, nqb);
 }
 
 // ---------------------------------------------------------------------------
