@@ -11,7 +11,6 @@
 #   c2nt       C2 with the cross K/V streamed non-temporally (A/B of the MALL-resident default)
 #   b5one      beam 5 on one lane
 #   bench1nts / benchqnts  C3 one lane / 2 lanes with token_timestamps off (A/B of the round-3 regression)
-#   bench1fm / benchqfm    the same with libmwx_fmamix.so (f16r rounding off: an A/B build, not shipped)
 #   probe      the decode-chain probe (scripts/probe/dec_chain_probe): fused seams bit-exact + per-layer times
 #   mfstest    the MX-fp8 tests with the MFMA-score cross-attention (MWX_XATTN_MFS=1)
 #   c5mfs / c5one  C5 on one lane with / without the MFMA scores
@@ -70,14 +69,15 @@ for s in "$@"; do
     tsfull) run tsfull 600 python -u -m pytest tests/test_gpu_fulldepth.py -k "bench_workload" -m gpu -v -s -rf --timeout 600 --timeout-method thread ;;
     bench3l) run bench3l 600 python -u bench.py --lanes 3 --steps 9 --warmup 3 --no-cpu-baseline --no-one-lane ;;
     ptests) run ptests 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
+    qw8tests) run qw8tests 600 env MWX_ENC_ATTN_QW=8 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shapes.py -k "encoder or greedy or batch" -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
+    prof1qw8) (export MWX_ENC_ATTN_QW=8; cd /tmp && run prof1qw8 600 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_prof1qw8" -o prof -- $B --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline) || exit 4; python3 scripts/prof_box.py "$O/${TAG}_prof1qw8" || exit 4 ;;
+    bench1qw8) run bench1qw8 400 env MWX_ENC_ATTN_QW=8 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
     b5one) run b5one 500 python -u bench.py --beam 5 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
     bench1g16) run bench1g16 400 env MWX_GEMM_GROUP=16 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
     bench1g32) run bench1g32 400 env MWX_GEMM_GROUP=32 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
     pmcg32) (export MWX_GEMM_GROUP=32; cd /tmp && run pmcg32_FETCH_SIZE 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/${TAG}_pmcg32_FETCH_SIZE" -o pmc -- $B --lanes 1 --steps 1 --warmup 0 --decode-steps 8 --no-cpu-baseline) || exit 5 ;;
     bench1nts) run bench1nts 400 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline --no-token-timestamps ;;
     benchqnts) run benchqnts 400 python -u bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-token-timestamps ;;
-    bench1fm) run bench1fm 400 env MWX_LIB=$GRAFT_REPO_ROOT/sentiric-stt-whisper-service_amd/libmwx_fmamix.so python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
-    benchqfm) run benchqfm 400 env MWX_LIB=$GRAFT_REPO_ROOT/sentiric-stt-whisper-service_amd/libmwx_fmamix.so python -u bench.py --steps 8 --warmup 2 --no-cpu-baseline ;;
     probe) run probe 200 env PROBE_ONLY=seam ./scripts/probe/dec_chain_probe 32 10 && run probel 200 env PROBE_ONLY=layer ./scripts/probe/dec_chain_probe 32 10 ;;
     benchqnp) run benchqnp 400 env MWX_PERF_PERIOD=1000000 python -u bench.py --steps 8 --warmup 2 --no-cpu-baseline ;;
     bench1np8) run bench1np8 400 env MWX_PERF_PERIOD=1000000 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;

@@ -28,8 +28,8 @@ namespace mwx {
 
 constexpr int VSTR = 72;  // padded V^T tile row (elements)
 
-template <typename T>
-__global__ __launch_bounds__(256) void enc_attn_kernel(const _Float16* __restrict__ q,
+template <typename T, int QW = 4>
+__global__ __launch_bounds__(64 * QW) void enc_attn_kernel(const _Float16* __restrict__ q,
                                                        const _Float16* __restrict__ k,
                                                        const _Float16* __restrict__ vt, T* __restrict__ o,
                                                        int H, int L, int Lp, float scale_log2,
@@ -50,7 +50,7 @@ __global__ __launch_bounds__(256) void enc_attn_kernel(const _Float16* __restric
   }
   const int bh = wgid / nqb;
   const int b = bh / H, h = bh - b * H;
-  const int q0 = (wgid - bh * nqb) * 128 + wid * 32;
+  const int q0 = (wgid - bh * nqb) * (32 * QW) + wid * 32;
   const _Float16* Q = q + (long)bh * L * 64;
   const _Float16* Kh = k + (long)bh * L * 64;
   const _Float16* VT = vt + (long)bh * 64 * Lp;
@@ -70,35 +70,34 @@ __global__ __launch_bounds__(256) void enc_attn_kernel(const _Float16* __restric
     for (int u = 0; u < 2; ++u) oacc[te][u] = f32x4{0, 0, 0, 0};
   float mrow[2] = {-INFINITY, -INFINITY}, lrow[2] = {0.0f, 0.0f};
 
-  // staging: thread t moves 16-B chunk (row = t/8 + 32 i, ch = t%8) of the K
-  // tile (64 keys x 64 dims) and of the V^T tile (64 dims x 64 keys)
+  // staging: thread t moves 16-B chunk (row = t/8 + (8 QW) i, ch = t%8) of the
+  // K tile (64 keys x 64 dims) and of the V^T tile (64 dims x 64 keys); NP
+  // passes of 8 QW rows
+  constexpr int NP = 64 / (8 * QW), RS = 8 * QW;
   const int srow = tid >> 3, sch = tid & 7;
-  const int kso0 = srow * 64 + ((sch ^ (srow & 7)) << 3);  // (row+32)&7 == row&7
+  const int kso0 = srow * 64 + ((sch ^ (srow & 7)) << 3);  // (row+RS)&7 == row&7
   const int vso0 = srow * VSTR + sch * 8;
 #define GLOAD(kb)                                                                    \
   do {                                                                               \
-    const int kr0 = min((kb) * 64 + srow, L - 1), kr1 = min((kb) * 64 + srow + 32, L - 1); \
-    rk0 = *reinterpret_cast<const uint4*>(Kh + (long)kr0 * 64 + sch * 8);            \
-    rk1 = *reinterpret_cast<const uint4*>(Kh + (long)kr1 * 64 + sch * 8);            \
     const int key0 = (kb) * 64 + sch * 8;                                            \
-    if (key0 < Lp) {                                                                 \
-      rv0 = *reinterpret_cast<const uint4*>(VT + (long)srow * Lp + key0);            \
-      rv1 = *reinterpret_cast<const uint4*>(VT + (long)(srow + 32) * Lp + key0);     \
-    } else {                                                                         \
-      rv0 = rv1 = uint4{0, 0, 0, 0};                                                 \
+    _Pragma("unroll") for (int p_ = 0; p_ < NP; ++p_) {                              \
+      const int kr = min((kb) * 64 + srow + RS * p_, L - 1);                         \
+      rk[p_] = *reinterpret_cast<const uint4*>(Kh + (long)kr * 64 + sch * 8);        \
+      rv[p_] = key0 < Lp ? *reinterpret_cast<const uint4*>(VT + (long)(srow + RS * p_) * Lp + key0) \
+                         : uint4{0, 0, 0, 0};                                        \
     }                                                                                \
   } while (0)
 #define SSTORE(buf)                                                          \
   do {                                                                       \
-    *reinterpret_cast<uint4*>(&ks[buf][kso0]) = rk0;                         \
-    *reinterpret_cast<uint4*>(&ks[buf][kso0 + 32 * 64]) = rk1;               \
-    *reinterpret_cast<uint4*>(&vs[buf][vso0]) = rv0;                         \
-    *reinterpret_cast<uint4*>(&vs[buf][vso0 + 32 * VSTR]) = rv1;             \
+    _Pragma("unroll") for (int p_ = 0; p_ < NP; ++p_) {                      \
+      *reinterpret_cast<uint4*>(&ks[buf][kso0 + RS * p_ * 64]) = rk[p_];     \
+      *reinterpret_cast<uint4*>(&vs[buf][vso0 + RS * p_ * VSTR]) = rv[p_];   \
+    }                                                                        \
   } while (0)
 
   const int nkb = (L + 63) / 64;
   {
-    uint4 rk0, rk1, rv0, rv1;
+    uint4 rk[NP], rv[NP];
     GLOAD(0);
     SSTORE(0);
   }
@@ -108,7 +107,7 @@ __global__ __launch_bounds__(256) void enc_attn_kernel(const _Float16* __restric
   auto tile = [&](const int kb, auto masked) {
     constexpr bool MASKED = decltype(masked)::value;
     const int cur = kb & 1;
-    uint4 rk0, rk1, rv0, rv1;  // tile kb+1 in flight (global -> registers -> LDS)
+    uint4 rk[NP], rv[NP];  // tile kb+1 in flight (global -> registers -> LDS)
     if (kb + 1 < nkb) GLOAD(kb + 1);
     // S^T = K Q^T : sacc[t][u] rows = keys 16t + 4g + r, col = query c16
     f32x4 sacc[4][2];
@@ -234,9 +233,16 @@ template <typename T>
 void enc_attention(const _Float16* q, const _Float16* k, const _Float16* vt, T* o, int B, int H,
                    int L, float scale, hipStream_t st) {
   const int Lp = (L + 7) & ~7;
-  const int nqb = (L + 127) / 128;
-  enc_attn_kernel<T><<<nqb * B * H, 256, 0, st>>>(q, k, vt, o, H, L, Lp,
-                                                  scale * 1.4426950408889634f, nqb);
+  // MWX_ENC_ATTN_QW=8: 8 waves (256 queries) per workgroup, each K / V tile
+  // staged once for twice the queries (the per-query arithmetic is the same)
+  static const int qw = getenv("MWX_ENC_ATTN_QW") && atoi(getenv("MWX_ENC_ATTN_QW")) == 8 ? 8 : 4;
+  const int nqb = (L + 32 * qw - 1) / (32 * qw);
+  if (qw == 8)
+    enc_attn_kernel<T, 8><<<nqb * B * H, 512, 0, st>>>(q, k, vt, o, H, L, Lp,
+                                                      scale * 1.4426950408889634f, nqb);
+  else
+    enc_attn_kernel<T, 4><<<nqb * B * H, 256, 0, st>>>(q, k, vt, o, H, L, Lp,
+                                                      scale * 1.4426950408889634f, nqb);
 }
 
 // ---------------------------------------------------------------------------
