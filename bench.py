@@ -117,15 +117,16 @@ def oracle_stt_transcribe(o, pcm16, steps):
                            for s in segs], o.eot, o.token_bytes)
 
 
-CPU_DEC_STEPS = 8  # decode steps the large-model CPU leg measures (the rest are extrapolated)
+CPU_DEC_STEPS = 8  # decode steps the 4-thread CPU leg measures (the rest are extrapolated)
 
 
-def cpu_large_sample(model_path, arch, threads, prompt_len, steps):
-    """The oracle (scalar C++ + OpenMP) on a bounded sample of ONE clip of the
-    benched model: full log-mel, conv stem + ALL encoder layers, the all-layer
-    cross K/V and the prompt + CPU_DEC_STEPS decode positions (KV-cached, on
-    the clip's own cross K/V) measured; only the remaining decode steps are
-    extrapolated, at the measured mean time per step."""
+def cpu_large_sample(model_path, arch, threads, prompt_len, steps, dec_steps=None):
+    """The oracle (scalar C++ + OpenMP) on ONE clip of the benched model:
+    full log-mel, conv stem + ALL encoder layers, the all-layer cross K/V and
+    the prompt + dec_steps decode positions (KV-cached, on the clip's own
+    cross K/V) measured; dec_steps None = every decode step of the window
+    (nothing extrapolated), else the remaining steps are extrapolated at the
+    measured mean time per step."""
     import mwx
     import orc
     o = orc.Oracle(model_path, threads=threads)
@@ -139,7 +140,7 @@ def cpu_large_sample(model_path, arch, threads, prompt_len, steps):
     t0 = time.perf_counter()
     k, v = o.cross(enc)
     t_cross = time.perf_counter() - t0
-    n_meas = prompt_len + CPU_DEC_STEPS
+    n_meas = prompt_len + (steps if dec_steps is None else min(dec_steps, steps))
     toks = [o.sot] + [300 + i for i in range(n_meas - 1)]
     t0 = time.perf_counter()
     o.decode_seq(k, v, toks)
@@ -179,14 +180,21 @@ def cpu_baseline(model_path, arch, threads, prompt_len, steps):
            "label": "CPU restatement of the reference path (whisper.cpp v1.8.2 semantics)"}
     legs = {}
     for th in sorted({4, threads}):
-        v, measured, t_clip, n_meas, n_total = cpu_large_sample(model_path, arch, th, prompt_len,
-                                                                steps)
+        # the reported leg (all granted cores) decodes the whole window; the
+        # 4-thread leg (the reference's n_threads default) samples CPU_DEC_STEPS
+        full = th == threads
+        v, measured, t_clip, n_meas, n_total = cpu_large_sample(
+            model_path, arch, th, prompt_len, steps, None if full else CPU_DEC_STEPS)
+        if n_meas == n_total:
+            what = (f"{n_total} of {n_total} decode positions: the whole window measured, "
+                    f"{t_clip:.1f} s/clip")
+        else:
+            what = (f"{n_meas} of {n_total} decode positions measured ({measured:.1f} s); the "
+                    f"other {n_total - n_meas} decode steps extrapolated at the measured mean: "
+                    f"{t_clip:.1f} s/clip")
         legs[th] = {"value": round(v, 4), "cores": th,
                     "sample": (f"1 clip of 30 s, {arch}: log-mel + conv + all {ARCH[arch][3]} "
-                               f"encoder layers + all-layer cross K/V + {n_meas} of {n_total} "
-                               f"decode positions measured ({measured:.1f} s); the other "
-                               f"{n_total - n_meas} decode steps extrapolated at the measured "
-                               f"mean: {t_clip:.1f} s/clip")}
+                               f"encoder layers + all-layer cross K/V + {what}")}
     out.update(legs[threads])
     out["threads4"] = legs[4]
     tiny = os.path.join(os.environ.get("TMPDIR", "/tmp"), "mwx_bench_tiny.en_f16.bin")

@@ -78,6 +78,16 @@ int mwx_test_sample_draws(struct mwx_context* ctx, const float* probs, const flo
  * previous setting. */
 int mwx_test_set_xattn_mfs(int on);
 
+/* The MX-fp8 grouped cross-attention kernel on given data: q [R][H*64] f32
+ * queries (rounded to f16 by the kernel), K / V as e4m3 codes [R/nq][H][n][64]
+ * with E8M0 scales [R/nq][H][n][2] (one per 32-element half), rows
+ * g*nq .. g*nq+nq-1 reading slot g; o [R][H*64] f32 = the kernel's 16-bit
+ * output (the context's weight type). Scores / P.V on MFMA or v_dot2 per
+ * mwx_test_set_xattn_mfs. Returns 0 or <0. */
+int mwx_test_xattn_mx(struct mwx_context* ctx, int R, int H, int n, int nq, const float* q,
+                      const uint8_t* k8, const uint8_t* ks, const uint8_t* v8, const uint8_t* vs,
+                      float* o);
+
 #ifdef __cplusplus
 }
 #endif

@@ -215,6 +215,10 @@ def lib() -> C.CDLL:
     L.mwx_test_decode_counters.argtypes = [P, C.POINTER(C.c_long), C.POINTER(C.c_long), C.c_int]
     L.mwx_test_set_xattn_mfs.restype = C.c_int
     L.mwx_test_set_xattn_mfs.argtypes = [C.c_int]
+    u8p = C.POINTER(C.c_uint8)
+    L.mwx_test_xattn_mx.restype = C.c_int
+    L.mwx_test_xattn_mx.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, fpp, u8p, u8p,
+                                    u8p, u8p, fpp]
     L.mwx_test_sample_draws.restype = C.c_int
     L.mwx_test_sample_draws.argtypes = [P, fpp, fpp, C.c_int, C.c_int, C.POINTER(C.c_double),
                                         C.POINTER(C.c_int), C.c_int, C.c_int, C.c_int,
@@ -580,6 +584,23 @@ class Context:
         lib().mwx_test_decode_counters(self.state(state_index), C.byref(st), C.byref(pf),
                                        1 if reset else 0)
         return st.value, pf.value
+
+    def test_xattn_mx(self, q: np.ndarray, k8: np.ndarray, ks: np.ndarray, v8: np.ndarray,
+                      vs: np.ndarray, nq: int) -> np.ndarray:
+        """mwx_test_xattn_mx: q [R][H*64] f32; k8 / v8 uint8 [R/nq][H][n][64];
+        ks / vs uint8 [R/nq][H][n][2]. Returns o [R][H*64] f32."""
+        R, D = q.shape
+        G, H, n, _ = k8.shape
+        assert G * nq == R and H * 64 == D
+        q = np.ascontiguousarray(q, dtype=np.float32)
+        arrs = [np.ascontiguousarray(a, dtype=np.uint8) for a in (k8, ks, v8, vs)]
+        o = np.empty((R, D), dtype=np.float32)
+        u8 = lambda a: a.ctypes.data_as(C.POINTER(C.c_uint8))
+        rc = lib().mwx_test_xattn_mx(self.ctx, R, H, n, nq, q.ctypes.data_as(C.POINTER(C.c_float)),
+                                     *[u8(a) for a in arrs], o.ctypes.data_as(C.POINTER(C.c_float)))
+        if rc != 0:
+            raise RuntimeError(f"mwx_test_xattn_mx failed ({rc})")
+        return o
 
     def test_decode_last(self, tokens: Sequence[int], out: Optional[np.ndarray] = None,
                          state_index: int = 0) -> np.ndarray:

@@ -810,3 +810,85 @@ def test_beam_search_vs_oracle_arithmetic(rich):
               f"{'none' if first is None else first}")
         assert first is None or first >= 12, (k, first)
     print(f"beam 5 vs oracle arithmetic: {full} of 4 clips token-identical end to end")
+
+
+def _e4m3_encode(v):
+    """e4m3fn codes (nearest even; |v| <= 448) of float64 values."""
+    a = np.abs(v)
+    sub = a < 2.0 ** -6
+    e = np.floor(np.log2(np.where(sub, 1.0, a))).astype(np.int64)
+    m = np.where(sub, np.rint(a / 2.0 ** -9), np.rint(a / np.ldexp(1.0, e - 3)) - 8)
+    # rounding up to the next binade
+    up = ~sub & (m == 8)
+    e = np.where(up, e + 1, e)
+    m = np.where(up, 0, m)
+    sub_to_norm = sub & (m == 8)
+    code = np.where(sub & ~sub_to_norm, m, 0) + np.where(sub_to_norm, 1 << 3, 0)
+    code = np.where(sub, code, ((e + 7) << 3) + m)
+    return (code.astype(np.int64) | np.where(v < 0, 0x80, 0)).astype(np.uint8)
+
+
+def _e4m3_decode(c):
+    c = c.astype(np.int64)
+    s = np.where(c & 0x80, -1.0, 1.0)
+    e, m = (c >> 3) & 15, c & 7
+    return s * np.where(e == 0, m / 8.0 * 2.0 ** -6, (1.0 + m / 8.0) * np.ldexp(1.0, e - 7))
+
+
+def _mx_rows(x):
+    """x [..., 64] -> (codes uint8 [..., 64], E8M0 scales uint8 [..., 2], the
+    dequantized float64 values): one power-of-two scale per 32-element half,
+    the smallest 2^E with max |x| <= 448 * 2^E."""
+    h = x.reshape(*x.shape[:-1], 2, 32).astype(np.float64)
+    amax = np.abs(h).max(axis=-1, keepdims=True)
+    E = np.ceil(np.log2(np.maximum(amax, 1e-30) / 448.0))
+    codes = _e4m3_encode(h / np.ldexp(1.0, E.astype(np.int64)))
+    deq = _e4m3_decode(codes) * np.ldexp(1.0, E.astype(np.int64))
+    return (codes.reshape(x.shape), (E[..., 0] + 127).astype(np.uint8),
+            deq.reshape(x.shape))
+
+
+@pytest.mark.parametrize("sharp", [False, True])
+def test_mx_cross_attention_kernel_vs_f64(micro, sharp):
+    """The MX-fp8 grouped cross-attention kernel (the C5 cross-attention) on
+    K / V with large-v3-like MX scale ranges (per-row magnitudes spread over
+    2^-12 .. 2^-2 scales) and 1500 keys, against float64 attention over the
+    same dequantized values and f16-rounded queries. Diffuse softmax (weights
+    ~1/1500: the case where folding the V scale into an f16 P underflowed) and
+    peaked softmax. Bound: max |o - o64| <= 3e-3 x max |o64| per row, for both
+    the MFMA (default) and the v_dot2 path, and MFMA error <= 1.5 x v_dot2's +
+    1e-4 x max |o64|."""
+    ctx, _, _ = micro
+    rng = np.random.default_rng(7 if sharp else 3)
+    H, n, nq, G = 2, 1500, 5, 2
+    R = G * nq
+    rowscale = np.exp2(rng.uniform(-5, 3, size=(G, H, n, 1)))
+    k = rng.standard_normal((G, H, n, 64)) * 0.35 * rowscale
+    v = rng.standard_normal((G, H, n, 64)) * rowscale
+    k8, ks, kd = _mx_rows(k)
+    v8, vs, vd = _mx_rows(v)
+    q = (rng.standard_normal((R, H * 64)) * (3.0 if sharp else 0.02)).astype(np.float32)
+    qh = q.astype(np.float16).astype(np.float64)
+    scale = 64.0 ** -0.25
+    ref = np.empty((R, H * 64))
+    for r in range(R):
+        g = r // nq
+        for h in range(H):
+            s = kd[g, h] @ qh[r, h * 64:(h + 1) * 64] * scale
+            p = np.exp(s - s.max())
+            p /= p.sum()
+            ref[r, h * 64:(h + 1) * 64] = p @ vd[g, h]
+    errs = {}
+    prev = mwx.set_xattn_mfs(True)
+    try:
+        for mfs in (True, False):
+            mwx.set_xattn_mfs(mfs)
+            o = ctx.test_xattn_mx(q, k8, ks, v8, vs, nq)
+            scale_r = np.abs(ref).max(axis=1, keepdims=True)
+            errs[mfs] = float((np.abs(o - ref) / scale_r).max())
+    finally:
+        mwx.set_xattn_mfs(None if prev < 0 else bool(prev))
+    print(f"MX cross-attention vs f64 ({'peaked' if sharp else 'diffuse'}): "
+          f"MFMA {errs[True]:.2e}, v_dot2 {errs[False]:.2e} (of max |o| per row)")
+    assert errs[True] <= 3e-3 and errs[False] <= 3e-3, errs
+    assert errs[True] <= 1.5 * errs[False] + 1e-4, errs
