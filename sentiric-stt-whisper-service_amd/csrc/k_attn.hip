@@ -233,16 +233,12 @@ template <typename T>
 void enc_attention(const _Float16* q, const _Float16* k, const _Float16* vt, T* o, int B, int H,
                    int L, float scale, hipStream_t st) {
   const int Lp = (L + 7) & ~7;
-  // MWX_ENC_ATTN_QW=8: 8 waves (256 queries) per workgroup, each K / V tile
-  // staged once for twice the queries (the per-query arithmetic is the same)
-  static const int qw = getenv("MWX_ENC_ATTN_QW") && atoi(getenv("MWX_ENC_ATTN_QW")) == 8 ? 8 : 4;
-  const int nqb = (L + 32 * qw - 1) / (32 * qw);
-  if (qw == 8)
-    enc_attn_kernel<T, 8><<<nqb * B * H, 512, 0, st>>>(q, k, vt, o, H, L, Lp,
-                                                      scale * 1.4426950408889634f, nqb);
-  else
-    enc_attn_kernel<T, 4><<<nqb * B * H, 256, 0, st>>>(q, k, vt, o, H, L, Lp,
-                                                      scale * 1.4426950408889634f, nqb);
+  // (8 waves = 256 queries per workgroup, each K / V tile staged once for
+  // twice the queries: measured slower, 704 vs 624 us per large-v3 layer,
+  // profiles/r04_ab_regression_beam.md)
+  const int nqb = (L + 127) / 128;
+  enc_attn_kernel<T, 4><<<nqb * B * H, 256, 0, st>>>(q, k, vt, o, H, L, Lp,
+                                                    scale * 1.4426950408889634f, nqb);
 }
 
 // ---------------------------------------------------------------------------
