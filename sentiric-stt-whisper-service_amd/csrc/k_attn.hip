@@ -294,7 +294,7 @@ __device__ __forceinline__ float dpp_sum8(float d) {
 // written to the cache and taken from LDS (its cache line may be stale in L1).
 // The loop body is straight-line (two batches per trip, no early exit), so the
 // compiler keeps exactly one batch in flight with counted vmcnt waits.
-template <typename T, bool SELF, int UBX = 8, bool NTL = !SELF, int NBC = 0>
+template <typename T, bool SELF, int UBX = 8, bool NTL = !SELF, int NBC = 0, bool VK = false>
 __global__ __launch_bounds__(256) void dec_attn_kernel(
     const float* __restrict__ P, int KS, int pcols, const float* __restrict__ bias, float qscale,
     float kscale, _Float16* __restrict__ kbase, _Float16* __restrict__ vbase,
@@ -411,6 +411,11 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
   // NBC: the second key batch is requested before the query is formed too,
   // so two batches are in flight from the start
   if constexpr (NBC > 0) LOADROWS(kb2, K, 1)
+  // VK (self, one batch of positions): V batch 0 requested with K batch 0, so
+  // the P.V does not wait for a second round trip after the softmax
+  if constexpr (SELF && VK) {
+    if (nb == 1) LOADROWS0(kb2, V)
+  }
   if (red) {
     float acc = pk[0];
 #pragma unroll
@@ -501,6 +506,11 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
     // <= 4 batches of 128 rows at UB = 4 (n <= 448): latency-bound, one batch
     // per trip (loading V batch 0 together with K batch 0 measured 10% slower
     // at UB = 8: occupancy 4 -> 3)
+    if (VK && nb == 1) {
+      if (wave_busy) score_batch(ka, 0);
+      softmax();
+      if (wave_busy) pv_batch(kb2, 0);
+    } else {
     for (int b = 0; wave_busy && b < nb; ++b) {
       if (b > 0) LOADROWS(ka, K, b)
       score_batch(ka, b);
@@ -510,6 +520,7 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
     for (int b = 0; wave_busy && b < nb; ++b) {
       if (b > 0) LOADROWS(ka, V, b)
       pv_batch(ka, b);
+    }
     }
   } else if constexpr (NBC > 0) {
     // cross with a compile-time even batch count (n = 1500: 6): the K batches
@@ -1457,7 +1468,14 @@ void dec_attention(const float* P, int KS, int pcols, const float* bias, float q
   // MWX_XATTN_NBC=0: the runtime-batch-count cross kernel (A/B of the
   // constant-count load stream)
   static const bool xattn_nbc = !(getenv("MWX_XATTN_NBC") && atoi(getenv("MWX_XATTN_NBC")) == 0);
-  if (fixed_len == 0 && self_ub4)
+  // MWX_SELF_VK=1: V batch 0 requested with K batch 0 when the history fits
+  // one batch (A/B; the arithmetic is the same)
+  static const bool self_vk = getenv("MWX_SELF_VK") && atoi(getenv("MWX_SELF_VK")) == 1;
+  if (fixed_len == 0 && self_ub4 && self_vk)
+    dec_attn_kernel<T, true, 4, false, 0, true><<<g, 256, 0, st>>>(
+        P, KS, pcols, bias, qscale, kscale, kbase, vbase, kv_index, pos, active, fixed_len,
+        kv_len_cap, o, H, scale, kvmap, own_from, map_row0, nq, R, write_new, span);
+  else if (fixed_len == 0 && self_ub4)
     dec_attn_kernel<T, true, 4><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale, kbase,
                                                    vbase, kv_index, pos, active, fixed_len,
                                                    kv_len_cap, o, H, scale, kvmap, own_from,

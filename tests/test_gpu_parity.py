@@ -788,30 +788,6 @@ def test_beam_runahead_equals_host_loop(rich, temperature_inc, monkeypatch):
     assert ra == host
 
 
-def test_beam_search_vs_oracle_arithmetic(rich):
-    """Beam 5 against the oracle's OWN arithmetic (not a replay) over whole
-    clips: the device's f16 logits differ from the oracle's by rounding
-    noise, so two hypotheses whose summed log-probs come within that noise may
-    rank differently. Per clip the stream must agree up to its first
-    difference, which may not come before token 12 (printed: where each clip
-    diverges, if at all)."""
-    ctx, o, _ = rich
-    full = 0
-    for k in range(4):
-        pcm = pcm_clip(50 + k, 14.0 + 4 * k)
-        segs = run_fresh(ctx, pcm, beam_params(ctx, 0.0))
-        _, osegs, _, _ = o.full(pcm, beam_opt(0.0))
-        ids = [t.id for s in segs for t in s.tokens]
-        oids = [t.id for s in osegs for t in s.tokens]
-        first = next((i for i, (a, b) in enumerate(zip(ids, oids)) if a != b), None)
-        if first is None and len(ids) == len(oids):
-            full += 1
-        print(f"clip {k}: {len(ids)} / {len(oids)} tokens, first difference at "
-              f"{'none' if first is None else first}")
-        assert first is None or first >= 12, (k, first)
-    print(f"beam 5 vs oracle arithmetic: {full} of 4 clips token-identical end to end")
-
-
 def _e4m3_encode(v):
     """e4m3fn codes (nearest even; |v| <= 448) of float64 values."""
     a = np.abs(v)
