@@ -294,7 +294,7 @@ __device__ __forceinline__ float dpp_sum8(float d) {
 // written to the cache and taken from LDS (its cache line may be stale in L1).
 // The loop body is straight-line (two batches per trip, no early exit), so the
 // compiler keeps exactly one batch in flight with counted vmcnt waits.
-template <typename T, bool SELF, int UBX = 8, bool NTL = !SELF, int NBC = 0, bool VK = false>
+template <typename T, bool SELF, int UBX = 8, bool NTL = !SELF, int NBC = 0>
 __global__ __launch_bounds__(256) void dec_attn_kernel(
     const float* __restrict__ P, int KS, int pcols, const float* __restrict__ bias, float qscale,
     float kscale, _Float16* __restrict__ kbase, _Float16* __restrict__ vbase,
@@ -411,11 +411,6 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
   // NBC: the second key batch is requested before the query is formed too,
   // so two batches are in flight from the start
   if constexpr (NBC > 0) LOADROWS(kb2, K, 1)
-  // VK (self, one batch of positions): V batch 0 requested with K batch 0, so
-  // the P.V does not wait for a second round trip after the softmax
-  if constexpr (SELF && VK) {
-    if (nb == 1) LOADROWS0(kb2, V)
-  }
   if (red) {
     float acc = pk[0];
 #pragma unroll
@@ -506,11 +501,6 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
     // <= 4 batches of 128 rows at UB = 4 (n <= 448): latency-bound, one batch
     // per trip (loading V batch 0 together with K batch 0 measured 10% slower
     // at UB = 8: occupancy 4 -> 3)
-    if (VK && nb == 1) {
-      if (wave_busy) score_batch(ka, 0);
-      softmax();
-      if (wave_busy) pv_batch(kb2, 0);
-    } else {
     for (int b = 0; wave_busy && b < nb; ++b) {
       if (b > 0) LOADROWS(ka, K, b)
       score_batch(ka, b);
@@ -520,7 +510,6 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
     for (int b = 0; wave_busy && b < nb; ++b) {
       if (b > 0) LOADROWS(ka, V, b)
       pv_batch(ka, b);
-    }
     }
   } else if constexpr (NBC > 0) {
     // cross with a compile-time even batch count (n = 1500: 6): the K batches
@@ -913,11 +902,37 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
 #pragma unroll
     for (int q = 0; q < NQ; ++q) redd[wid][q] = sum[q];
   __syncthreads();
+  // P = f16(e * (float)(1/sum)) (ggml order). The v_dot2 P.V below takes the
+  // weights of its row pairs (j, j + 8) as packed f16 pairs: P is written
+  // back over the scores as pp[q][(j >> 4) * 8 + (j & 7)] = {P[j], P[j + 8]}
+  // (0 past n), so each pair is one LDS read instead of two reads and three
+  // conversions (the same f16 values: bit-identical). The reads of a
+  // query's exps all precede the barrier before its pairs are written.
+  if constexpr (MFS && KV8) {
 #pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    const double t = (redd[0][q] + redd[1][q]) + (redd[2][q] + redd[3][q]);
-    const float inv = (float)(1.0 / t);
-    for (int j = tid; j < n; j += 256) sc[q][j] = (float)f16r(sc[q][j] * inv);
+    for (int q = 0; q < NQ; ++q) {
+      const double t = (redd[0][q] + redd[1][q]) + (redd[2][q] + redd[3][q]);
+      const float inv = (float)(1.0 / t);
+      for (int j = tid; j < n; j += 256) sc[q][j] = (float)f16r(sc[q][j] * inv);
+    }
+  } else {
+    constexpr int NPR = DEC_MAX_KEYS / 2 / 256;  // pairs per thread per query
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const double t = (redd[0][q] + redd[1][q]) + (redd[2][q] + redd[3][q]);
+      const float inv = (float)(1.0 / t);
+      h2 pr[NPR];
+#pragma unroll
+      for (int i = 0; i < NPR; ++i) {
+        const int pi = tid + 256 * i, j0 = (pi >> 3) * 16 + (pi & 7), j1 = j0 + 8;
+        const float e0 = sc[q][min(j0, n - 1)], e1 = sc[q][min(j1, n - 1)];
+        pr[i] = h2{j0 < n ? f16r(e0 * inv) : (_Float16)0.0f, j1 < n ? f16r(e1 * inv) : (_Float16)0.0f};
+      }
+      __syncthreads();
+      h2* pp = reinterpret_cast<h2*>(&sc[q][0]);
+#pragma unroll
+      for (int i = 0; i < NPR; ++i) pp[tid + 256 * i] = pr[i];
+    }
   }
   __syncthreads();
   if constexpr (MFS && KV8) {
@@ -1017,12 +1032,11 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
       h2 vp[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) vp[e] = h2{vv[uu][e], vv[uu + 1][e]};
+      (void)j1;
+      const int pidx = (j0 >> 4) * 8 + (j0 & 7);
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
-        float p0 = sc[q][min(j0, n - 1)], p1 = sc[q][min(j1, n - 1)];
-        if (j0 >= n) p0 = 0.0f;
-        if (j1 >= n) p1 = 0.0f;
-        const h2 ph = h2{(_Float16)p0, (_Float16)p1};
+        const h2 ph = reinterpret_cast<const h2*>(&sc[q][0])[pidx];
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc[q][e] = __builtin_amdgcn_fdot2(ph, vp[e], acc[q][e], false);
       }
@@ -1083,218 +1097,6 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
   span_end(span);
 }
 
-// MX-fp8 cross K/V cache, NQ rows of one clip (dec_xattn_kernel's KV8 path
-// restructured for memory-level parallelism): an fp8 row is half the bytes of
-// an f16 row, so a lane takes whole 256-row batches (8 rows, 64 B) instead of
-// half batches, and the K batches then the V batches form one stream with two
-// batches in flight (round 2's half-batch stream kept ~2 KB per wave in
-// flight: 60 us for 127.5 MB at 32 clips x 5 rows, 0.27 of HBM). Every row's
-// arithmetic is dec_xattn_kernel's: the same rows per lane, the same widening
-// (v_cvt_scalef32_pk_f16_fp8), scores, softmax order and P.V pairs.
-template <typename T, int NQ>
-__global__ __launch_bounds__(256) void dec_xattn8_kernel(
-    const float* __restrict__ P, int KS, int pcols, const float* __restrict__ bias,
-    const uint8_t* __restrict__ kbase, const uint8_t* __restrict__ vbase,
-    const uint8_t* __restrict__ kscale8, const uint8_t* __restrict__ vscale8,
-    const int* __restrict__ kv_index, const int* __restrict__ active, int n, int cap, int R,
-    T* __restrict__ o, int H, float scale) {
-  __shared__ float sc[NQ][DEC_MAX_KEYS];
-  __shared__ float redf[4][NQ];
-  __shared__ double redd[4][NQ];
-  __shared__ float pv[4][64][9];
-  __shared__ float sq[NQ][64];
-  const int g = blockIdx.y, h = blockIdx.x, row0 = g * NQ;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int kg = lane >> 3, c = lane & 7;
-  bool act[NQ];
-  bool any = false;
-  const int slot = kv_index ? kv_index[row0] : row0;
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    act[q] = row0 + q < R && active[min(row0 + q, R - 1)];
-    any |= act[q];
-  }
-  asm volatile("" ::"s"(slot));
-  if (!any) return;
-  const int D = H * 64;
-  const long rbase = ((long)slot * H + h) * cap;
-  const uint8_t* K8 = kbase + rbase * 64;
-  const uint8_t* V8 = vbase + rbase * 64;
-  const uint8_t* KS8 = kscale8 + rbase * 2;
-  const uint8_t* VS8 = vscale8 + rbase * 2;
-  const int nb = (n + 255) >> 8;
-  const int jmax = n - 1;
-  // stream position t: K batch t (t < nb), then V batch t - nb
-  auto load = [&](uint2 (&qb)[8], uint32_t& sr, int t) {
-    const bool isv = t >= nb;
-    const int b = isv ? t - nb : t;
-    const uint8_t* base = isv ? V8 : K8;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int j = min(b * 256 + wid * 64 + u * 8 + kg, jmax);
-      const u32x2 q2 = ld_stream<true>(reinterpret_cast<const u32x2*>(base + (long)j * 64 + c * 8));
-      qb[u] = uint2{q2[0], q2[1]};
-    }
-    sr = *reinterpret_cast<const uint16_t*>((isv ? VS8 : KS8) +
-                                           (long)min(b * 256 + wid * 64 + lane, jmax) * 2);
-  };
-  auto widen = [&](const uint2 (&qb)[8], uint32_t sr, int u) {
-    const uint32_t pr = (uint32_t)__shfl((int)sr, u * 8 + kg, 64);
-    return dequant_h8(qb[u], (pr >> (8 * (c >> 2))) & 0xffu);
-  };
-  // queries (as dec_xattn_kernel): slab loads first, then the first batches
-  const long pstride = (long)R * pcols;
-  constexpr int QI = (NQ * 64 + 255) / 256;
-  float pq[QI][8];
-#pragma unroll
-  for (int i = 0; i < QI; ++i) {
-    const int t = tid + 256 * i;
-    const int q = min(t >> 6, NQ - 1), e = t & 63;
-    const float* pp = P + (long)min(row0 + q, R - 1) * pcols + h * 64 + e;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) pq[i][k] = pp[min(k, KS - 1) * pstride];
-  }
-  const float bq = bias[h * 64 + (tid & 63)];
-  uint2 qa[8], qb[8];
-  uint32_t sa = 0, sb = 0;
-  load(qa, sa, 0);
-  if (1 < 2 * nb) load(qb, sb, 1);
-#pragma unroll
-  for (int i = 0; i < QI; ++i) {
-    const int t = tid + 256 * i;
-    if (t < NQ * 64) {
-      const int q = t >> 6, e = t & 63;
-      float acc = pq[i][0];
-#pragma unroll
-      for (int k = 1; k < 8; ++k) acc += k < KS ? pq[i][k] : 0.0f;
-      sq[q][e] = (float)f16r(acc + bq);
-    }
-  }
-  __syncthreads();
-  h2 qh[NQ][4];
-#pragma unroll
-  for (int q = 0; q < NQ; ++q)
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      qh[q][e] = h2{(_Float16)sq[q][c * 8 + 2 * e], (_Float16)sq[q][c * 8 + 2 * e + 1]};
-  float acc[NQ][8];
-#pragma unroll
-  for (int q = 0; q < NQ; ++q)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) acc[q][e] = 0.0f;
-  auto score = [&](const uint2 (&qbuf)[8], uint32_t sr, int b) {
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const f16x8 kk = widen(qbuf, sr, u);
-      const int j = b * 256 + wid * 64 + u * 8 + kg;
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        float d = dot8(qh[q], kk);
-        d = dpp_sum8(d);
-        if (c == 0 && j < n) sc[q][j] = d * scale;
-      }
-      __builtin_amdgcn_sched_barrier(0);  // one row's conversions live at a time
-    }
-  };
-  auto softmax = [&]() {
-    __syncthreads();
-    float mx[NQ];
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      float m = -INFINITY;
-      for (int j = tid; j < n; j += 256) m = fmaxf(m, sc[q][j]);
-      mx[q] = wave_max_dpp(m);
-    }
-    if (lane == 0)
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) redf[wid][q] = mx[q];
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < NQ; ++q)
-      mx[q] = fmaxf(fmaxf(redf[0][q], redf[1][q]), fmaxf(redf[2][q], redf[3][q]));
-    double sum[NQ];
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      double sm = 0.0;
-      for (int j = tid; j < n; j += 256) {
-        const float e = expf(sc[q][j] - mx[q]);
-        sc[q][j] = e;
-        sm += (double)e;
-      }
-      sum[q] = wave_sum_d_dpp(sm);
-    }
-    if (lane == 0)
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) redd[wid][q] = sum[q];
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const double t = (redd[0][q] + redd[1][q]) + (redd[2][q] + redd[3][q]);
-      const float inv = (float)(1.0 / t);
-      for (int j = tid; j < n; j += 256) sc[q][j] = (float)f16r(sc[q][j] * inv);
-    }
-    __syncthreads();
-  };
-  auto pvb = [&](const uint2 (&qbuf)[8], uint32_t sr, int b) {
-#pragma unroll
-    for (int u = 0; u < 8; u += 2) {  // row pairs (u, u+1) as in dec_attn_kernel
-      const f16x8 v0 = widen(qbuf, sr, u), v1 = widen(qbuf, sr, u + 1);
-      const int j0 = b * 256 + wid * 64 + u * 8 + kg, j1 = j0 + 8;
-      h2 vp[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) vp[e] = h2{v0[e], v1[e]};
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        float p0 = sc[q][min(j0, n - 1)], p1 = sc[q][min(j1, n - 1)];
-        if (j0 >= n) p0 = 0.0f;
-        if (j1 >= n) p1 = 0.0f;
-        const h2 ph = h2{(_Float16)p0, (_Float16)p1};
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc[q][e] = __builtin_amdgcn_fdot2(ph, vp[e], acc[q][e], false);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  // (nb even, the caller's condition: V batch 0 lands in qa, 1 in qb)
-#pragma unroll 1
-  for (int t = 0; t < nb; t += 2) {
-    score(qa, sa, t);
-    load(qa, sa, t + 2);
-    score(qb, sb, t + 1);
-    load(qb, sb, t + 3);
-  }
-  softmax();
-#pragma unroll 1
-  for (int b = 0; b < nb; b += 2) {
-    pvb(qa, sa, b);
-    if (b + 2 < nb) load(qa, sa, nb + b + 2);
-    pvb(qb, sb, b + 1);
-    if (b + 3 < nb) load(qb, sb, nb + b + 3);
-  }
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float a = acc[q][e];
-      a += __shfl_xor(a, 8, 64);
-      a += __shfl_xor(a, 16, 64);
-      a += __shfl_xor(a, 32, 64);
-      acc[q][e] = a;
-    }
-    if (kg == 0) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) pv[wid][c][e] = acc[q][e];
-    }
-    __syncthreads();
-    if (tid < 64 && act[q]) {
-      const int cc = tid >> 3, e = tid & 7;
-      const float r = (pv[0][cc][e] + pv[1][cc][e]) + (pv[2][cc][e] + pv[3][cc][e]);
-      o[pack_index(row0 + q, h * 64 + cc * 8 + e, D)] = to_t<T>(r);
-    }
-    __syncthreads();
-  }
-}
-
 static std::atomic<int>& xattn_mfs_mode() {
   static std::atomic<int> m{-1};
   return m;
@@ -1337,25 +1139,6 @@ bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float*
                                                         kscale8, vscale8, kv_index, active,    \
                                                         n_keys, cap, R, o, H, scale, span);    \
   } while (0)
-  // MX-fp8 cache: MWX_XATTN8=1 selects the whole-batch two-in-flight stream
-  // (dec_xattn8_kernel). Off by default: measured 69.2 us per launch against
-  // 52.6 us for the half-batch stream of dec_xattn_kernel at beam 5, large-v3
-  // (gpurun_out s6); kept as the A/B.
-  static const bool x8 = getenv("MWX_XATTN8") && atoi(getenv("MWX_XATTN8")) != 0;
-  if (kv8 && x8 && ((n_keys + 255) / 256) % 2 == 0) {
-    const uint8_t* k8 = reinterpret_cast<const uint8_t*>(kbase);
-    const uint8_t* v8 = reinterpret_cast<const uint8_t*>(vbase);
-    switch (nq) {
-#define X8(N)                                                                                  \
-  case N:                                                                                      \
-    dec_xattn8_kernel<T, N><<<g, 256, 0, st>>>(P, KS, pcols, bias, k8, v8, kscale8, vscale8,    \
-                                               kv_index, active, n_keys, cap, R, o, H, scale); \
-    return true;
-      X8(1) X8(2) X8(3) X8(4) X8(5) X8(6) X8(7) X8(8)
-#undef X8
-      default: return false;
-    }
-  }
   // MX-fp8 cache: scores on MFMA (default; MWX_XATTN_MFS=0 or
   // xattn_mfs_set(0): the v_dot2 scores, the A/B: C5 one lane 735.8 -> 778.8
   // audio-s/s, 52.4 -> 44.6 us per launch)
@@ -1468,14 +1251,7 @@ void dec_attention(const float* P, int KS, int pcols, const float* bias, float q
   // MWX_XATTN_NBC=0: the runtime-batch-count cross kernel (A/B of the
   // constant-count load stream)
   static const bool xattn_nbc = !(getenv("MWX_XATTN_NBC") && atoi(getenv("MWX_XATTN_NBC")) == 0);
-  // MWX_SELF_VK=1: V batch 0 requested with K batch 0 when the history fits
-  // one batch (A/B; the arithmetic is the same)
-  static const bool self_vk = getenv("MWX_SELF_VK") && atoi(getenv("MWX_SELF_VK")) == 1;
-  if (fixed_len == 0 && self_ub4 && self_vk)
-    dec_attn_kernel<T, true, 4, false, 0, true><<<g, 256, 0, st>>>(
-        P, KS, pcols, bias, qscale, kscale, kbase, vbase, kv_index, pos, active, fixed_len,
-        kv_len_cap, o, H, scale, kvmap, own_from, map_row0, nq, R, write_new, span);
-  else if (fixed_len == 0 && self_ub4)
+  if (fixed_len == 0 && self_ub4)
     dec_attn_kernel<T, true, 4><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale, kbase,
                                                    vbase, kv_index, pos, active, fixed_len,
                                                    kv_len_cap, o, H, scale, kvmap, own_from,
