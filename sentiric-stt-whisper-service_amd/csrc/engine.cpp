@@ -770,6 +770,17 @@ struct Driver {
   const Hparams& hp;
   int d, H, L_enc, L_dec, V, Tctx, Lp;
   LogitsConst LC;
+  // run-ahead: the step's lp_pick runs inside the advance kernel (pick_in())
+  bool pick_in_advance = false;
+  PickIn pick_in() const {
+    PickIn p;
+    p.logits = (const float*)S.logits.p;
+    p.flt = (const float*)S.lpflt.p;
+    p.parts = (const LPPart*)S.lpparts.p;
+    p.res = (const LPRes*)S.lpres.p;
+    p.C = LC;
+    return p;
+  }
   // rows per clip in the current decode run (beam_size / best_of decoders are
   // consecutive rows of one clip); decode groups never split such a run
   int xgroup = 1;
@@ -1105,11 +1116,12 @@ struct Driver {
     bool k5 = false;
     int ks_prev = 0;  // the last FFN2's split-K factor and bias (folded into
     const float* bias_prev = nullptr;  // the next consumer)
+    bool embed = false;  // the first LayerNorm forms x from the embeddings
   };
-  void layers_begin(const LayerRows& rw, LayerRun& c, hipStream_t s) {
+  void layers_begin(const LayerRows& rw, LayerRun& c, hipStream_t) {
     c = LayerRun{};
     c.xd = rw.xd;
-    embed<T>(Wt(C.tok_emb), C.dec_pe, rw.tok, rw.pos, rw.act, rw.xd, rw.n, d, s);
+    c.embed = true;  // (no launch: layer 0's LN1 embeds, ln_dec EmbedIn)
   }
   // The d- and 3d-wide projections run as split-K GEMMs writing f32 partial
   // slabs; each consumer (LN: bias + residual, attention: bias/scale/f16 and
@@ -1122,8 +1134,16 @@ struct Driver {
     _Float16* ks = rw.kself + l * layer_self;
     _Float16* vs = rw.vself + l * layer_self;
     T* hd = rw.hd;
+    EmbedIn<T> emb;
+    if (c.embed) {
+      emb.te = Wt(C.tok_emb);
+      emb.pe = C.dec_pe;
+      emb.tok = rw.tok;
+      emb.pos = rw.pos;
+      c.embed = false;
+    }
     layer_norm_dec<T>(c.xd, W.ln1_w, W.ln1_b, hd, n, d, rw.act, s, c.ks_prev ? rw.Pres : nullptr,
-                      c.ks_prev, c.bias_prev);
+                      c.ks_prev, c.bias_prev, emb);
     { PerfScope ps(S, "dec_gemm", s);
       c.k1 = gemm_splitk_partials<T>(hd, Dw(W.qkv), n, 3 * d, d, rw.Pqkv, s); }
     static const int pf_selfwrite =
@@ -1407,7 +1427,7 @@ struct Driver {
                    (const RowCtl*)S.ctl.p + r0, (TokOut*)S.tokout.p + r0, pr, lp, LC, n,
                    LPScratch{(float*)S.lpflt.p + (size_t)r0 * V, (LPPart*)S.lpparts.p + r0 * LP_G,
                              (LPRes*)S.lpres.p + r0 * LP_G},
-                   s);
+                   s, !pick_in_advance);
     if (want_probs) {  // std::discrete_distribution draws of the sampling rows
       const int KD = S.draw_k;
       sample_draws(pr, lp, V, (const double*)S.du.p + (size_t)r0 * KD, (const int*)S.dnd.p + r0,

@@ -122,7 +122,8 @@ __global__ __launch_bounds__(256) void ln_dec_kernel(float* __restrict__ x,
                                                      const int* __restrict__ active,
                                                      const float* __restrict__ P, int KS,
                                                      long pstride,
-                                                     const float* __restrict__ pbias) {
+                                                     const float* __restrict__ pbias,
+                                                     EmbedIn<T> emb) {
   __shared__ double red[2][4];
   const int row = blockIdx.x;
   // the row, its split-K slabs and the activity flag are all requested before
@@ -131,8 +132,23 @@ __global__ __launch_bounds__(256) void ln_dec_kernel(float* __restrict__ x,
   const bool own = tid * 8 < N;
   const int i0 = own ? tid * 8 : 0;
   float* xr = x + (long)row * N + i0;
-  const f32x4 xa = *reinterpret_cast<const f32x4*>(xr);
-  const f32x4 xc = *reinterpret_cast<const f32x4*>(xr + 4);
+  f32x4 xa, xc;
+  if (emb.te) {
+    // x = te[tok] + pe[pos] (ggml_get_rows(d_te) + ggml_get_rows(d_pe)), the ids first
+    const typename Elt<T>::v8 er =
+        *reinterpret_cast<const typename Elt<T>::v8*>(emb.te + (long)emb.tok[row] * N + i0);
+    const float* pr = emb.pe + (long)emb.pos[row] * N + i0;
+    const f32x4 pa = *reinterpret_cast<const f32x4*>(pr);
+    const f32x4 pc = *reinterpret_cast<const f32x4*>(pr + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      xa[e] = to_f<T>(er[e]) + pa[e];
+      xc[e] = to_f<T>(er[4 + e]) + pc[e];
+    }
+  } else {
+    xa = *reinterpret_cast<const f32x4*>(xr);
+    xc = *reinterpret_cast<const f32x4*>(xr + 4);
+  }
   f32x4 pk[8][2];
   f32x4 pb0, pb1;
   if (P) {
@@ -172,6 +188,8 @@ __global__ __launch_bounds__(256) void ln_dec_kernel(float* __restrict__ x,
         if (k < KS) acc += pk[k][e >> 2][e & 3];
       v[e] = (acc + (e < 4 ? pb0[e] : pb1[e - 4])) + v[e];
     }
+  }
+  if (P || emb.te) {
     if (own) {
       *reinterpret_cast<f32x4*>(xr) = f32x4{v[0], v[1], v[2], v[3]};
       *reinterpret_cast<f32x4*>(xr + 4) = f32x4{v[4], v[5], v[6], v[7]};
@@ -212,29 +230,8 @@ __global__ __launch_bounds__(256) void ln_dec_kernel(float* __restrict__ x,
 template <typename T>
 void layer_norm_dec(float* x, const float* w, const float* b, T* y, int M, int N,
                     const int* active, hipStream_t st, const float* P, int KS,
-                    const float* pbias) {
-  ln_dec_kernel<T><<<M, 256, 0, st>>>(x, w, b, y, N, active, P, KS, (long)M * N, pbias);
-}
-
-// x[r] = te[tok[r]] + pe[pos[r]]   (ggml_get_rows(d_te) + ggml_get_rows(d_pe))
-template <typename T>
-__global__ __launch_bounds__(256) void embed_kernel(const T* __restrict__ te,
-                                                    const float* __restrict__ pe,
-                                                    const int* __restrict__ tok,
-                                                    const int* __restrict__ pos,
-                                                    const int* __restrict__ active,
-                                                    float* __restrict__ x, int d) {
-  const int r = blockIdx.x;
-  if (!active[r]) return;
-  const T* er = te + (long)tok[r] * d;
-  const float* pr = pe + (long)pos[r] * d;
-  for (int i = threadIdx.x; i < d; i += 256) x[(long)r * d + i] = to_f<T>(er[i]) + pr[i];
-}
-
-template <typename T>
-void embed(const T* te, const float* pe, const int* tok, const int* pos, const int* active,
-           float* x, int R, int d, hipStream_t st) {
-  embed_kernel<T><<<R, 256, 0, st>>>(te, pe, tok, pos, active, x, d);
+                    const float* pbias, const EmbedIn<T>& emb) {
+  ln_dec_kernel<T><<<M, 256, 0, st>>>(x, w, b, y, N, active, P, KS, (long)M * N, pbias, emb);
 }
 
 template void layer_norm<_Float16>(const float*, const float*, const float*, _Float16*, int, int,
@@ -242,13 +239,11 @@ template void layer_norm<_Float16>(const float*, const float*, const float*, _Fl
 template void layer_norm<__bf16>(const float*, const float*, const float*, __bf16*, int, int,
                                  const int*, hipStream_t, const float*, int, const float*);
 template void layer_norm_dec<_Float16>(float*, const float*, const float*, _Float16*, int, int,
-                                       const int*, hipStream_t, const float*, int, const float*);
+                                       const int*, hipStream_t, const float*, int, const float*,
+                                       const EmbedIn<_Float16>&);
 template void layer_norm_dec<__bf16>(float*, const float*, const float*, __bf16*, int, int,
-                                     const int*, hipStream_t, const float*, int, const float*);
-template void embed<_Float16>(const _Float16*, const float*, const int*, const int*, const int*,
-                              float*, int, int, hipStream_t);
-template void embed<__bf16>(const __bf16*, const float*, const int*, const int*, const int*, float*,
-                            int, int, hipStream_t);
+                                     const int*, hipStream_t, const float*, int, const float*,
+                                     const EmbedIn<__bf16>&);
 
 // ---------------------------------------------------------------------------
 // logits processing + greedy sampling
@@ -545,15 +540,11 @@ __global__ __launch_bounds__(LP_T) void lp_probs_kernel(float* __restrict__ flt,
   }
 }
 
-__global__ __launch_bounds__(64) void lp_pick_kernel(const float* __restrict__ logits,
-                                                     const float* __restrict__ flt,
-                                                     const LPPart* __restrict__ parts,
-                                                     const LPRes* __restrict__ res,
-                                                     const RowCtl* __restrict__ ctl,
-                                                     TokOut* __restrict__ out, LogitsConst C) {
-  const int row = blockIdx.x;
-  const RowCtl c = ctl[row];
-  if (!c.active || !c.sample || threadIdx.x != 0) return;
+// phase 3 for one row (sampling rows only): lp_pick_kernel, or the run-ahead
+// advance kernels directly (no launch of its own)
+__device__ TokOut lp_pick_row(int row, const RowCtl& c, const float* __restrict__ logits,
+                              const float* __restrict__ flt, const LPPart* __restrict__ parts,
+                              const LPRes* __restrict__ res, const LogitsConst& C) {
   const int V = C.n_vocab;
   const LPStats st = lp_combine(parts + row * LP_G, c.want_nosp);
   const LPRes* R = res + row * LP_G;
@@ -578,16 +569,28 @@ __global__ __launch_bounds__(64) void lp_pick_kernel(const float* __restrict__ l
   t.plog = plog;  // (host applies the id >= beg -> tid/pt override)
   t.nosp = c.want_nosp ? expf(logits[(long)row * V + C.nosp_id] - st.rlse) : 0.0f;
   t.pad = 0;
-  out[row] = t;
+  return t;
+}
+
+__global__ __launch_bounds__(64) void lp_pick_kernel(const float* __restrict__ logits,
+                                                     const float* __restrict__ flt,
+                                                     const LPPart* __restrict__ parts,
+                                                     const LPRes* __restrict__ res,
+                                                     const RowCtl* __restrict__ ctl,
+                                                     TokOut* __restrict__ out, LogitsConst C) {
+  const int row = blockIdx.x;
+  const RowCtl c = ctl[row];
+  if (!c.active || !c.sample || threadIdx.x != 0) return;
+  out[row] = lp_pick_row(row, c, logits, flt, parts, res, C);
 }
 
 void logits_process(float* logits, const float* static_mask, const RowCtl* ctl, TokOut* out,
                     float* probs, float* logprobs, const LogitsConst& C, int R, LPScratch ws,
-                    hipStream_t st) {
+                    hipStream_t st, bool pick) {
   const dim3 g(LP_G, R);
   lp_filter_kernel<<<g, LP_T, 0, st>>>(logits, static_mask, ctl, ws.flt, ws.parts, C);
   lp_probs_kernel<<<g, LP_T, 0, st>>>(ws.flt, ws.parts, ctl, ws.res, probs, logprobs, C);
-  lp_pick_kernel<<<R, 64, 0, st>>>(logits, ws.flt, ws.parts, ws.res, ctl, out, C);
+  if (pick) lp_pick_kernel<<<R, 64, 0, st>>>(logits, ws.flt, ws.parts, ws.res, ctl, out, C);
 }
 
 // The token loop's per-row rules on the token a row generated this step
@@ -647,15 +650,20 @@ __global__ __launch_bounds__(256) void row_advance_kernel(RowRun* __restrict__ r
                                                           const int* __restrict__ prompt,
                                                           int* __restrict__ si,
                                                           RowCtl* __restrict__ ctl,
-                                                          const TokOut* __restrict__ out,
-                                                          RunReport* __restrict__ rep, RunConst C) {
+                                                          TokOut* __restrict__ out,
+                                                          RunReport* __restrict__ rep, RunConst C,
+                                                          PickIn pk) {
   const int step = *run_step;
   const int R = C.R;
   RunReport* slot = rep + (long)(step % C.nslot) * R;
   for (int r = threadIdx.x; r < R; r += blockDim.x) {
     RowRun w = run[r];
     const RowCtl k = ctl[r];
-    const TokOut t = out[r];
+    TokOut t = out[r];
+    if (pk.parts && k.active && k.sample) {  // (the step's lp_pick, here)
+      t = lp_pick_row(r, k, pk.logits, pk.flt, pk.parts, pk.res, pk.C);
+      out[r] = t;
+    }
     if (!w.stopped) {
       if (k.sample) token_rules(w, t.id, C);
       if (!w.stopped) w.fed++;
@@ -704,11 +712,12 @@ __global__ __launch_bounds__(BA_T) void beam_advance_kernel(RowRun* __restrict__
                                                             const int* __restrict__ prompt,
                                                             int* __restrict__ si,
                                                             RowCtl* __restrict__ ctl,
-                                                            const TokOut* __restrict__ out,
+                                                            TokOut* __restrict__ out,
                                                             RunReport* __restrict__ rep, RunConst C,
-                                                            BeamRun B) {
+                                                            BeamRun B, PickIn pk) {
   extern __shared__ int smap[];  // [n][Tctx]: maps of the decoders others take over
   __shared__ RowRun sw[BA_MAXN];
+  __shared__ RowCtl s_ctl[BA_MAXN];  // this step's controls (ctl is rewritten below)
   __shared__ int s_smp[BA_MAXN], s_src[BA_MAXN], s_tok[BA_MAXN], s_need[BA_MAXN],
       s_own[BA_MAXN];
   __shared__ double s_csum[BA_MAXN];
@@ -719,7 +728,8 @@ __global__ __launch_bounds__(BA_T) void beam_advance_kernel(RowRun* __restrict__
   const int step = run_step[blockIdx.x];
   if (tid < n) {
     sw[tid] = run[r0 + tid];
-    s_smp[tid] = ctl[r0 + tid].sample;
+    s_ctl[tid] = ctl[r0 + tid];
+    s_smp[tid] = s_ctl[tid].sample;
     s_src[tid] = tid;
     s_need[tid] = 0;
   }
@@ -838,7 +848,13 @@ __global__ __launch_bounds__(BA_T) void beam_advance_kernel(RowRun* __restrict__
     run[r] = w;
     const int sl = step % C.nslot;
     RunReport o;
-    o.out = out[r];
+    const RowCtl k0 = s_ctl[tid];
+    if (pk.parts && k0.active && k0.sample) {  // (the step's lp_pick, here)
+      o.out = lp_pick_row(r, k0, pk.logits, pk.flt, pk.parts, pk.res, pk.C);
+      out[r] = o.out;
+    } else {
+      o.out = out[r];
+    }
     o.tok = tok;
     o.pos = w.fed;
     o.act = nx.active;
@@ -863,16 +879,17 @@ __global__ __launch_bounds__(64) void perf_empty_kernel() {}
 void launch_perf_empty(hipStream_t st) { perf_empty_kernel<<<1, 64, 0, st>>>(); }
 
 void row_advance(RowRun* run, int* run_step, const int* prompt, int* stepin, RowCtl* ctl,
-                 const TokOut* out, RunReport* rep, const RunConst& C, hipStream_t st) {
-  row_advance_kernel<<<1, 256, 0, st>>>(run, run_step, prompt, stepin, ctl, out, rep, C);
+                 TokOut* out, RunReport* rep, const RunConst& C, const PickIn& pk,
+                 hipStream_t st) {
+  row_advance_kernel<<<1, 256, 0, st>>>(run, run_step, prompt, stepin, ctl, out, rep, C, pk);
 }
 
 void beam_advance(RowRun* run, int* run_step, const int* prompt, int* stepin, RowCtl* ctl,
-                  const TokOut* out, RunReport* rep, const RunConst& C, const BeamRun& B,
-                  hipStream_t st) {
+                  TokOut* out, RunReport* rep, const RunConst& C, const BeamRun& B,
+                  const PickIn& pk, hipStream_t st) {
   const size_t lds = (size_t)B.n * B.Tctx * 4;
   beam_advance_kernel<<<C.R / B.n, BA_T, lds, st>>>(run, run_step, prompt, stepin, ctl, out, rep,
-                                                   C, B);
+                                                   C, B, pk);
 }
 
 

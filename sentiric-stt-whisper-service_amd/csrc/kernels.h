@@ -156,13 +156,20 @@ void layer_norm(const float* x, const float* w, const float* b, T* y, int M, int
 // Decode LayerNorm: as above, but y is written as decode-GEMM A tiles
 // (pack_index) and each thread owns 8 consecutive elements (N % 8 == 0,
 // N <= 2048).
+// EmbedIn (the first LayerNorm of a step): x is first formed as the token +
+// position embedding, x = te[tok[row]] + pe[pos[row]] (embed's arithmetic),
+// and written, so no separate embed launch precedes the layer stack.
+template <typename T>
+struct EmbedIn {
+  const T* te = nullptr;
+  const float* pe = nullptr;
+  const int* tok = nullptr;
+  const int* pos = nullptr;
+};
 template <typename T>
 void layer_norm_dec(float* x, const float* w, const float* b, T* y, int M, int N,
                     const int* active, hipStream_t st, const float* P, int KS,
-                    const float* pbias);
-template <typename T>
-void embed(const T* te, const float* pe, const int* tok, const int* pos, const int* active,
-           float* x, int R, int d, hipStream_t st);
+                    const float* pbias, const EmbedIn<T>& emb = EmbedIn<T>());
 
 
 // encoder self-attention: q,k [B][H][L][64], vt [B][H][64][L] f16 -> o [B*L][H*64] (T)
@@ -276,8 +283,29 @@ struct RunReport {
 };
 // empty one-wave kernel (timing-event overhead calibration, bench.py)
 void launch_perf_empty(hipStream_t st);
+struct LPPart;
+struct LPRes;
+struct LogitsConst {
+  int n_vocab;
+  int eot;
+  int beg;
+  int space_id;       // token id of " " (suppress_blank)
+  int suppress_blank;
+  int max_initial_tid;  // timestamps > beg + tid0 suppressed at the first step (-1: off)
+  int nosp_id;
+};
+// The step's logits-processing phase 3 (lp_pick) run inside the advance
+// kernel (parts != nullptr: logits_process was launched with pick = false)
+struct PickIn {
+  const float* logits = nullptr;
+  const float* flt = nullptr;
+  const LPPart* parts = nullptr;
+  const LPRes* res = nullptr;
+  LogitsConst C{};
+};
 void row_advance(RowRun* run, int* run_step, const int* prompt, int* stepin, RowCtl* ctl,
-                 const TokOut* out, RunReport* rep, const RunConst& C, hipStream_t st);
+                 TokOut* out, RunReport* rep, const RunConst& C, const PickIn& pk,
+                 hipStream_t st);
 
 struct Draw;
 // Run-ahead beam search: per clip (n decoders = rows r0 .. r0+n-1), the
@@ -305,18 +333,9 @@ struct BeamRun {
   Draw* drep;         // [nslot][R][KD] the step's draws, for the host replay
 };
 void beam_advance(RowRun* run, int* run_step, const int* prompt, int* stepin, RowCtl* ctl,
-                  const TokOut* out, RunReport* rep, const RunConst& C, const BeamRun& B,
-                  hipStream_t st);
+                  TokOut* out, RunReport* rep, const RunConst& C, const BeamRun& B,
+                  const PickIn& pk, hipStream_t st);
 
-struct LogitsConst {
-  int n_vocab;
-  int eot;
-  int beg;
-  int space_id;       // token id of " " (suppress_blank)
-  int suppress_blank;
-  int max_initial_tid;  // timestamps > beg + tid0 suppressed at the first step (-1: off)
-  int nosp_id;
-};
 // Logits processing is split over LP_G chunks of LP_CHUNK vocabulary entries
 // per row (LP_G * LP_CHUNK >= n_vocab for every Whisper vocabulary).
 constexpr int LP_G = 16;
@@ -336,9 +355,11 @@ struct LPScratch {
   LPPart* parts;  // [R][LP_G]
   LPRes* res;     // [R][LP_G]
 };
+// pick = false: phase 3 (lp_pick) is left to the run-ahead advance kernel
+// (PickIn)
 void logits_process(float* logits, const float* static_mask, const RowCtl* ctl, TokOut* out,
                     float* probs, float* logprobs, const LogitsConst& C, int R, LPScratch ws,
-                    hipStream_t st);
+                    hipStream_t st, bool pick = true);
 
 // std::discrete_distribution draws from the probs rows (k_misc.hip):
 // out[row][d] for d < ndraw[row] (<= KD <= 16), u[row][d] =
