@@ -277,11 +277,14 @@ __device__ __forceinline__ float dot8(const h2* q, f16x8 k) {
 }
 
 // sum over the 8 lanes of an aligned lane group (DPP: xor 1, xor 2 within a
-// quad, then the mirrored quad); every lane of the group gets the same value
+// quad, then the mirrored quad); every lane of the group gets the same value.
+// update_dpp with bound_ctrl (all sources valid: the same values as mov_dpp)
+// lets each step compile to one v_add_f32_dpp instead of a v_mov_b32_dpp and
+// a v_add_f32
 __device__ __forceinline__ float dpp_sum8(float d) {
-  d += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(d), 0xB1, 0xF, 0xF, false));
-  d += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(d), 0x4E, 0xF, 0xF, false));
-  d += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(d), 0x141, 0xF, 0xF, false));
+  d += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(d), 0xB1, 0xF, 0xF, true));
+  d += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(d), 0x4E, 0xF, 0xF, true));
+  d += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(d), 0x141, 0xF, 0xF, true));
   return d;
 }
 

@@ -131,9 +131,12 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 // combined as (r0 + r1) + (r2 + r3); every lane gets the result. A
 // ds_bpermute shuffle costs an LDS round trip per step (six per reduction,
 // twelve for a double); these cost a few cycles each.
+// (update_dpp with bound_ctrl: every lane of these row-local patterns has a
+// valid source, so the result is mov_dpp's, and the compiler can fold the
+// move into the consuming add / max as one v_*_dpp instruction)
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, true);
 }
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v) {
