@@ -69,6 +69,8 @@ for s in "$@"; do
     tsfull) run tsfull 600 python -u -m pytest tests/test_gpu_fulldepth.py -k "bench_workload" -m gpu -v -s -rf --timeout 600 --timeout-method thread ;;
     bench3l) run bench3l 600 python -u bench.py --lanes 3 --steps 9 --warmup 3 --no-cpu-baseline --no-one-lane ;;
     ptests) run ptests 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
+    tr8) run tr8 120 ./scripts/probe/tr8_probe ;;
+    mxtests) run mxtests 700 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shapes.py tests/test_gpu_prefill.py -k "mx or fp8" -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
     b5one) run b5one 500 python -u bench.py --beam 5 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
     bench1g16) run bench1g16 400 env MWX_GEMM_GROUP=16 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
     bench1g32) run bench1g32 400 env MWX_GEMM_GROUP=32 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;

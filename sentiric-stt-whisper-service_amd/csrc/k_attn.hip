@@ -623,7 +623,7 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
     const int* __restrict__ kv_index, const int* __restrict__ active, int n, int cap, int R,
     T* __restrict__ o, int H, float scale, unsigned long long* span = nullptr) {
   span_start(span);
-  __shared__ float sc[NQ][DEC_MAX_KEYS];
+  __shared__ __attribute__((aligned(16))) float sc[NQ][DEC_MAX_KEYS];
   __shared__ float redf[4][NQ];
   __shared__ double redd[4][NQ];
   __shared__ float pv[4][64][9];
@@ -977,9 +977,14 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
         return d < -126 ? 0.0f : __uint_as_float((uint32_t)(127 + d) << 23);
       };
       f16x8 pa[2];
+      // the lane's 8 weights in two 16-B reads (kb is a multiple of 8 and
+      // kb + 7 < 32 ceil(n / 32) <= DEC_MAX_KEYS; entries past n are
+      // replaced by 0 below)
+      const f32x4 pw0 = *reinterpret_cast<const f32x4*>(&sc[qrow][kb]);
+      const f32x4 pw1 = *reinterpret_cast<const f32x4*>(&sc[qrow][kb + 4]);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        float p = sc[qrow][min(kb + j, n - 1)];
+        float p = j < 4 ? pw0[j] : pw1[j - 4];
         if (mrow >= NQ || kb + j >= n) p = 0.0f;
         const uint32_t sp = (sv[j >> 1] >> (16 * (j & 1))) & 0xffffu;
         pa[0][j] = (_Float16)(p * pow2((int)(sp & 0xffu) - smax0));
@@ -988,14 +993,18 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
       const float tscale[2] = {e8m0((uint32_t)smax0), e8m0((uint32_t)smax1)};
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
-        const int e = 16 * nt + mrow;
-        uint32_t w0 = 0, w1 = 0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int r = 8 * gq + j;
-          const uint32_t b = vw[r * 64 + (e ^ (((r >> 3) & 3) * 16))];
-          if (j < 4) w0 |= b << (8 * j); else w1 |= b << (8 * (j - 4));
-        }
+        // the lane's B operand: column e = 16 nt + mrow of the tile's rows
+        // 8 gq .. 8 gq + 7 (their chunk nt ^ gq in the swizzled image), one
+        // byte per row, by a transposed LDS read: ds_read_b64_tr_b8 gives
+        // lane 16 g + i column i of the 8 rows whose 16-byte blocks the
+        // group's lanes 2 q + p address (row q, bytes 8 p .. 8 p + 7;
+        // mapping pinned on the GPU, scripts/probe/tr8_probe.hip). EXEC is
+        // all ones here (the tile loop is wave-uniform).
+        typedef int v2i_t __attribute__((ext_vector_type(2)));
+        const uint8_t* src = vw + (8 * gq + (mrow >> 1)) * 64 + ((nt ^ gq) * 16) + 8 * (mrow & 1);
+        const v2i_t tw = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
+            (__attribute__((address_space(3))) v2i_t*)(src));
+        const uint32_t w0 = (uint32_t)tw[0], w1 = (uint32_t)tw[1];
         const f16x8 vb = dequant_h8(uint2{w0, w1}, 127u);
         const f32x4 z = {0.0f, 0.0f, 0.0f, 0.0f};
         const f32x4 tp = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa[nt >> 1], vb, z, 0, 0, 0);
