@@ -150,8 +150,8 @@ __global__ __launch_bounds__(64 * QW) void enc_attn_kernel(const _Float16* __res
       for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) mx = fmaxf(mx, sacc[t][u][r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      mx = max_xor16(mx);
+      mx = max_xor32(mx);
       const float mnew = fmaxf(mrow[u], mx * scale_log2);
       // v_exp_f32 directly (exponents here are <= 0; the libm wrapper only
       // adds the denormal-range rescale, for results far below f16 resolution)
@@ -173,8 +173,8 @@ __global__ __launch_bounds__(64 * QW) void enc_attn_kernel(const _Float16* __res
           rs += ps[t][r];
           rs += ps[t][r + 1];
         }
-      rs += __shfl_xor(rs, 16, 64);
-      rs += __shfl_xor(rs, 32, 64);
+      rs = add_xor16(rs);
+      rs = add_xor32(rs);
       lrow[u] = lrow[u] * alpha + rs;
       mrow[u] = mnew;
 #pragma unroll
@@ -563,9 +563,9 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
 #undef LOADROWS0
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    acc[e] += __shfl_xor(acc[e], 8, 64);
-    acc[e] += __shfl_xor(acc[e], 16, 64);
-    acc[e] += __shfl_xor(acc[e], 32, 64);
+    acc[e] = add_xor8(acc[e]);
+    acc[e] = add_xor16(acc[e]);
+    acc[e] = add_xor32(acc[e]);
   }
   if (kg == 0) {
 #pragma unroll
@@ -969,10 +969,10 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
           smax1 = max(smax1, (int)(sp >> 8));
         }
       }
-      smax0 = max(smax0, __shfl_xor(smax0, 16, 64));
-      smax0 = max(smax0, __shfl_xor(smax0, 32, 64));
-      smax1 = max(smax1, __shfl_xor(smax1, 16, 64));
-      smax1 = max(smax1, __shfl_xor(smax1, 32, 64));
+      smax0 = max_xor16_i(smax0);
+      smax0 = max_xor32_i(smax0);
+      smax1 = max_xor16_i(smax1);
+      smax1 = max_xor32_i(smax1);
       auto pow2 = [](int d) {  // 2^d for d <= 0 (0 below 2^-126)
         return d < -126 ? 0.0f : __uint_as_float((uint32_t)(127 + d) << 23);
       };
@@ -1089,9 +1089,9 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       float a = acc[q][e];
-      a += __shfl_xor(a, 8, 64);
-      a += __shfl_xor(a, 16, 64);
-      a += __shfl_xor(a, 32, 64);
+      a = add_xor8(a);
+      a = add_xor16(a);
+      a = add_xor32(a);
       acc[q][e] = a;
     }
     if (kg == 0) {

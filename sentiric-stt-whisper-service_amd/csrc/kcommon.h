@@ -150,6 +150,40 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
   const uint64_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), lane);
   return __longlong_as_double((long long)((hi << 32) | lo));
 }
+// x (op) x-of-lane^m for m = 8, 16, 32 without an LDS round trip (the same
+// values as __shfl_xor, which compiles to ds_bpermute): m = 8 by DPP
+// row_ror:8 inside a 16-lane row; m = 16 / 32 by gfx950's row swaps
+// v_permlane16_swap / v_permlane32_swap, whose two results hold the lane's
+// own value and its partner's (in an order that depends on the row: the ops
+// used here are commutative, so the result is the same bits either way)
+__device__ __forceinline__ float add_xor8(float a) {
+  return a + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(a), 0x128, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float add_xor16(float a) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_int(a), __float_as_int(a), false, false);
+  return __int_as_float(r[0]) + __int_as_float(r[1]);
+}
+__device__ __forceinline__ float add_xor32(float a) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_int(a), __float_as_int(a), false, false);
+  return __int_as_float(r[0]) + __int_as_float(r[1]);
+}
+__device__ __forceinline__ float max_xor16(float a) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_int(a), __float_as_int(a), false, false);
+  return fmaxf(__int_as_float(r[0]), __int_as_float(r[1]));
+}
+__device__ __forceinline__ float max_xor32(float a) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_int(a), __float_as_int(a), false, false);
+  return fmaxf(__int_as_float(r[0]), __int_as_float(r[1]));
+}
+__device__ __forceinline__ int max_xor16_i(int a) {
+  const auto r = __builtin_amdgcn_permlane16_swap(a, a, false, false);
+  return max((int)r[0], (int)r[1]);
+}
+__device__ __forceinline__ int max_xor32_i(int a) {
+  const auto r = __builtin_amdgcn_permlane32_swap(a, a, false, false);
+  return max((int)r[0], (int)r[1]);
+}
+
 __device__ __forceinline__ double wave_sum_d_dpp(double v) {
   v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
   v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
