@@ -445,6 +445,9 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
   // scores (q.k in f32 over the f16 rows)
   auto score_batch = [&](const f16x8* kk, int bidx) {
     __builtin_amdgcn_sched_barrier(0);  // keep exactly one batch of loads ahead
+    // every lane of an 8-lane group holds the row's sum (dpp_sum8's steps are
+    // symmetric), so lane c stores row u = c: one LDS write per batch
+    float du = 0.0f;
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
       const int j = bidx * BR + wid * (8 * UB) + u * 8 + kg;
@@ -452,25 +455,50 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
       const bool isnew = SELF && min(j, n - 1) == jnew;
       float d = dot8(qh, isnew ? nkh : kk[u]);
       d = dpp_sum8(d);
-      if (c == 0 && j < n) sc[j] = d * scale;
+      du = (u == 0 || c == u) ? d : du;
     }
+    const int jc = bidx * BR + wid * (8 * UB) + c * 8 + kg;
+    if (c < UB && jc < n) sc[jc] = du * scale;
   };
   // softmax over the n scores in LDS (ggml order: f32 max, exp, double sum,
-  // P = f16(e * (float)(1/sum)))
+  // P = f16(e * (float)(1/sum))). Thread tid owns scores j = tid + 256 i (the
+  // order of its double sum), read once and kept in registers. P is written
+  // over the scores as packed f16 pairs pp[(j >> 4) * 8 + (j & 7)] =
+  // {P[j], P[j + 8]} (0 past n), the row pairs (u, u + 1) of pv_batch: key
+  // j + 8 is owned by lane ^ 8 (DPP row_ror:8), and the pair's lane with bit 3
+  // clear writes it (same f16 values as one read per row: bit-identical)
   auto softmax = [&]() {
+    constexpr int NI = DEC_MAX_KEYS / 256;
+    float sv[NI];
     __syncthreads();
     float mx = -INFINITY;
-    for (int j = tid; j < n; j += 256) mx = fmaxf(mx, sc[j]);
-    mx = block_max_256(mx, redf);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int j = tid + 256 * i;
+      sv[i] = j < n ? sc[j] : -INFINITY;
+      mx = fmaxf(mx, sv[i]);
+    }
+    mx = block_max_256(mx, redf);  // (its barriers order every score read before the P writes)
     double sum = 0.0;
-    for (int j = tid; j < n; j += 256) {
-      const float e = expf(sc[j] - mx);
-      sc[j] = e;
-      sum += (double)e;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      if (tid + 256 * i < n) {
+        const float e = expf(sv[i] - mx);
+        sv[i] = e;
+        sum += (double)e;
+      }
     }
     sum = block_sum_256d(sum, redd);
     const float inv = (float)(1.0 / sum);
-    for (int j = tid; j < n; j += 256) sc[j] = (float)f16r(sc[j] * inv);
+    h2* pp = reinterpret_cast<h2*>(sc);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int j = tid + 256 * i;
+      const _Float16 p = j < n ? f16r(sv[i] * inv) : (_Float16)0.0f;
+      const uint32_t own = (uint32_t)__builtin_bit_cast(uint16_t, p);
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)own, 0x128, 0xF, 0xF, true);
+      if ((tid & 8) == 0) pp[(j >> 4) * 8 + (j & 7)] = __builtin_bit_cast(h2, own | (hi << 16));
+    }
     __syncthreads();
   };
   float acc[8];
@@ -479,21 +507,23 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
   f16x8 nvh;
 #pragma unroll
   for (int e = 0; e < 8; ++e) nvh[e] = (_Float16)nv[e];
-  // P.V with v_dot2_f32_f16 over the lane's row pairs (u, u+1): acc[e] +=
-  // p_u*v_u[e] + p_u1*v_u1[e] (P is f16 exact, as ggml rounds it)
+  // P.V with v_dot2_f32_f16 over the lane's row pairs (u, u+1) = keys
+  // (j0, j0 + 8): acc[e] += p_u*v_u[e] + p_u1*v_u1[e] (P is f16 exact, as
+  // ggml rounds it), the pair one LDS read (0 past n)
+  static_assert(UB % 2 == 0, "row pairs");
+  const h2* ppr = reinterpret_cast<const h2*>(sc);
   auto pv_batch = [&](const f16x8* vv, int bidx) {
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < UB; u += 2) {
-      h2 ph;
+      const int j0 = bidx * BR + wid * (8 * UB) + u * 8 + kg;
+      // (pairs past DEC_MAX_KEYS / 2 are clamped: their rows are past n)
+      const h2 ph = ppr[min((j0 >> 4) * 8 + kg, DEC_MAX_KEYS / 2 - 1)];
       f16x8 r[2];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        const int j = bidx * BR + wid * (8 * UB) + (u + t) * 8 + kg;
+        const int j = j0 + 8 * t;
         const bool isnew = SELF && min(j, n - 1) == jnew;
-        float p = sc[min(j, n - 1)];  // (unconditional read: no exec-masked ds_read)
-        if (j >= n) p = 0.0f;          // p = 0 past the end
-        ph[t] = (_Float16)p;
         r[t] = isnew ? nvh : vv[u + t];
       }
 #pragma unroll
@@ -761,12 +791,17 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
     for (int uu = 0; uu < UH; ++uu) {
       const int u = half * UH + uu;
       const int j = bidx * 256 + wid * 64 + u * 8 + kg;
+      // every lane of the 8-lane group holds each query's sum (dpp_sum8's
+      // steps are symmetric), so lane c stores query c's score: one LDS
+      // write per key row instead of NQ
+      float dc = 0.0f;
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
         float d = dot8(qh[q], kk[uu]);
         d = dpp_sum8(d);
-        if (c == 0 && j < n) sc[q][j] = d * scale;
+        dc = (q == 0 || c == q) ? d : dc;
       }
+      if (c < NQ && j < n) sc[c][j] = dc * scale;
       __builtin_amdgcn_sched_barrier(0);  // one key row's conversions live at a time
     }
   };
@@ -875,12 +910,21 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
     }
   }
   __syncthreads();
-  // softmax per query (block_max_256 / block_sum_256d order)
+  // softmax per query (block_max_256 / block_sum_256d order). Thread tid owns
+  // scores j = tid + 256 i (the order of its double sum); they are read from
+  // LDS once and kept in registers through max, exp and P.
+  constexpr int NI = DEC_MAX_KEYS / 256;
+  float sv[NQ][NI];
   float mx[NQ];
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     float m = -INFINITY;
-    for (int j = tid; j < n; j += 256) m = fmaxf(m, sc[q][j]);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int j = tid + 256 * i;
+      sv[q][i] = j < n ? sc[q][j] : -INFINITY;
+      m = fmaxf(m, sv[q][i]);
+    }
     mx[q] = wave_max_dpp(m);
   }
   if (lane == 0)
@@ -894,10 +938,13 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     double sm = 0.0;
-    for (int j = tid; j < n; j += 256) {
-      const float e = expf(sc[q][j] - mx[q]);
-      sc[q][j] = e;
-      sm += (double)e;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      if (tid + 256 * i < n) {
+        const float e = expf(sv[q][i] - mx[q]);
+        sv[q][i] = e;
+        sm += (double)e;
+      }
     }
     sum[q] = wave_sum_d_dpp(sm);
   }
@@ -905,36 +952,33 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
 #pragma unroll
     for (int q = 0; q < NQ; ++q) redd[wid][q] = sum[q];
   __syncthreads();
-  // P = f16(e * (float)(1/sum)) (ggml order). The v_dot2 P.V below takes the
-  // weights of its row pairs (j, j + 8) as packed f16 pairs: P is written
-  // back over the scores as pp[q][(j >> 4) * 8 + (j & 7)] = {P[j], P[j + 8]}
-  // (0 past n), so each pair is one LDS read instead of two reads and three
-  // conversions (the same f16 values: bit-identical). The reads of a
-  // query's exps all precede the barrier before its pairs are written.
-  if constexpr (MFS && KV8) {
+  // P = f16(e * (float)(1/sum)) (ggml order), written over the scores (no
+  // thread reads a score after the barrier above). The v_dot2 P.V below takes
+  // the weights of its row pairs (j, j + 8) as packed f16 pairs,
+  // pp[q][(j >> 4) * 8 + (j & 7)] = {P[j], P[j + 8]} (0 past n), so each pair
+  // is one LDS read instead of two reads and three conversions (the same f16
+  // values: bit-identical). Key j + 8 is owned by lane ^ 8 (DPP row_ror:8),
+  // and the lane of the pair with bit 3 clear writes it.
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const double t = (redd[0][q] + redd[1][q]) + (redd[2][q] + redd[3][q]);
-      const float inv = (float)(1.0 / t);
-      for (int j = tid; j < n; j += 256) sc[q][j] = (float)f16r(sc[q][j] * inv);
-    }
-  } else {
-    constexpr int NPR = DEC_MAX_KEYS / 2 / 256;  // pairs per thread per query
+  for (int q = 0; q < NQ; ++q) {
+    const double t = (redd[0][q] + redd[1][q]) + (redd[2][q] + redd[3][q]);
+    const float inv = (float)(1.0 / t);
+    if constexpr (MFS && KV8) {
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const double t = (redd[0][q] + redd[1][q]) + (redd[2][q] + redd[3][q]);
-      const float inv = (float)(1.0 / t);
-      h2 pr[NPR];
-#pragma unroll
-      for (int i = 0; i < NPR; ++i) {
-        const int pi = tid + 256 * i, j0 = (pi >> 3) * 16 + (pi & 7), j1 = j0 + 8;
-        const float e0 = sc[q][min(j0, n - 1)], e1 = sc[q][min(j1, n - 1)];
-        pr[i] = h2{j0 < n ? f16r(e0 * inv) : (_Float16)0.0f, j1 < n ? f16r(e1 * inv) : (_Float16)0.0f};
+      for (int i = 0; i < NI; ++i) {
+        const int j = tid + 256 * i;
+        if (j < n) sc[q][j] = (float)f16r(sv[q][i] * inv);
       }
-      __syncthreads();
+    } else {
       h2* pp = reinterpret_cast<h2*>(&sc[q][0]);
 #pragma unroll
-      for (int i = 0; i < NPR; ++i) pp[tid + 256 * i] = pr[i];
+      for (int i = 0; i < NI; ++i) {
+        const int j = tid + 256 * i;
+        const _Float16 p = j < n ? f16r(sv[q][i] * inv) : (_Float16)0.0f;
+        const uint32_t own = (uint32_t)__builtin_bit_cast(uint16_t, p);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)own, 0x128, 0xF, 0xF, true);
+        if ((tid & 8) == 0) pp[(j >> 4) * 8 + (j & 7)] = __builtin_bit_cast(h2, own | (hi << 16));
+      }
     }
   }
   __syncthreads();
