@@ -412,8 +412,13 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
   }
   LOADROWS0(ka, K)
   // NBC: the second key batch is requested before the query is formed too,
-  // so two batches are in flight from the start
+  // so two batches are in flight from the start. SELF: value batch 0 is
+  // requested with key batch 0 (into kb2, which self does not use otherwise):
+  // the grid (rows x heads workgroups at <= 4 waves per SIMD) is resident
+  // at once, so the extra registers cost no occupancy, and the value rows no
+  // longer wait for the scores
   if constexpr (NBC > 0) LOADROWS(kb2, K, 1)
+  if constexpr (SELF) LOADROWS0(kb2, V)
   if (red) {
     float acc = pk[0];
 #pragma unroll
@@ -531,17 +536,19 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
     }
   };
   if constexpr (SELF) {
-    // <= 4 batches of 128 rows at UB = 4 (n <= 448): latency-bound, one batch
-    // per trip (loading V batch 0 together with K batch 0 measured 10% slower
-    // at UB = 8: occupancy 4 -> 3)
+    // <= 4 batches of 128 rows at UB = 4 (n <= 448): latency-bound, one key
+    // batch per trip; value batch 0 was requested with key batch 0 (at UB = 8
+    // that measured 10% slower: occupancy 4 -> 3), value batch 1 is requested
+    // before the softmax
     for (int b = 0; wave_busy && b < nb; ++b) {
       if (b > 0) LOADROWS(ka, K, b)
       score_batch(ka, b);
     }
-    LOADROWS0(ka, V)
+    if (wave_busy && nb > 1) LOADROWS(ka, V, 1)
     softmax();
-    for (int b = 0; wave_busy && b < nb; ++b) {
-      if (b > 0) LOADROWS(ka, V, b)
+    if (wave_busy) pv_batch(kb2, 0);
+    for (int b = 1; wave_busy && b < nb; ++b) {
+      if (b > 1) LOADROWS(ka, V, b)
       pv_batch(ka, b);
     }
   } else if constexpr (NBC > 0) {
