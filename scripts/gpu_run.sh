@@ -4,6 +4,7 @@
 # steps (each under its own time limit; the first failure ends the run):
 #   tests      pytest -m gpu (one process)
 #   smoke      __graft_entry__.smoke()
+#   abh / ab<commit>  2-lane bench of HEAD's / an older build's library (ablib/, built beforehand)
 #   bench      default bench line (C3: 2 lanes + one-lane value + CPU baseline)
 #   benchq     default bench without the CPU baseline (quick)
 #   bench1     C3 on one lane
@@ -51,6 +52,9 @@ run() {  # name, seconds, command...
 }
 for s in "$@"; do
   case $s in
+    ab*)  # A/B of builds on one box: ablib/libmwx_<build>.so, 2 lanes
+      v=${s#ab}; [ "$v" = h ] && v=head
+      run "${s}_$(date +%s)" 400 env MWX_LIB=$GRAFT_REPO_ROOT/ablib/libmwx_$v.so python -u bench.py --steps 12 --warmup 3 --no-cpu-baseline --no-one-lane ;;
     tests) run tests 1150 python -u -m pytest tests -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python -u bench.py --steps 20 --warmup 5 ;;

@@ -412,13 +412,14 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
   }
   LOADROWS0(ka, K)
   // NBC: the second key batch is requested before the query is formed too,
-  // so two batches are in flight from the start. SELF: value batch 0 is
-  // requested with key batch 0 (into kb2, which self does not use otherwise):
-  // the grid (rows x heads workgroups at <= 4 waves per SIMD) is resident
-  // at once, so the extra registers cost no occupancy, and the value rows no
-  // longer wait for the scores
+  // so two batches are in flight from the start
   if constexpr (NBC > 0) LOADROWS(kb2, K, 1)
-  if constexpr (SELF) LOADROWS0(kb2, V)
+  // Cross: the packed score stores and the register softmax with f16 P pairs
+  // (below). Self keeps one score store per row and the LDS softmax: with
+  // them (and with value batch 0 requested beside key batch 0) it was faster
+  // alone but cost the two-lane bench ~1.2 % (A/B on one box, 4 runs each,
+  // profiles/r04_ab_regression_beam.md)
+  constexpr bool SPACK = !SELF, SREG = !SELF;
   if (red) {
     float acc = pk[0];
 #pragma unroll
@@ -450,8 +451,8 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
   // scores (q.k in f32 over the f16 rows)
   auto score_batch = [&](const f16x8* kk, int bidx) {
     __builtin_amdgcn_sched_barrier(0);  // keep exactly one batch of loads ahead
-    // every lane of an 8-lane group holds the row's sum (dpp_sum8's steps are
-    // symmetric), so lane c stores row u = c: one LDS write per batch
+    // SPACK: every lane of an 8-lane group holds the row's sum (dpp_sum8's
+    // steps are symmetric), so lane c stores row u = c: one LDS write per batch
     float du = 0.0f;
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
@@ -460,19 +461,41 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
       const bool isnew = SELF && min(j, n - 1) == jnew;
       float d = dot8(qh, isnew ? nkh : kk[u]);
       d = dpp_sum8(d);
-      du = (u == 0 || c == u) ? d : du;
+      if constexpr (SPACK)
+        du = (u == 0 || c == u) ? d : du;
+      else if (c == 0 && j < n)
+        sc[j] = d * scale;
     }
-    const int jc = bidx * BR + wid * (8 * UB) + c * 8 + kg;
-    if (c < UB && jc < n) sc[jc] = du * scale;
+    if constexpr (SPACK) {
+      const int jc = bidx * BR + wid * (8 * UB) + c * 8 + kg;
+      if (c < UB && jc < n) sc[jc] = du * scale;
+    }
   };
   // softmax over the n scores in LDS (ggml order: f32 max, exp, double sum,
-  // P = f16(e * (float)(1/sum))). Thread tid owns scores j = tid + 256 i (the
-  // order of its double sum), read once and kept in registers. P is written
+  // P = f16(e * (float)(1/sum))). SREG: thread tid owns scores j = tid + 256 i
+  // (the order of its double sum), read once and kept in registers. P is written
   // over the scores as packed f16 pairs pp[(j >> 4) * 8 + (j & 7)] =
   // {P[j], P[j + 8]} (0 past n), the row pairs (u, u + 1) of pv_batch: key
   // j + 8 is owned by lane ^ 8 (DPP row_ror:8), and the pair's lane with bit 3
   // clear writes it (same f16 values as one read per row: bit-identical)
   auto softmax = [&]() {
+    if constexpr (!SREG) {
+      __syncthreads();
+      float mx = -INFINITY;
+      for (int j = tid; j < n; j += 256) mx = fmaxf(mx, sc[j]);
+      mx = block_max_256(mx, redf);
+      double sum = 0.0;
+      for (int j = tid; j < n; j += 256) {
+        const float e = expf(sc[j] - mx);
+        sc[j] = e;
+        sum += (double)e;
+      }
+      sum = block_sum_256d(sum, redd);
+      const float inv = (float)(1.0 / sum);
+      for (int j = tid; j < n; j += 256) sc[j] = (float)f16r(sc[j] * inv);
+      __syncthreads();
+      return;
+    }
     constexpr int NI = DEC_MAX_KEYS / 256;
     float sv[NI];
     __syncthreads();
@@ -523,7 +546,18 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
     for (int u = 0; u < UB; u += 2) {
       const int j0 = bidx * BR + wid * (8 * UB) + u * 8 + kg;
       // (pairs past DEC_MAX_KEYS / 2 are clamped: their rows are past n)
-      const h2 ph = ppr[min((j0 >> 4) * 8 + kg, DEC_MAX_KEYS / 2 - 1)];
+      h2 ph;
+      if constexpr (SREG) {
+        ph = ppr[min((j0 >> 4) * 8 + kg, DEC_MAX_KEYS / 2 - 1)];
+      } else {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int j = j0 + 8 * t;
+          float p = sc[min(j, n - 1)];
+          if (j >= n) p = 0.0f;
+          ph[t] = (_Float16)p;
+        }
+      }
       f16x8 r[2];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
@@ -536,19 +570,18 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
     }
   };
   if constexpr (SELF) {
-    // <= 4 batches of 128 rows at UB = 4 (n <= 448): latency-bound, one key
-    // batch per trip; value batch 0 was requested with key batch 0 (at UB = 8
-    // that measured 10% slower: occupancy 4 -> 3), value batch 1 is requested
-    // before the softmax
+    // <= 4 batches of 128 rows at UB = 4 (n <= 448): latency-bound, one batch
+    // per trip (loading V batch 0 together with K batch 0 measured 10% slower
+    // at UB = 8, occupancy 4 -> 3, and 1.2 % slower on the two-lane bench at
+    // UB = 4)
     for (int b = 0; wave_busy && b < nb; ++b) {
       if (b > 0) LOADROWS(ka, K, b)
       score_batch(ka, b);
     }
-    if (wave_busy && nb > 1) LOADROWS(ka, V, 1)
+    LOADROWS0(ka, V)
     softmax();
-    if (wave_busy) pv_batch(kb2, 0);
-    for (int b = 1; wave_busy && b < nb; ++b) {
-      if (b > 1) LOADROWS(ka, V, b)
+    for (int b = 0; wave_busy && b < nb; ++b) {
+      if (b > 0) LOADROWS(ka, V, b)
       pv_batch(ka, b);
     }
   } else if constexpr (NBC > 0) {
