@@ -52,6 +52,9 @@ run() {  # name, seconds, command...
 }
 for s in "$@"; do
   case $s in
+    abb*)  # the same for beam 5 (ablib/libmwx_<build>.so, 2 lanes)
+      v=${s#abb}; [ "$v" = h ] && v=head
+      run "${s}_$(date +%s)" 500 env MWX_LIB=$GRAFT_REPO_ROOT/ablib/libmwx_$v.so python -u bench.py --beam 5 --steps 4 --warmup 1 --no-cpu-baseline --no-one-lane ;;
     ab*)  # A/B of builds on one box: ablib/libmwx_<build>.so, 2 lanes
       v=${s#ab}; [ "$v" = h ] && v=head
       run "${s}_$(date +%s)" 400 env MWX_LIB=$GRAFT_REPO_ROOT/ablib/libmwx_$v.so python -u bench.py --steps 12 --warmup 3 --no-cpu-baseline --no-one-lane ;;
