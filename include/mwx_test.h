@@ -64,6 +64,14 @@ int mwx_test_decode_last(struct mwx_context* ctx, struct mwx_state* state, const
 int mwx_test_gemm_mx(struct mwx_context* ctx, int M, int N, int K, const float* a,
                      const float* w, float* c);
 
+/* The encoder FFN1 GEMM with its GELU epilogue on given data: a [M][K] and
+ * w [N][K] rounded to bf16 (bf16 != 0) or f16, bias [N]; out [M][N] =
+ * gelu_ggml(a.w + bias) in that type, widened to f32. use_table: the f16 GELU
+ * table looked up from LDS (the engine's path) or tanhf per output. N % 64 ==
+ * 0, K % 64 == 0. Returns 0 or <0. */
+int mwx_test_gemm_gelu(struct mwx_context* ctx, int M, int N, int K, const float* a,
+                       const float* w, const float* bias, int bf16, int use_table, float* out);
+
 /* std::discrete_distribution draws on the device (k_misc.hip sample_draws):
  * probs / logprobs [R][V], u [R][KD] (generate_canonical<double, 53> values),
  * ndraw [R] (<= KD <= 16); ids [R][KD] out. exact != 0 runs only the

@@ -111,6 +111,7 @@ struct Context {
   int device = 0;
   int cpad = 128;  // conv1 input channels padded (3*cpad % 64 == 0)
   void* arena = nullptr;
+  uint16_t* gelu_tab = nullptr;  // f16 GELU table (gelu_table_build), read by the encoder GELU GEMMs
   const float* d_filters = nullptr;
   const float* d_tables = nullptr;  // hann[400], cos[400], sin[400]
   const _Float16* conv1_w = nullptr;
@@ -707,6 +708,9 @@ static bool upload_model(Context& C, const ModelFile& mf) {
   HIPC(hipMalloc(&C.arena, A.host.size()));
   HIPC(hipMemcpy(C.arena, A.host.data(), A.host.size(), hipMemcpyHostToDevice));
   for (auto& f : A.fixups) *f.second = (const uint8_t*)C.arena + f.first;
+  HIPC(hipMalloc(&C.gelu_tab, GELU_TAB_N * sizeof(uint16_t)));
+  gelu_table_build(C.gelu_tab, nullptr);
+  HIPC(hipDeviceSynchronize());
   MWX_LOG_INFO("mwx: uploaded %.1f MB of weights to device %d\n", A.host.size() / 1048576.0,
                C.device);
   return true;
@@ -873,6 +877,7 @@ struct Driver {
     EpiParams e;
     // conv1 (k3 s1 p1) as a GEMM over overlapping rows of the padded window
     e.bias = C.conv1_b;
+    e.gelu_tab = C.gelu_tab;
     e.c16 = h1p + d;
     e.ldc = d;
     e.c_bstride = (long)(T2 + 2) * d;
@@ -935,6 +940,7 @@ struct Driver {
       layer_norm<T>(x, W.ln2_w, W.ln2_b, h, M, d, nullptr, st);
       e = EpiParams();
       e.bias = W.fc1_b;
+      e.gelu_tab = C.gelu_tab;
       e.c16 = ff;
       e.ldc = 4 * d;
       { PerfScope ps(S, "enc_gemm", st);

@@ -181,8 +181,15 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
   const TE* A = reinterpret_cast<const TE*>(Av);
   const TE* W = reinterpret_cast<const TE*>(Wv);
   // one __shared__ array only (a second one can make hipcc drain the LDS DMA
-  // before every ds_read): [stage][A rows 0..255 | W rows 0..255][128 B]
-  __shared__ __attribute__((aligned(16))) TE lds[NSTG][(BM + BN) * BKE];
+  // before every ds_read): [stage][A rows 0..255 | W rows 0..255][128 B].
+  // EPI_GELU: after the main loop, bytes [0, 64 KB) stage the outputs (8 waves
+  // x 64 rows x 64 columns of 16 bits) and the GELU table follows at GT_OFF
+  constexpr int RING_B = NSTG * (BM + BN) * BKE * (int)sizeof(TE);
+  constexpr int GT_OFF = 65536;
+  constexpr int LDS_B =
+      EPI == EPI_GELU ? (RING_B > GT_OFF + 2 * GELU_TAB_N ? RING_B : GT_OFF + 2 * GELU_TAB_N) : RING_B;
+  __shared__ __attribute__((aligned(16))) TE lds_raw[LDS_B / sizeof(TE)];
+  TE(*lds)[(BM + BN) * BKE] = reinterpret_cast<TE(*)[(BM + BN) * BKE]>(lds_raw);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / GWN, wn = wid % GWN;
   const int nbn = (N + BN - 1) / BN;
@@ -363,13 +370,68 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
     // Epilogue through LDS: the ring is idle now; each wave stages its 128x64
     // tile (16 KB) so every global store is a 16-B (8-B for V^T) vector.
     __builtin_amdgcn_s_barrier();  // all waves are past their last ring read
+    uint16_t* gtl = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(lds_raw) + GT_OFF);
+    if constexpr (EPI == EPI_GELU) {
+      if (P.gelu_tab) {  // (uniform) the table into LDS, 16 B per thread and step
+        for (int i = tid; i < GELU_TAB_N / 8; i += 512)
+          reinterpret_cast<uint4*>(gtl)[i] = reinterpret_cast<const uint4*>(P.gelu_tab)[i];
+        __syncthreads();
+      }
+    }
     if (wc0 >= N) {                // (N % 64 == 0: a wave's 64 columns are all in or all out)
       span_end(P.span);
       return;
     }
     uint16_t* wl = reinterpret_cast<uint16_t*>(&lds[0][0]) + wid * 8192;
     float* wlf = reinterpret_cast<float*>(wl);
-    if constexpr (STAGED16) {
+    if constexpr (EPI == EPI_GELU) {
+      // two 64-row halves of the wave tile through 8 KB of LDS per wave
+      uint16_t* wg = reinterpret_cast<uint16_t*>(&lds[0][0]) + wid * 4096;
+      auto half = [&](int hh, auto tabc) {
+        constexpr bool TB = decltype(tabc)::value;
+#pragma unroll
+        for (int i = hh * (GFM / 2); i < (hh + 1) * (GFM / 2); ++i)
+#pragma unroll
+          for (int j = 0; j < GFN; ++j) {
+            const int lc = j * 16 + (lane & 15);
+            const float bv = P.bias[wc0 + lc];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int lr = (i - hh * (GFM / 2)) * 16 + (lane >> 4) * 4 + r;
+              const float a = acc[i][j][r] + bv;
+              const float g = TB ? gelu_ggml_tab(a, gtl) : gelu_ggml(a);
+              uint16_t bits;
+              if constexpr (OUT16) {
+                bits = __builtin_bit_cast(uint16_t, (_Float16)g);
+              } else {
+                bits = __builtin_bit_cast(uint16_t, to_t<T>(g));
+              }
+              wg[lr * 64 + lc] = bits;
+            }
+          }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 4
+        for (int it = 0; it < 8; ++it) {
+          const int row = it * 8 + (lane >> 3), ch = lane & 7;
+          const int m = wr0 + hh * 64 + row;
+          if (m >= M) continue;
+          const uint4 v = *reinterpret_cast<const uint4*>(&wg[row * 64 + ch * 8]);
+          _Float16* dst = reinterpret_cast<_Float16*>(P.c16) + (long)bz * P.c_bstride +
+                          (long)m * P.ldc + wc0 + ch * 8;
+          *reinterpret_cast<uint4*>(dst) = v;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      };
+      if (P.gelu_tab) {
+        half(0, std::true_type{});
+        half(1, std::true_type{});
+      } else {
+        half(0, std::false_type{});
+        half(1, std::false_type{});
+      }
+    } else if constexpr (STAGED16) {
       // a wave's 64 columns are one head (d % 64 == 0): part / layer / head / k|v
       int part = 0, h = 0, layer = 0;
       if constexpr (EPI == EPI_ENC_QKV) {
@@ -393,16 +455,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
             const int lr = i * 16 + (lane >> 4) * 4 + r;
             const float a = acc[i][j][r];
             uint16_t bits;
-            if constexpr (EPI == EPI_GELU) {
-              const float g = gelu_ggml(a + P.bias[n]);
-              if constexpr (OUT16) {
-                const _Float16 hv = (_Float16)g;
-                bits = __builtin_bit_cast(uint16_t, hv);
-              } else {
-                const T tv = to_t<T>(g);
-                bits = __builtin_bit_cast(uint16_t, tv);
-              }
-            } else if constexpr (EPI == EPI_ENC_QKV) {
+            if constexpr (EPI == EPI_ENC_QKV) {
               const _Float16 hv = f16r(a + P.bias[n]);
               bits = __builtin_bit_cast(uint16_t, hv);
             } else {  // cross K: f16(acc * kscale); V: f16(acc + b)
@@ -455,10 +508,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
             }
           }
           _Float16* dst;
-          if constexpr (EPI == EPI_GELU) {
-            dst = reinterpret_cast<_Float16*>(P.c16) + (long)bz * P.c_bstride + (long)m * P.ldc +
-                  wc0 + ch * 8;
-          } else {
+          {
             const int b = m / P.L, t = m - b * P.L;
             if constexpr (EPI == EPI_ENC_QKV) {
               dst = (part == 0 ? P.q : P.k) + (((long)b * P.H + h) * P.L + t) * 64 + ch * 8;
@@ -538,6 +588,25 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
       }
     }
   span_end(P.span);
+}
+
+// the f16 GELU table (kernels.h GELU_TAB_*): gelu_ggml's expression for every
+// f16 input of magnitude <= 10, by the same device code
+__global__ void gelu_table_kernel(uint16_t* __restrict__ tab) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= GELU_TAB_N) return;
+  uint16_t out = 0;
+  if (i < 2 * GELU_TAB_HALF) {
+    const int neg = i >= GELU_TAB_HALF;
+    const uint16_t hb = (uint16_t)((i - neg * GELU_TAB_HALF) | (neg << 15));
+    const float xh = (float)__builtin_bit_cast(_Float16, hb);
+    out = __builtin_bit_cast(uint16_t, f16r(gelu_f32(xh)));
+  }
+  tab[i] = out;
+}
+
+void gelu_table_build(uint16_t* tab, hipStream_t st) {
+  gelu_table_kernel<<<(GELU_TAB_N + 255) / 256, 256, 0, st>>>(tab);
 }
 
 // ---------------------------------------------------------------------------

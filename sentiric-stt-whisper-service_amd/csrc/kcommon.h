@@ -82,6 +82,19 @@ __device__ __forceinline__ float gelu_ggml(float x) {
   return (float)f16r(gelu_f32(xh));
 }
 
+// gelu_ggml(x) by table lookup (gelu_table_build fills the table with the
+// f16(gelu_f32(h)) gelu_ggml computes for every f16 h with |h| <= 10): the
+// same value for every x (NaN passes through as in gelu_f32)
+template <typename TP>
+__device__ __forceinline__ float gelu_ggml_tab(float x, TP tab) {
+  if (x <= -10.0f) return 0.0f;
+  if (x >= 10.0f) return x;
+  if (x != x) return x;
+  const uint16_t hb = __builtin_bit_cast(uint16_t, f16r(x));
+  const int idx = (hb & 0x7fff) + (hb >> 15) * GELU_TAB_HALF;
+  return (float)__builtin_bit_cast(_Float16, tab[idx]);
+}
+
 // OCP MX-fp8 block rule (k_mx.hip, the cross K/V cache epilogue; host:
 // quant.cpp mx_quantize_row, oracle mx_round_rows): the E8M0 exponent of a
 // 32-element block is the smallest e with amax <= 448 * 2^e (no clipping);

@@ -59,7 +59,19 @@ struct EpiParams {
   // E8M0 scales (two per (time, head) row of 64)
   uint8_t* ks8 = nullptr;
   uint8_t* vs8 = nullptr;
+  // EPI_GELU in gemm_big's staged epilogue: the f16 GELU table
+  // (gelu_table_build), copied to LDS after the main loop and looked up
+  // instead of evaluating tanhf per output (the same values)
+  const uint16_t* gelu_tab = nullptr;
 };
+
+// f16 GELU table: entry i < GELU_TAB_HALF holds f16(gelu_f32(h)) (kcommon.h,
+// the expression gelu_ggml evaluates) for the f16 value h with bits i
+// (0 <= h <= 10), entry GELU_TAB_HALF + i the same for bits 0x8000 | i; padded
+// to a multiple of 8 entries
+constexpr int GELU_TAB_HALF = 0x4901;
+constexpr int GELU_TAB_N = (2 * GELU_TAB_HALF + 7) / 8 * 8;
+void gelu_table_build(uint16_t* tab, hipStream_t st);
 
 // The encoder GEMMs on MX-fp8 operands (e4m3 bytes + E8M0 scale per 32 k,
 // P.sa / P.sw): EPI_ENC_QKV, EPI_GELU (16-bit T output), EPI_RES, EPI_CROSS_KV.

@@ -550,6 +550,26 @@ class Context:
             raise RuntimeError("mwx_test_gemm_mx failed")
         return c
 
+    def test_gemm_gelu(self, a: np.ndarray, w: np.ndarray, bias: np.ndarray, bf16: bool,
+                       use_table: bool) -> np.ndarray:
+        """gelu_ggml(a @ w^T + bias) by the encoder FFN1 GEMM (gemm_big, staged
+        GELU epilogue), operands rounded to bf16 / f16; table lookup or tanhf."""
+        a = np.ascontiguousarray(a, dtype=np.float32)
+        w = np.ascontiguousarray(w, dtype=np.float32)
+        bias = np.ascontiguousarray(bias, dtype=np.float32)
+        M, K = a.shape
+        N = w.shape[0]
+        out = np.empty((M, N), np.float32)
+        fn = lib().mwx_test_gemm_gelu
+        fn.restype = C.c_int
+        fn.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_float),
+                       C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_int, C.c_int,
+                       C.POINTER(C.c_float)]
+        if fn(self.ctx, M, N, K, fptr(a), fptr(w), fptr(bias), int(bf16), int(use_table),
+              fptr(out)) != 0:
+            raise RuntimeError("mwx_test_gemm_gelu failed")
+        return out
+
     def test_encode(self, pcm: np.ndarray, seek: int = 0, cross: bool = True,
                     state_index: int = 0):
         pcm = np.ascontiguousarray(pcm, dtype=np.float32)

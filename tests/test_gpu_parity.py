@@ -626,6 +626,32 @@ def test_mx_gemm_exact(micro):
         # is not a plain f32 fma chain)
         assert err.max() < 5e-5, (M, N, K, err.max())
         assert err.mean() < 2e-6, (M, N, K, err.mean())
+def test_gemm_gelu_table_equals_tanhf(micro):
+    """The encoder FFN1 GEMM's GELU epilogue by the f16 table in LDS (the
+    engine's path) gives exactly the outputs of evaluating gelu_ggml (tanhf)
+    per output, for f16 and bf16 operands; pre-activations spread over
+    [-14, 14] cover the +-10 saturation edges and every f16 exponent in between.
+    Partial 256-row tiles included. A float64 GELU of the float64 product
+    bounds both (16-bit output rounding + the f16 input rounding)."""
+    ctx, _, _ = micro
+    rng = np.random.default_rng(11)
+    M, N, K = 300, 512, 256
+    a = rng.standard_normal((M, K)).astype(np.float32) * rng.uniform(0.001, 1.0, (M, 1)).astype(np.float32)
+    w = rng.standard_normal((N, K)).astype(np.float32) * 0.06
+    bias = rng.uniform(-12, 12, N).astype(np.float32)
+    for bf16 in (False, True):
+        t = ctx.test_gemm_gelu(a, w, bias, bf16, True)
+        d = ctx.test_gemm_gelu(a, w, bias, bf16, False)
+        assert np.array_equal(t.view(np.uint32), d.view(np.uint32)), (bf16, np.abs(t - d).max())
+        rnd = _bf16 if bf16 else (lambda x: x.astype(np.float16).astype(np.float32))
+        x = rnd(a).astype(np.float64) @ rnd(w).astype(np.float64).T + bias
+        g = 0.5 * x * (1 + np.tanh(np.sqrt(2 / np.pi) * x * (1 + 0.044715 * x * x)))
+        g = np.where(x <= -10, 0.0, np.where(x >= 10, x, g))
+        assert (np.abs(x) > 10).mean() > 0.05 and (np.abs(x) < 1).mean() > 0.05
+        err = np.abs(t - g) / np.maximum(np.abs(g), 1e-3)
+        assert err.max() < 2e-2, (bf16, err.max())
+
+
 def test_mxfp8_encoder_matches_mx_oracle(make_model):
     """MWX_COMPUTE_MXFP8: encoder and cross-K/V GEMMs on block-scaled fp8 MFMA.
     The oracle's ORC_MXFP8 mode applies the same MX rounding to the same
