@@ -862,6 +862,10 @@ def main():
 
     if rank == 0:
         roof, roof_enc = make_roofs(timed, args.steps)
+        if roof_enc is not None and lanes > 1:
+            roof_enc["note"] = ("spans of the encoder GEMMs while the other lanes' decode "
+                                "kernels share the CUs (the encoder runs on a low-priority "
+                                "stream); one_lane.roofline_encoder is the uncontended rate")
         roof_1lane = None
         if timed_1lane is not None:
             r1, e1 = make_roofs(timed_1lane, steps_1lane)
