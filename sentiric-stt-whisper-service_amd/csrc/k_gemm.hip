@@ -534,9 +534,24 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
         }
       }
     } else {
-      // f32 outputs (residual stream): two 64-row halves of the wave tile
+      // f32 outputs (residual stream): two 64-row halves of the wave tile.
+      // The half's residual (EPI_RES) / positional rows (EPI_CONV2) are
+      // requested before its staging, so their latency runs under it
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
+        f32x4 rin[16];
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+          const int row = it * 4 + (lane >> 4), ch = lane & 15;
+          const int m = wr0 + hh * 64 + row;
+          if (m < M) {
+            if constexpr (EPI == EPI_RES)
+              rin[it] = *reinterpret_cast<const f32x4*>(P.r32 + (long)bz * P.c_bstride +
+                                                         (long)m * P.ldc + wc0 + ch * 4);
+            else
+              rin[it] = *reinterpret_cast<const f32x4*>(P.pe + (long)m * P.ldc + wc0 + ch * 4);
+          }
+        }
 #pragma unroll
         for (int i = hh * (GFM / 2); i < (hh + 1) * (GFM / 2); ++i)
 #pragma unroll
@@ -552,7 +567,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
           }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll 4
+#pragma unroll
         for (int it = 0; it < 16; ++it) {
           const int row = it * 4 + (lane >> 4), ch = lane & 15;
           const int m = wr0 + hh * 64 + row;
@@ -560,13 +575,10 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
           const f32x4 v = *reinterpret_cast<const f32x4*>(&wlf[row * 64 + ch * 4]);
           const long idx = (long)bz * P.c_bstride + (long)m * P.ldc + wc0 + ch * 4;
           f32x4 o;
-          if constexpr (EPI == EPI_RES) {
-            const f32x4 res = *reinterpret_cast<const f32x4*>(P.r32 + idx);
-            o = v + res;  // (acc + bias) + residual
-          } else {
-            const f32x4 pe = *reinterpret_cast<const f32x4*>(P.pe + (long)m * P.ldc + wc0 + ch * 4);
-            o = pe + v;  // pe + gelu(acc + bias)
-          }
+          if constexpr (EPI == EPI_RES)
+            o = v + rin[it];  // (acc + bias) + residual
+          else
+            o = rin[it] + v;  // pe + gelu(acc + bias)
           *reinterpret_cast<f32x4*>(P.c32 + idx) = o;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
