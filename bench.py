@@ -903,7 +903,8 @@ def main():
                      + "; seeded weights in the ggml .bin layout)"),
             "config": {
                 "workload": (f"whisper-{args.arch}{' (-rich weights)' if args.rich else ''} "
-                             f"{args.wtype}: batches of {args.clips} x "
+                             f"{'MX-fp8 compute (from the ' + args.wtype + ' file)' if args.fp8 else args.wtype}"
+                             f": batches of {args.clips} x "
                              f"{args.clip_seconds:g} s clips per GPU ({lanes} in flight), mel + "
                              f"encoder + cross-KV + {args.decode_steps or 'until-EOT'} "
                              f"{'beam-%d' % args.beam if args.beam > 1 else 'greedy'} KV-cached "

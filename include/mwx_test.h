@@ -52,6 +52,11 @@ int mwx_test_dequantize(int type, const void* src, long n, float* dst);
 int mwx_test_decode_counters(struct mwx_state* state, long* steps, long* prefill_positions,
                              int reset);
 
+/* Run-ahead decode attempts a state redid on the host-driven token loop
+ * because the device's advance and the host's replay disagreed (or
+ * MWX_TEST_RA_MISMATCH=k forced it at step k). reset != 0 zeroes it. */
+long mwx_test_runahead_fallbacks(struct mwx_state* state, int reset);
+
 /* As mwx_test_decode, but only the logits of the last token are copied out
  * (logits_last [n_vocab]). */
 int mwx_test_decode_last(struct mwx_context* ctx, struct mwx_state* state, const int* tokens,

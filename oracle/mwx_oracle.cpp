@@ -34,6 +34,7 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <limits>
 #include <map>
 #include <random>
 #include <regex>
@@ -911,6 +912,51 @@ struct Result {
   std::vector<std::vector<int>> window_tokens;  // raw tokens of every window (debug)
 };
 
+// Decision trace (test hook, orc_trace_*): every float-sensitive decision
+// full() takes, in order, with the oracle-side margin by which it was taken.
+// Two runs on different logits (the oracle's own arithmetic and the device's
+// logits, replayed) agree up to their first differing event; that event's
+// margin against the measured logits error says whether the divergence is a
+// near-tie or a differing rule (tests/test_gpu_beam_oracle.py).
+enum TraceKind {
+  TR_DRAW = 1,      // discrete_distribution draw: a = draw index, b = id; margin = distance
+                    // of the uniform to the nearest cumulative boundary of id's interval
+  TR_ARGMAX = 2,    // greedy pick: b = id; margin = top-1 - top-2 logprob
+  TR_ASSIGN = 3,    // beam hand-over: a = source decoder, b = last token id; margin = the
+                    // smallest sum_logprobs_all gap to a neighbouring distinct candidate
+  TR_TSMASS = 4,    // timestamp-mass rule: a = forced; margin = |log sum p(ts) - max text logprob|
+  TR_BEST = 5,      // best decoder: a = id; margin = best score - runner-up score
+  TR_FALLBACK = 6,  // a = success; margin = distance of the deciding quantity to its threshold
+  TR_NOSPEECH = 7,  // window is_no_speech: a = value; margin as above
+  TR_EXACT_TIE = 8, // two DISTINCT beam candidates tied exactly on (sum_logprobs_all, decoder)
+                    // (upstream std::sort leaves their order unspecified: DESIGN §2 D5)
+  TR_STATUS = 9,    // decoder state after a step: a = completed + 2 failed, b = result_len
+};
+struct TraceEv {
+  int kind, seek, it, step, dec, a, b;
+  double margin, v;
+};
+static bool g_trace_on = false;
+static std::vector<TraceEv> g_trace;
+static struct { int seek = 0, it = 0, step = -1, dec = 0; } g_tctx;
+static void trace(int kind, int a, int b, double margin, double v = 0.0) {
+  if (g_trace_on)
+    g_trace.push_back({kind, g_tctx.seek, g_tctx.it, g_tctx.step, g_tctx.dec, a, b, margin, v});
+}
+// margin of a libstdc++ discrete_distribution draw: rng is the generator
+// state BEFORE the draw (its uniform is generate_canonical<double, 53>, the
+// search lower_bound over the normalised partial sums)
+static void trace_draw(const std::vector<float>& probs, std::mt19937 rng, int k, int id) {
+  if (!g_trace_on) return;
+  const double u = std::generate_canonical<double, std::numeric_limits<double>::digits>(rng);
+  double sum = 0.0;
+  for (float p : probs) sum += p;
+  double lo = 0.0;
+  for (int i = 0; i < id; ++i) lo += probs[i] / sum;
+  const double hi = lo + probs[id] / sum;
+  trace(TR_DRAW, k, id, std::min(u - lo, hi - u), u);
+}
+
 static const std::vector<std::string> kNonSpeech = {
     "\"", "#", "(", ")", "*", "+", "/", ":", ";", "<", "=", ">", "@", "[", "\\", "]", "^",
     "_", "`", "{", "|", "}", "~", "「", "」", "『", "』", "<<", ">>", "<<<", ">>>", "--",
@@ -1005,6 +1051,7 @@ static void process_logits(const Model& m, const Params& P, Decoder& dec, const 
       if (lse > 0.0f) ts_logprob = logf(lse) + lmax;
     }
     const float max_text = *std::max_element(dec.logprobs.begin(), dec.logprobs.begin() + m.beg);
+    trace(TR_TSMASS, ts_logprob > max_text, 0, fabs((double)ts_logprob - (double)max_text));
     if (ts_logprob > max_text) {
       for (int i = 0; i < m.beg; ++i) {
         logits[i] = -INFINITY;
@@ -1042,9 +1089,17 @@ static TokenData sample_token(const Model& m, Decoder& dec, bool best) {
         r.plog = lp[i];
       }
     }
+    if (g_trace_on) {
+      float second = -INFINITY;
+      for (int i = 0; i < n; ++i)
+        if (i != r.id && lp[i] > second) second = lp[i];
+      trace(TR_ARGMAX, 0, r.id, (double)r.plog - (double)second);
+    }
   } else {
     std::discrete_distribution<> dist(probs.begin(), probs.end());
+    const std::mt19937 before = dec.rng;
     r.id = dist(dec.rng);
+    trace_draw(probs, before, 0, r.id);
     r.p = probs[r.id];
     r.plog = lp[r.id];
   }
@@ -1083,7 +1138,9 @@ static std::vector<TokenData> sample_topk(const Model& m, Decoder& dec, int k) {
   std::vector<TokenData> out;
   for (int i = 0; i < k; ++i) {
     TokenData r;
+    const std::mt19937 before = dec.rng;
     r.id = dist(dec.rng);
+    trace_draw(probs, before, i, r.id);
     r.tid = tid;
     r.p = probs[r.id];
     r.plog = lp[r.id];
@@ -1112,6 +1169,7 @@ struct BeamCand {
   bool has_ts;
   Sequence seq;
 };
+
 
 static void sequence_score(const Params& P, Sequence& s) {
   if (s.result_len == 0) return;
@@ -1418,11 +1476,15 @@ static int full(const Model& m, Params P, const float* samples, int n_samples, R
   while (true) {
     if (seek + delta_min >= seek_end) break;
     encode_at(seek);
+    g_tctx.seek = seek;
     if (seek > seek_start && seek + 500 >= seek_end) prompt_past.clear();
     int best_id = 0;
     float no_speech_prob = 0.0f;
     for (int it = 0; it < (int)temps.size(); ++it) {
       const float t_cur = temps[it];
+      g_tctx.it = it;
+      g_tctx.step = -1;
+      g_tctx.dec = 0;
       int n_cur = 1;
       if (P.strategy == 0) {
         if (t_cur > 0.0f) n_cur = P.best_of;
@@ -1468,6 +1530,7 @@ static int full(const Model& m, Params P, const float* samples, int n_samples, R
       }
       const int n_max = P.bench_fixed_steps > 0 ? P.bench_fixed_steps : m.n_text_ctx / 2 - 4;
       for (int i = 0; i < n_max; ++i) {
+        g_tctx.step = i;
         if (P.strategy == 1) {
           // beam search: beam_size candidates per live decoder, sorted by
           // sum_logprobs_all (desc, then decoder index), assigned in order,
@@ -1477,26 +1540,56 @@ static int full(const Model& m, Params P, const float* samples, int n_samples, R
           for (int j = 0; j < n_cur; ++j) {
             auto& d = decs[j];
             if (d.completed || d.failed) continue;
+            g_tctx.dec = j;
             for (const auto& tok : sample_topk(m, d, P.beam_size)) {
               cands.push_back({j, d.seek_delta, d.has_ts, d.seq});
               cands.back().seq.tokens.push_back(tok);
               cands.back().seq.sum_logprobs_all += tok.plog;
             }
           }
-          // (upstream std::sort leaves candidates tied on both keys in an
-          // unspecified order; stable keeps their draw order: DESIGN §2 D5)
-          std::stable_sort(cands.begin(), cands.end(), [](const BeamCand& a, const BeamCand& b) {
+          // upstream std::sort: candidates tied on both keys come out in an
+          // unspecified order; the engine keeps their draw
+          // order. Such a tie between DISTINCT sequences is traced
+          // (TR_EXACT_TIE): where none occurs, the two orders agree.
+          std::sort(cands.begin(), cands.end(), [](const BeamCand& a, const BeamCand& b) {
             if (a.seq.sum_logprobs_all != b.seq.sum_logprobs_all)
               return a.seq.sum_logprobs_all > b.seq.sum_logprobs_all;
             return a.decoder_idx < b.decoder_idx;
           });
+          if (g_trace_on) {
+            for (size_t c = 1; c < cands.size(); ++c)
+              if (cands[c].seq.sum_logprobs_all == cands[c - 1].seq.sum_logprobs_all &&
+                  cands[c].decoder_idx == cands[c - 1].decoder_idx &&
+                  !tokens_equal(cands[c].seq, cands[c - 1].seq))
+                trace(TR_EXACT_TIE, cands[c].decoder_idx, cands[c].seq.tokens.back().id, 0.0);
+          }
+          // distance in sum_logprobs_all from candidate c to the nearest
+          // candidate before / after it that is a different sequence
+          auto assign_margin = [&](size_t c) {
+            double g = INFINITY;
+            for (size_t e = c; e-- > 0;)
+              if (!tokens_equal(cands[e].seq, cands[c].seq)) {
+                g = std::min(g, cands[e].seq.sum_logprobs_all - cands[c].seq.sum_logprobs_all);
+                break;
+              }
+            for (size_t e = c + 1; e < cands.size(); ++e)
+              if (!tokens_equal(cands[e].seq, cands[c].seq)) {
+                g = std::min(g, cands[c].seq.sum_logprobs_all - cands[e].seq.sum_logprobs_all);
+                break;
+              }
+            return g;
+          };
           size_t cur_c = 0;
           std::vector<int> src(n_cur, -1);
           for (int j = 0; j < n_cur; ++j) {
             auto& d = decs[j];
             if (d.completed || d.failed) continue;
             if (cur_c >= cands.size()) cur_c = 0;
+            const size_t cur_pos = cur_c;
             const BeamCand& cur = cands[cur_c++];
+            g_tctx.dec = j;
+            trace(TR_ASSIGN, cur.decoder_idx, cur.seq.tokens.back().id, assign_margin(cur_pos),
+                  cur.seq.sum_logprobs_all);
             while (cands.size() > cur_c && tokens_equal(cands[cur_c].seq, cur.seq) && i > 0) ++cur_c;
             d.seek_delta = cur.seek_delta;
             d.has_ts = cur.has_ts;
@@ -1512,6 +1605,7 @@ static int full(const Model& m, Params P, const float* samples, int n_samples, R
           for (int j = 0; j < n_cur; ++j) {
             auto& d = decs[j];
             if (d.completed || d.failed) continue;
+            g_tctx.dec = j;
             d.seq.tokens.push_back(sample_token(m, d, t_cur < 1e-6f));
             d.seq.sum_logprobs_all += d.seq.tokens.back().plog;
           }
@@ -1553,13 +1647,17 @@ static int full(const Model& m, Params P, const float* samples, int n_samples, R
           }
         }
         bool all = true;
-        for (int j = 0; j < n_cur; ++j)
+        for (int j = 0; j < n_cur; ++j) {
           if (!(decs[j].completed || decs[j].failed)) all = false;
+          g_tctx.dec = j;
+          trace(TR_STATUS, decs[j].completed + 2 * decs[j].failed, decs[j].seq.result_len, INFINITY);
+        }
         if (all) break;
         const int n_past = (int)prompt.size() + i;
         for (int j = 0; j < n_cur; ++j) {
           auto& d = decs[j];
           if (d.failed || d.completed) continue;
+          g_tctx.dec = j;
           const int tok = d.seq.tokens.back().id;
           if (ext) {
             std::vector<int> ctxt(prompt);
@@ -1587,11 +1685,27 @@ static int full(const Model& m, Params P, const float* samples, int n_samples, R
           best_id = j;
         }
       }
+      g_tctx.step = n_max;
+      g_tctx.dec = best_id;
+      if (g_trace_on) {
+        double runner = -INFINITY;
+        for (int j = 0; j < n_cur; ++j)
+          if (!decs[j].failed && j != best_id && !tokens_equal(decs[j].seq, decs[best_id].seq))
+            runner = std::max(runner, decs[j].seq.score);
+        trace(TR_BEST, best_id, decs[best_id].seq.result_len, best_score - runner, best_score);
+      }
       bool success = true;
       if (it != (int)temps.size() - 1) {
         const auto& d = decs[best_id];
         if (d.failed || (d.seq.avg_logprobs < P.logprob_thold && no_speech_prob < P.no_speech_thold))
           success = false;
+        if (g_trace_on) {
+          const double ga = (double)P.logprob_thold - d.seq.avg_logprobs;  // > 0: below
+          const double gn = (double)P.no_speech_thold - no_speech_prob;
+          trace(TR_FALLBACK, success, d.failed,
+                d.failed ? INFINITY : (success ? std::max(ga > 0 ? 0.0 : -ga, gn > 0 ? 0.0 : -gn)
+                                               : std::min(ga, gn)));
+        }
       }
       if (success) break;
     }
@@ -1606,6 +1720,12 @@ static int full(const Model& m, Params P, const float* samples, int n_samples, R
         R.window_tokens.push_back(ids);
       }
       const bool is_no_speech = no_speech_prob > P.no_speech_thold && best.seq.avg_logprobs < P.logprob_thold;
+      if (g_trace_on) {
+        const double gn = (double)no_speech_prob - P.no_speech_thold;  // > 0: above
+        const double ga = (double)P.logprob_thold - best.seq.avg_logprobs;
+        trace(TR_NOSPEECH, is_no_speech, 0,
+              is_no_speech ? std::min(gn, ga) : std::max(gn > 0 ? 0.0 : -gn, ga > 0 ? 0.0 : -ga));
+      }
       prompt_past.clear();
       if (prompt.front() == m.prev)
         prompt_past.insert(prompt_past.end(), prompt.begin() + 1, prompt.end() - prompt_init.size());
@@ -1714,6 +1834,27 @@ void orc_set_threads(int n) {
 #endif
 }
 void orc_set_enc_layer_limit(int n) { g_enc_layer_limit = n; }
+// decision trace (TraceKind above): on = 1 clears and starts recording
+void orc_trace_enable(int on) {
+  g_trace_on = on != 0;
+  if (on) g_trace.clear();
+}
+int orc_trace_count() { return (int)g_trace.size(); }
+// where full() stands (for an external-logits callback): {seek, it, step, dec}
+void orc_trace_ctx(int* out) {
+  out[0] = g_tctx.seek;
+  out[1] = g_tctx.it;
+  out[2] = g_tctx.step;
+  out[3] = g_tctx.dec;
+}
+// ints[7] = {kind, seek, it, step, dec, a, b}; dbls[2] = {margin, v}
+void orc_trace_get(int i, int* ints, double* dbls) {
+  const TraceEv& e = g_trace.at(i);
+  int v[7] = {e.kind, e.seek, e.it, e.step, e.dec, e.a, e.b};
+  for (int k = 0; k < 7; ++k) ints[k] = v[k];
+  dbls[0] = e.margin;
+  dbls[1] = e.v;
+}
 void orc_set_external(ExtEncodeFn enc, ExtLogitsFn lg, void* user) {
   g_ext_encode = enc;
   g_ext_logits = lg;

@@ -83,6 +83,10 @@ def lib() -> C.CDLL:
     L.orc_process_logits.restype = None
     L.orc_process_logits.argtypes = [P, fp, C.POINTER(C.c_int), C.c_int, C.c_int, C.c_int,
                                      C.POINTER(C.c_int), fp, fp, fp, fp, C.POINTER(C.c_int), fp]
+    L.orc_trace_enable.argtypes = [C.c_int]
+    L.orc_trace_count.restype = C.c_int
+    L.orc_trace_get.argtypes = [C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_double)]
+    L.orc_trace_ctx.argtypes = [C.POINTER(C.c_int)]
     L.orc_prosody.restype = None
     L.orc_prosody.argtypes = [fp, C.c_int64, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, P]
     L.orc_resample.restype = C.c_long
@@ -153,6 +157,47 @@ class FullOptions:
         return cls(strategy=0 if beam_size <= 1 else 1, best_of=5, beam_size=beam_size,
                    token_timestamps=True, suppress_nst=True, no_speech_thold=0.85,
                    entropy_thold=2.40, logprob_thold=-0.7, temperature=0.0, language="auto")
+
+
+TRACE_KINDS = {1: "draw", 2: "argmax", 3: "assign", 4: "ts_mass", 5: "best", 6: "fallback",
+               7: "no_speech", 8: "exact_tie", 9: "status"}
+
+
+@dataclass
+class TraceEv:
+    """One float-sensitive decision of full() (mwx_oracle.cpp TraceKind):
+    where it was taken (window seek, temperature index, step, decoder), what
+    was decided (a, b) and the oracle-side margin it was decided by."""
+    kind: str
+    seek: int
+    it: int
+    step: int
+    dec: int
+    a: int
+    b: int
+    margin: float
+    v: float
+
+    def key(self):
+        return (self.kind, self.seek, self.it, self.step, self.dec, self.a, self.b)
+
+
+def trace_ctx():
+    """(seek, temperature index, step, decoder) full() is at — read inside a
+    full_external logits callback: the logits it asks for feed that decoder's
+    decision at step + 1 (step -1: the prompt, shared by all decoders)."""
+    v = (C.c_int * 4)()
+    lib().orc_trace_ctx(v)
+    return tuple(v)
+
+
+def first_divergence(ta: List[TraceEv], tb: List[TraceEv]) -> Optional[int]:
+    """Index of the first event whose decision differs between two traces
+    (None if one is a prefix of the other and both have the same length)."""
+    for i, (x, y) in enumerate(zip(ta, tb)):
+        if x.key() != y.key():
+            return i
+    return None if len(ta) == len(tb) else min(len(ta), len(tb))
 
 
 class Oracle:
@@ -269,6 +314,22 @@ class Oracle:
                                  len(hist), int(has_ts), int(seek_delta), ip, fpv, _fp(lg),
                                  _fp(lp), _fp(pr), ti, tf)
         return lg, lp, pr, (ti[0], ti[1], tf[0], tf[1], tf[2], tf[3])
+
+    def traced(self, fn, *args, **kw):
+        """(fn(*args, **kw), [TraceEv]) with the decision trace recorded."""
+        L = lib()
+        L.orc_trace_enable(1)
+        try:
+            out = fn(*args, **kw)
+            evs = []
+            ints = (C.c_int * 7)()
+            dbl = (C.c_double * 2)()
+            for i in range(L.orc_trace_count()):
+                L.orc_trace_get(i, ints, dbl)
+                evs.append(TraceEv(TRACE_KINDS[ints[0]], *list(ints)[1:], dbl[0], dbl[1]))
+            return out, evs
+        finally:
+            L.orc_trace_enable(0)
 
     def full_external(self, pcm: np.ndarray, opt: FullOptions, encode_fn, logits_fn):
         """full() with every decode answered by callbacks: encode_fn(seek) and

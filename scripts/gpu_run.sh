@@ -72,9 +72,10 @@ for s in "$@"; do
     bench1g0) run bench1g0 400 env MWX_GEMM_GROUP=0 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
     beamtests) run beamtests 700 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shapes.py tests/test_gpu_prefill.py -k "beam" -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
     b5onenra) run b5onenra 500 env MWX_NO_RUNAHEAD=1 python -u bench.py --beam 5 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
-    beamra) run beamra 400 python -u -m pytest tests/test_gpu_parity.py -k "runahead" -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
+    beamra) run beamra 400 python -u -m pytest tests/test_gpu_parity.py -k "runahead or beam" -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
     tsfull) run tsfull 600 python -u -m pytest tests/test_gpu_fulldepth.py -k "bench_workload" -m gpu -v -s -rf --timeout 600 --timeout-method thread ;;
     bench3l) run bench3l 600 python -u bench.py --lanes 3 --steps 9 --warmup 3 --no-cpu-baseline --no-one-lane ;;
+    beamorc) run beamorc 900 python -u -m pytest tests/test_gpu_beam_oracle.py -m gpu -v -s -rf --timeout 800 --timeout-method thread ;;
     ptests) run ptests 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
     tr8) run tr8 120 ./scripts/probe/tr8_probe ;;
     mxtests) run mxtests 700 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shapes.py tests/test_gpu_prefill.py -k "mx or fp8" -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;

@@ -35,6 +35,32 @@ __global__ void empty_kernel(float* p) {
   if (p && threadIdx.x == 0 && blockIdx.x == 0x7fffffff) p[0] = 1.0f;
 }
 
+// launch-cost probes: an empty kernel's cost in a graph
+// chain against its grid size, its LDS allocation and its kernarg size, and the
+// cost of the dirty L2 lines a kernel leaves behind (end-of-kernel release)
+__global__ void empty_lds_kernel(float* p) {
+  extern __shared__ float lds[];
+  if (p && threadIdx.x == 0 && blockIdx.x == 0x7fffffff) p[0] = lds[0];
+}
+struct BigArg {
+  float v[256];  // 1 KB of kernel arguments
+};
+__global__ void empty_bigarg_kernel(BigArg a, float* p) {
+  if (p && threadIdx.x == 0 && blockIdx.x == 0x7fffffff) p[0] = a.v[threadIdx.x & 255];
+}
+// each workgroup stores 4 KB (256 lanes x 16 B): plain stores (dirty L2 lines)
+// or non-temporal stores
+typedef float f4v __attribute__((ext_vector_type(4)));
+template <bool NT>
+__global__ __launch_bounds__(256) void store_kernel(f4v* p) {
+  const f4v v = {1.0f, 2.0f, 3.0f, (float)blockIdx.x};
+  f4v* q = p + (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (NT)
+    __builtin_nontemporal_store(v, q);
+  else
+    *q = v;
+}
+
 __global__ void fill_kernel(uint16_t* p, size_t n, uint32_t seed) {
   size_t i = blockIdx.x * 256ull + threadIdx.x;
   for (; i < n; i += (size_t)gridDim.x * 256) {
@@ -357,6 +383,22 @@ int main(int argc, char** argv) {
   };
   std::vector<Op> ops = {
       {"empty 512 WG", 1, [&](int) { empty_kernel<<<512, 256, 0, s>>>(nullptr); }},
+      {"launch: empty 1 WG", 1, [&](int) { empty_kernel<<<1, 256, 0, s>>>(nullptr); }},
+      {"launch: empty 64 WG", 1, [&](int) { empty_kernel<<<64, 256, 0, s>>>(nullptr); }},
+      {"launch: empty 128 WG", 1, [&](int) { empty_kernel<<<128, 256, 0, s>>>(nullptr); }},
+      {"launch: empty 256 WG", 1, [&](int) { empty_kernel<<<256, 256, 0, s>>>(nullptr); }},
+      {"launch: empty 1024 WG", 1, [&](int) { empty_kernel<<<1024, 256, 0, s>>>(nullptr); }},
+      {"launch: empty 2048 WG", 1, [&](int) { empty_kernel<<<2048, 256, 0, s>>>(nullptr); }},
+      {"launch: empty 512 WG x 64 thr", 1, [&](int) { empty_kernel<<<512, 64, 0, s>>>(nullptr); }},
+      {"launch: empty 512 WG x 1024 thr", 1, [&](int) { empty_kernel<<<512, 1024, 0, s>>>(nullptr); }},
+      {"launch: empty 512 WG, 64 KB LDS", 1,
+       [&](int) { empty_lds_kernel<<<512, 256, 65536, s>>>(nullptr); }},
+      {"launch: empty 512 WG, 1 KB kernarg", 1,
+       [&](int) { empty_bigarg_kernel<<<512, 256, 0, s>>>(BigArg{}, nullptr); }},
+      {"launch: 40 WG store 160 KB", 1, [&](int) { store_kernel<false><<<40, 256, 0, s>>>((f4v*)slab2); }},
+      {"launch: 40 WG store 160 KB nt", 1, [&](int) { store_kernel<true><<<40, 256, 0, s>>>((f4v*)slab2); }},
+      {"launch: 640 WG store 2.6 MB", 1, [&](int) { store_kernel<false><<<640, 256, 0, s>>>((f4v*)slab2); }},
+      {"launch: 640 WG store 2.6 MB nt", 1, [&](int) { store_kernel<true><<<640, 256, 0, s>>>((f4v*)slab2); }},
       {"res_o (skinny RES K=d)", 1, [&](int l) { gemm_decode<T>(EPI_RES, od, wl(l, 1), R, d, d, ep_res(), s); }},
       {"res_fc2 (skinny RES K=4d)", 1,
        [&](int l) { gemm_decode<T>(EPI_RES, ffd, wl(l, 5), R, d, 4 * d, ep_res(), s); }},

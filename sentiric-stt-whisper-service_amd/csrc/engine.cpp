@@ -23,6 +23,7 @@
 #include <mutex>
 #include <random>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -215,6 +216,8 @@ struct State {
   // counters (mwx_test_decode_counters): decode steps launched, prompt
   // positions prefilled
   long n_steps = 0, n_prefill = 0;
+  // run-ahead attempts redone on the host loop (mwx_test_runahead_fallbacks)
+  long n_ra_fallback = 0;
   DBuf lpflt, lpparts, lpres;  // logits-processing scratch
   // beam search KV hand-over without copies: per row, positions below
   // kvown[row] are read from row kvmap[row][pos] (host copies in kvmap_h/kvown_h)
@@ -1146,6 +1149,8 @@ struct Driver {
       emb.pe = C.dec_pe;
       emb.tok = rw.tok;
       emb.pos = rw.pos;
+      emb.n_tok = V;
+      emb.n_pos = Tctx;
       c.embed = false;
     }
     layer_norm_dec<T>(c.xd, W.ln1_w, W.ln1_b, hd, n, d, rw.act, s, c.ks_prev ? rw.Pres : nullptr,

@@ -135,9 +135,11 @@ __global__ __launch_bounds__(256) void ln_dec_kernel(float* __restrict__ x,
   f32x4 xa, xc;
   if (emb.te) {
     // x = te[tok] + pe[pos] (ggml_get_rows(d_te) + ggml_get_rows(d_pe)), the ids first
+    const int tk = min(max(emb.tok[row], 0), emb.n_tok - 1);
+    const int ps = min(max(emb.pos[row], 0), emb.n_pos - 1);
     const typename Elt<T>::v8 er =
-        *reinterpret_cast<const typename Elt<T>::v8*>(emb.te + (long)emb.tok[row] * N + i0);
-    const float* pr = emb.pe + (long)emb.pos[row] * N + i0;
+        *reinterpret_cast<const typename Elt<T>::v8*>(emb.te + (long)tk * N + i0);
+    const float* pr = emb.pe + (long)ps * N + i0;
     const f32x4 pa = *reinterpret_cast<const f32x4*>(pr);
     const f32x4 pc = *reinterpret_cast<const f32x4*>(pr + 4);
 #pragma unroll

@@ -177,6 +177,9 @@ struct EmbedIn {
   const float* pe = nullptr;
   const int* tok = nullptr;
   const int* pos = nullptr;
+  // rows of te / pe: the gather runs before the inactive-row exit, so its
+  // indices are clamped (an inactive row may carry any token / position)
+  int n_tok = 1, n_pos = 1;
 };
 template <typename T>
 void layer_norm_dec(float* x, const float* w, const float* b, T* y, int M, int N,

@@ -213,6 +213,8 @@ def lib() -> C.CDLL:
     L.mwx_test_dequantize.argtypes = [C.c_int, C.c_void_p, C.c_long, C.POINTER(C.c_float)]
     L.mwx_test_decode_counters.restype = C.c_int
     L.mwx_test_decode_counters.argtypes = [P, C.POINTER(C.c_long), C.POINTER(C.c_long), C.c_int]
+    L.mwx_test_runahead_fallbacks.restype = C.c_long
+    L.mwx_test_runahead_fallbacks.argtypes = [P, C.c_int]
     L.mwx_test_set_xattn_mfs.restype = C.c_int
     L.mwx_test_set_xattn_mfs.argtypes = [C.c_int]
     u8p = C.POINTER(C.c_uint8)
@@ -604,6 +606,10 @@ class Context:
         lib().mwx_test_decode_counters(self.state(state_index), C.byref(st), C.byref(pf),
                                        1 if reset else 0)
         return st.value, pf.value
+
+    def runahead_fallbacks(self, state_index: int = 0, reset: bool = True) -> int:
+        """Run-ahead attempts redone on the host loop (mwx_test_runahead_fallbacks)."""
+        return lib().mwx_test_runahead_fallbacks(self.state(state_index), 1 if reset else 0)
 
     def test_xattn_mx(self, q: np.ndarray, k8: np.ndarray, ks: np.ndarray, v8: np.ndarray,
                       vs: np.ndarray, nq: int) -> np.ndarray:

@@ -1,0 +1,120 @@
+"""C5 at its benched size (BASELINE.json configs[4]: large-v3, fp8 weights on
+CDNA4's fp8 MFMA, beam 5, 10-min long-form): the full-depth model (32 + 32
+layers) in the engine's MX-fp8 compute mode (e4m3 operands with E8M0 scales per
+32 elements for the encoder / cross-K/V / decoder weight GEMMs and the cross
+K/V cache), which bench.py --fp8 --beam 5 --clip-seconds 600 times.
+
+The reference arithmetic for this mode is the oracle's ORC_MXFP8 mode (the
+same MX quantisation points, f32 elsewhere): the MX rounding of the operands is
+the oracle's, only the summation order differs. whisper.cpp has no fp8 path,
+so this mode is a declared deviation of the engine and its
+parity is against that restatement."""
+
+import numpy as np
+import pytest
+
+import mwx
+import orc
+from test_gpu_parity import pcm_clip
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(900)]
+
+BENCH_STEPS = 220
+
+
+@pytest.fixture(scope="module")
+def v3path(make_model):
+    return make_model("large-v3", mwx.GGML_BF16)
+
+
+def greedy_opt(steps):
+    opt = orc.FullOptions.service_defaults()
+    opt.temperature_inc = 0.0
+    opt.language = "en"
+    opt.bench_fixed_steps = steps
+    return opt
+
+
+def test_full_depth_mxfp8_teacher_forced_220_steps(v3path):
+    """The C5 model end to end on one bench window: the MX oracle's own
+    pipeline (its MX encoder, cross K/V and decoder) decodes 220 greedy steps
+    under bench_fixed_steps; along that stream the device's teacher-forced
+    logits (its fp8 encoder, cross cache and decoder) stay within the stated
+    tolerance, its argmax equals the oracle's token at every step whose oracle
+    top-1 margin exceeds 2 x err, and its free-running ids equal the oracle's
+    up to the first step inside that noise."""
+    omx = orc.Oracle(v3path, mxfp8=True)
+    pcm = pcm_clip(0)
+    _, osegs, _, _ = omx.full(pcm, greedy_opt(BENCH_STEPS))
+    oids = [t.id for s in osegs for t in s.tokens]
+    assert len(oids) == BENCH_STEPS
+    prompt = [omx.sot, omx.sot + 1, omx.transcribe]
+    toks = prompt + oids[:-1]
+    mel, _ = omx.mel(pcm)
+    k, v = omx.cross(omx.encode(mel))
+    lg_o = omx.decode_seq(k, v, toks)[len(prompt) - 1:]
+    with mwx.Context.open(v3path, compute=mwx.COMPUTE_MXFP8) as ctx:
+        p = ctx.default_params(mwx.SAMPLING_GREEDY)
+        p.language = b"en"
+        p.temperature_inc = 0.0
+        p.suppress_nst = True
+        p.token_timestamps = True
+        p.bench_fixed_steps = BENCH_STEPS
+        assert ctx.full(pcm, p, state_index=0) == 0
+        ids = [t.id for s in ctx.segments(0) for t in s.tokens]
+        ctx.test_encode(pcm, cross=False, state_index=1)
+        lg_d = ctx.test_decode(toks)[len(prompt) - 1:]
+    n_text = omx.eot
+    err = float(np.abs(lg_d[:, :n_text] - lg_o[:, :n_text]).max())
+    so = np.sort(lg_o[:, :n_text], axis=1)
+    m = so[:, -1] - so[:, -2]
+    agree = 0
+    for i in range(BENCH_STEPS):
+        pre, _, _, rec = omx.process_logits(lg_o[i], oids[:i], False, 3000, suppress_nst=True,
+                                            bench_fixed_steps=BENCH_STEPS)
+        assert rec[0] == oids[i]
+        if m[i] > 2 * err:
+            dmask = np.where(np.isneginf(pre), -np.inf, lg_d[i])
+            assert int(np.argmax(dmask)) == oids[i], (i, float(m[i]), err)
+            agree += 1
+    first = next((i for i, (a, b) in enumerate(zip(ids, oids)) if a != b), None)
+    print(f"full-depth large-v3 MX-fp8, {BENCH_STEPS} steps: logits err {err:.4f} (mean "
+          f"{float(np.abs(lg_d[:, :n_text] - lg_o[:, :n_text]).mean()):.4f}); oracle top-1 margin "
+          f"min {m.min():.4f} median {np.median(m):.4f}; teacher-forced argmax checked at {agree} "
+          f"steps; free-running ids equal up to step {BENCH_STEPS if first is None else first}")
+    # fp8 operand rounding over 32 + 32 layers: each MX GEMM's f32 summation
+    # order differs from the oracle's; bf16 full depth measures 0.142 (same
+    # test in bf16), the 2 + 2-layer fp8 test 0.09
+    assert err < 0.5, err
+    assert agree >= BENCH_STEPS // 2, agree
+    if first is not None:
+        assert m[first] <= 2 * err, (first, ids[first], oids[first], float(m[first]), err)
+
+
+def test_c5_bench_call_batch_equals_single(v3path):
+    """bench.py's own C5 call at full size — large-v3 MX-fp8, beam 5, 600-s
+    clips from device-resident PCM (20 windows each, bench_fixed_steps 220,
+    token timestamps on): 3 clips in one mwx_full_batch give, clip for clip,
+    the token records (id, t0, t1, p) of each clip decoded alone."""
+    n = 3
+    with mwx.Context.open(v3path, compute=mwx.COMPUTE_MXFP8) as ctx:
+        p = ctx.default_params(mwx.SAMPLING_BEAM_SEARCH)  # (bench.py main(), same fields)
+        p.beam_search.beam_size = 5
+        p.language = b"en"
+        p.temperature = 0.0
+        p.temperature_inc = 0.0
+        p.token_timestamps = True
+        p.suppress_nst = True
+        p.bench_fixed_steps = BENCH_STEPS
+        pcms = [mwx.pcm16_to_f32(mwx.synth_pcm16(k, 600 * 16000)) for k in range(n)]
+        for i in range(n + 1):
+            ctx.state(i)
+        dev = [ctx.upload(x) for x in pcms]
+        assert ctx.full_batch_device(dev, p, 0) == 0
+        batched = [ctx.token_records(c) for c in range(n)]
+        assert all(len(b) == 20 * BENCH_STEPS for b in batched), [len(b) for b in batched]
+        for c in range(n):
+            assert ctx.full_batch_device(dev[c:c + 1], p, n) == 0
+            assert ctx.token_records(n) == batched[c], c
+        for b in dev:
+            b.free()

@@ -626,6 +626,8 @@ def test_mx_gemm_exact(micro):
         # is not a plain f32 fma chain)
         assert err.max() < 5e-5, (M, N, K, err.max())
         assert err.mean() < 2e-6, (M, N, K, err.mean())
+
+
 def test_gemm_gelu_table_equals_tanhf(micro):
     """The encoder FFN1 GEMM's GELU epilogue by the f16 table in LDS (the
     engine's path) gives exactly the outputs of evaluating gelu_ggml (tanhf)
@@ -812,6 +814,36 @@ def test_beam_runahead_equals_host_loop(rich, temperature_inc, monkeypatch):
     print("tokens per clip:", [len(x) for x in ra])
     assert sum(len(x) for x in ra) > 20
     assert ra == host
+
+
+@pytest.mark.parametrize("beam,fault_step", [(5, 0), (5, 3), (1, 2)])
+def test_runahead_mismatch_falls_back_to_host_loop(rich, beam, fault_step, monkeypatch):
+    """A disagreement between the device's run-ahead advance and the host's
+    replay (forced at run-ahead step `fault_step` by MWX_TEST_RA_MISMATCH)
+    does not fail the request: the attempt is redone on the host-driven loop
+    and the batch's token records equal a run on the host loop throughout
+    (beam 5, the service default, and greedy)."""
+    ctx, _, _ = rich
+    p = service_params(ctx, beam=beam, temperature_inc=0.0, language=b"en")
+    pcms = [pcm_clip(60 + k, 11.0 + 6 * k) for k in range(3)]
+
+    def run():
+        base = len(ctx.states)
+        for i in range(3):
+            ctx.state(base + i)
+        ctx.runahead_fallbacks(base)
+        assert ctx.full_batch_states(pcms, p, range(base, base + 3)) == 0
+        return [ctx.token_records(base + i) for i in range(3)], ctx.runahead_fallbacks(base)
+
+    monkeypatch.setenv("MWX_NO_RUNAHEAD", "1")
+    host, n0 = run()
+    monkeypatch.delenv("MWX_NO_RUNAHEAD")
+    monkeypatch.setenv("MWX_TEST_RA_MISMATCH", str(fault_step))
+    redone, n1 = run()
+    print(f"beam {beam}, fault at step {fault_step}: {n1} attempt(s) redone on the host loop, "
+          f"{sum(len(x) for x in host)} tokens")
+    assert n0 == 0 and n1 >= 1
+    assert redone == host
 
 
 def _e4m3_encode(v):
