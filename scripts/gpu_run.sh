@@ -67,6 +67,8 @@ for s in "$@"; do
     c2nt) run c2nt 300 env MWX_XATTN_NT=1 python -u bench.py --arch base --wtype f16 --clips 1 --lanes 1 --steps 20 --warmup 3 --no-cpu-baseline ;;
     mfstest) run mfstest 600 env MWX_XATTN_MFS=1 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shapes.py -k "mxfp8" -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
     c5mfs) run c5mfs 700 env MWX_XATTN_MFS=1 python -u bench.py --fp8 --beam 5 --clip-seconds 600 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline ;;
+    c5onevd1) run c5onevd1 700 env MWX_XATTN_VD=1 python -u bench.py --fp8 --beam 5 --clip-seconds 600 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline ;;
+    vdtests) run vdtests 400 python -u -m pytest tests/test_gpu_parity.py -k "v_depth or mx_cross or mxfp8" -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
     c5one) run c5one 700 python -u bench.py --fp8 --beam 5 --clip-seconds 600 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline ;;
     bench1np) run bench1np 400 env MWX_PREFILL_MIN=0 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
     bench1g0) run bench1g0 400 env MWX_GEMM_GROUP=0 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
@@ -76,6 +78,10 @@ for s in "$@"; do
     tsfull) run tsfull 600 python -u -m pytest tests/test_gpu_fulldepth.py -k "bench_workload" -m gpu -v -s -rf --timeout 600 --timeout-method thread ;;
     bench3l) run bench3l 600 python -u bench.py --lanes 3 --steps 9 --warmup 3 --no-cpu-baseline --no-one-lane ;;
     beamorc) run beamorc 900 python -u -m pytest tests/test_gpu_beam_oracle.py -m gpu -v -s -rf --timeout 800 --timeout-method thread ;;
+    c5tests) run c5tests 1100 python -u -m pytest tests/test_gpu_c5.py -m gpu -v -s -rf --timeout 1000 --timeout-method thread ;;
+    probelaunch) for k in launch "empty 512" res_ splitk skinny ln_dec; do run "probe_$(echo $k | tr -d ' ')" 200 env PROBE_ONLY="$k" ./scripts/probe/dec_chain_probe 32 10 || exit 6; done ;;
+    stream) run stream 300 python -u bench.py --stream --arch base --wtype f16 --steps 3 --warmup 1 ;;
+    streamv3) run streamv3 400 python -u bench.py --stream --arch large-v3 --wtype bf16 --steps 2 --warmup 1 ;;
     ptests) run ptests 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
     tr8) run tr8 120 ./scripts/probe/tr8_probe ;;
     mxtests) run mxtests 700 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shapes.py tests/test_gpu_prefill.py -k "mx or fp8" -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
@@ -99,6 +105,14 @@ for s in "$@"; do
     pmcb5)  # instruction mix / stall counters of the beam-5 (and fp8) kernels
       (cd /tmp && run pmcb5 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d "$O/${TAG}_pmcb5" -o pmc -- $B --beam 5 --lanes 1 --steps 1 --warmup 0 --decode-steps 8 --no-cpu-baseline) || exit 5
       (cd /tmp && run pmcc5 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d "$O/${TAG}_pmcc5" -o pmc -- $B --fp8 --beam 5 --lanes 1 --steps 1 --warmup 0 --decode-steps 8 --no-cpu-baseline) || exit 5 ;;
+    pmcx)  # the grouped cross-attentions (beam 5 bf16, C5 MX-fp8): mix, LDS / MFMA / occupancy, FETCH
+      for leg in b5 c5; do
+        F=""; [ $leg = c5 ] && F="--fp8"
+        (cd /tmp && run pmcx_${leg}_mix 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d "$O/${TAG}_pmcx_${leg}_mix" -o pmc -- $B $F --beam 5 --lanes 1 --steps 1 --warmup 0 --decode-steps 8 --no-cpu-baseline) || exit 5
+        (cd /tmp && run pmcx_${leg}_lds 400 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d "$O/${TAG}_pmcx_${leg}_lds" -o pmc -- $B $F --beam 5 --lanes 1 --steps 1 --warmup 0 --decode-steps 8 --no-cpu-baseline) || exit 5
+        (cd /tmp && run pmcx_${leg}_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/${TAG}_pmcx_${leg}_fetch" -o pmc -- $B $F --beam 5 --lanes 1 --steps 1 --warmup 0 --decode-steps 8 --no-cpu-baseline) || exit 5
+        for x in mix lds fetch; do python3 scripts/pmc_mix.py "$O/${TAG}_pmcx_${leg}_$x" 12 > "$O/${TAG}_pmcx_${leg}_$x.md" || exit 5; done
+      done ;;
     pmc)
       for C in FETCH_SIZE WRITE_SIZE; do
         (cd /tmp && run pmc_$C 400 rocprofv3 --pmc $C --output-format csv -d "$O/${TAG}_pmc_$C" -o pmc -- $B --lanes 1 --steps 1 --warmup 0 --decode-steps 8 --no-cpu-baseline) || exit 5

@@ -21,6 +21,26 @@ def main():
             k = r["Kernel_Name"]
             acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
             disp[k].add(r["Dispatch_Id"])
+    key = "SQ_WAVE_CYCLES" if any("SQ_WAVE_CYCLES" in c for c in acc.values()) else None
+    if key is None:  # a pass without the SQ mix: every counter per dispatch
+        rows = sorted(acc.items(), key=lambda kv: -sum(kv[1].values()))[:top]
+        names = sorted({n for _, c in rows for n in c})
+        print("| kernel | dispatches | " + " | ".join(f"{n} / disp" for n in names) + " | derived |")
+        print("|---|---|" + "---|" * len(names) + "---|")
+        for k, c in rows:
+            n = len(disp[k])
+            der = []
+            if "FETCH_SIZE" in c:  # KiB per dispatch; gfx950 counts wide reads at half
+                der.append(f"fetch x2 {2 * c['FETCH_SIZE'] / n / 1024:.2f} MB")
+            if "SQ_LDS_BANK_CONFLICT" in c and c.get("SQ_LDS_IDX_ACTIVE"):
+                der.append(f"LDS conflict {c['SQ_LDS_BANK_CONFLICT'] / c['SQ_LDS_IDX_ACTIVE']:.3f}")
+            if "SQ_VALU_MFMA_BUSY_CYCLES" in c and c.get("GRBM_GUI_ACTIVE"):
+                der.append(f"MFMA busy {c['SQ_VALU_MFMA_BUSY_CYCLES'] / (1024 * c['GRBM_GUI_ACTIVE'] / 8):.3f}")
+            if "SQ_WAVES" in c and c.get("GRBM_GUI_ACTIVE"):
+                der.append(f"waves {c['SQ_WAVES'] / n:.0f}")
+            print(f"| `{k[:60]}` | {n} | " + " | ".join(f"{c.get(x, 0) / n:.4g}" for x in names)
+                  + " | " + "; ".join(der) + " |")
+        return
     rows = sorted(acc.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0))[:top]
     print("| kernel | dispatches | wave cycles / disp | wait (mem/barrier) | issue stall | VALU active | VALU insts / disp | LDS insts / disp |")
     print("|---|---|---|---|---|---|---|---|")

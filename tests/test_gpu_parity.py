@@ -926,3 +926,30 @@ def test_mx_cross_attention_kernel_vs_f64(micro, sharp):
           f"MFMA {errs[True]:.2e}, v_dot2 {errs[False]:.2e} (of max |o| per row)")
     assert errs[True] <= 3e-3 and errs[False] <= 3e-3, errs
     assert errs[True] <= 1.5 * errs[False] + 1e-4, errs
+
+
+@pytest.mark.parametrize("nq", [1, 5, 7])
+def test_mx_cross_attention_v_depth_bit_identical(micro, nq, monkeypatch):
+    """The MFMA MX-fp8 cross-attention keeps 4 V tiles per wave in flight
+    (round 5) instead of 1 (MWX_XATTN_VD=1, the round-4 kernel): only the
+    load schedule differs, so the outputs are bit-identical (1500 and 777
+    keys: a last tile group with fewer tiles than slots)."""
+    ctx, _, _ = micro
+    rng = np.random.default_rng(11 + nq)
+    H, G = 3, 2
+    R = G * nq
+    for n in (1500, 777):
+        rowscale = np.exp2(rng.uniform(-5, 3, size=(G, H, n, 1)))
+        k8, ks, _ = _mx_rows(rng.standard_normal((G, H, n, 64)) * 0.35 * rowscale)
+        v8, vs, _ = _mx_rows(rng.standard_normal((G, H, n, 64)) * rowscale)
+        q = (rng.standard_normal((R, H * 64)) * 0.5).astype(np.float32)
+        prev = mwx.set_xattn_mfs(True)
+        try:
+            monkeypatch.setenv("MWX_XATTN_VD", "1")
+            o1 = ctx.test_xattn_mx(q, k8, ks, v8, vs, nq)
+            monkeypatch.delenv("MWX_XATTN_VD")
+            o4 = ctx.test_xattn_mx(q, k8, ks, v8, vs, nq)
+        finally:
+            mwx.set_xattn_mfs(None if prev < 0 else bool(prev))
+        assert np.isfinite(o4).all()
+        assert np.array_equal(o1.view(np.uint32), o4.view(np.uint32)), (nq, n)
