@@ -82,6 +82,8 @@ for s in "$@"; do
     probelaunch) for k in launch "empty 512" res_ splitk skinny ln_dec; do run "probe_$(echo $k | tr -d ' ')" 200 env PROBE_ONLY="$k" ./scripts/probe/dec_chain_probe 32 10 || exit 6; done ;;
     stream) run stream 300 python -u bench.py --stream --arch base --wtype f16 --steps 3 --warmup 1 ;;
     streamv3) run streamv3 400 python -u bench.py --stream --arch large-v3 --wtype bf16 --steps 2 --warmup 1 ;;
+    g8tests) run g8tests 300 python -u -m pytest tests/test_gpu_parity.py -k "8phase or gemm_gelu or encoder_and_cross" -m gpu -v -s -rf --timeout 120 --timeout-method thread ;;
+    bench1g8) run bench1g8 400 env MWX_GEMM_8PH=1 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
     ptests) run ptests 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
     tr8) run tr8 120 ./scripts/probe/tr8_probe ;;
     mxtests) run mxtests 700 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shapes.py tests/test_gpu_prefill.py -k "mx or fp8" -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;

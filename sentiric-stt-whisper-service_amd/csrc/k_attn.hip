@@ -685,8 +685,7 @@ __device__ __forceinline__ f16x8 dequant_h8(uint2 raw, uint32_t e) {
 // sums). A query's scores depend only on its own row, so results do not depend
 // on the group size NQ. Each wave streams its tiles (wave w: w, w + 4, ...)
 // four at a time, two groups in flight. Softmax and P.V are the kernel's own.
-template <typename T, int NQ, bool KV8 = false, bool NTL = true, int NBC = 0, bool MFS = false,
-          int VD = 1>
+template <typename T, int NQ, bool KV8 = false, bool NTL = true, int NBC = 0, bool MFS = false>
 __global__ __launch_bounds__(256) void dec_xattn_kernel(
     const float* __restrict__ P, int KS, int pcols, const float* __restrict__ bias,
     const void* __restrict__ kbase, const void* __restrict__ vbase,
@@ -876,33 +875,29 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
   // in LDS (fp8 codes, 16-B chunks XOR-swizzled by (row >> 3) so a 32-lane
   // half's byte reads hit distinct banks) and reads each lane's B operand
   // (8 keys at one e) from there; the A operand is the query's P times the V
-  // scale of each key (per scale half), so the codes enter the MFMA unscaled.
-  // VD tiles per wave are in flight (slot s holds tiles w + 4 (s + VD i)):
-  // with one, each tile's load latency was exposed (the V pass ran at about a
-  // third of the K pass's rate)
+  // scale of each key (per scale half), so the codes enter the MFMA unscaled
   __shared__ __attribute__((aligned(16))) uint8_t vtile[MFS && KV8 ? 4 : 1][MFS && KV8 ? 32 * 64 : 16];
   const int nt32 = (n + 31) >> 5;
   const int vrow = lane >> 1, vch = 2 * (lane & 1);
-  // the tiles' bytes (rows vrow, chunks vch, vch + 1) and V scales per slot
-  u32x4 vr0[VD], vr1[VD], vsr[VD];
-  auto v_load = [&](int sl, int t) {
+  u32x4 vr0, vr1, vsr;  // the next tile's bytes (rows vrow, chunks vch, vch + 1) and V scales
+  auto v_load = [&](int t) {
     const u32x4* src = reinterpret_cast<const u32x4*>(V8 + (long)min(t * 32 + vrow, jmax) * 64) + vch;
-    vr0[sl] = ld_stream<NTL>(src);
-    vr1[sl] = ld_stream<NTL>(src + 1);
+    vr0 = ld_stream<NTL>(src);
+    vr1 = ld_stream<NTL>(src + 1);
     const int k0 = t * 32 + 8 * gq;  // scales of the lane's 8 A-operand keys
     if (k0 + 7 <= jmax) {
       // (two 8-B reads: a (slot, head)'s scale rows start 3000 B apart, so a
       // 16-B read here is only 8-B aligned)
       const u32x2 lo = *reinterpret_cast<const u32x2*>(VS8 + (long)k0 * 2);
       const u32x2 hi = *reinterpret_cast<const u32x2*>(VS8 + (long)k0 * 2 + 8);
-      vsr[sl] = u32x4{lo[0], lo[1], hi[0], hi[1]};
+      vsr = u32x4{lo[0], lo[1], hi[0], hi[1]};
     } else {
       uint32_t w[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         w[i] = (uint32_t)*reinterpret_cast<const uint16_t*>(VS8 + (long)min(k0 + 2 * i, jmax) * 2) |
                ((uint32_t)*reinterpret_cast<const uint16_t*>(VS8 + (long)min(k0 + 2 * i + 1, jmax) * 2) << 16);
-      vsr[sl] = u32x4{w[0], w[1], w[2], w[3]};
+      vsr = u32x4{w[0], w[1], w[2], w[3]};
     }
   };
   if constexpr (MFS) {
@@ -941,9 +936,7 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
         for (int i = 0; i < TD; ++i) score_tile(1, i, wid + 4 * (TD * (grp + 1) + i));
       }
     }
-#pragma unroll
-    for (int sl = 0; sl < VD; ++sl)  // (in flight across the softmax)
-      if (wid + 4 * sl < nt32) v_load(sl, wid + 4 * sl);
+    if (wid < nt32) v_load(wid);  // (in flight across the softmax)
   } else if constexpr (NBC > 0) {
 #pragma unroll 1
     for (int b = 0; b < NBC - 1; ++b) k_trip(b, false);
@@ -1037,18 +1030,14 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
     for (int i = 0; i < 4; ++i) oacc[i] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     const int qrow = min(mrow, NQ - 1);
 #pragma unroll 1
-    for (int t0 = wid; t0 < nt32; t0 += 4 * VD)
-#pragma unroll
-    for (int sl = 0; sl < VD; ++sl) {
-      const int t = t0 + 4 * sl;
-      if (t >= nt32) break;  // (wave-uniform)
+    for (int t = wid; t < nt32; t += 4) {
       {  // stage the tile (this wave's region only: in-order LDS, no barrier)
         const int sw = (vrow >> 3) & 3;
-        *reinterpret_cast<u32x4*>(vw + vrow * 64 + ((vch ^ sw) * 16)) = vr0[sl];
-        *reinterpret_cast<u32x4*>(vw + vrow * 64 + (((vch + 1) ^ sw) * 16)) = vr1[sl];
+        *reinterpret_cast<u32x4*>(vw + vrow * 64 + ((vch ^ sw) * 16)) = vr0;
+        *reinterpret_cast<u32x4*>(vw + vrow * 64 + (((vch + 1) ^ sw) * 16)) = vr1;
       }
-      const u32x4 sv = vsr[sl];
-      if (t + 4 * VD < nt32) v_load(sl, t + 4 * VD);
+      const u32x4 sv = vsr;
+      if (t + 4 < nt32) v_load(t + 4);
       // A operands: P'[q][key] = P x 2^(s(key, half) - smax(half)), keys
       // t*32 + 8(l>>4) + j, with smax the largest V scale exponent of the
       // tile's 32 keys in that half; the tile's product is scaled by
@@ -1250,17 +1239,11 @@ bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float*
   // xattn_mfs_set(0): the v_dot2 scores, the A/B: C5 one lane 735.8 -> 778.8
   // audio-s/s, 52.4 -> 44.6 us per launch)
   const bool mfs = xattn_mfs_on();
-  // V tiles in flight per wave of the MFMA path (MWX_XATTN_VD=1: one, the
-  // round-4 kernel, for A/B; read per launch so a test can compare both)
-  const bool vd1 = getenv("MWX_XATTN_VD") && atoi(getenv("MWX_XATTN_VD")) == 1;
   switch (nq) {
 #define XQ(N)                                  \
   case N:                                      \
-    if (kv8 && mfs && vd1)                     \
-      dec_xattn_kernel<T, N, true, true, 0, true, 1><<<g, 256, 0, st>>>(P, KS, pcols, bias, kbase, \
-          vbase, kscale8, vscale8, kv_index, active, n_keys, cap, R, o, H, scale, span);       \
-    else if (kv8 && mfs)                       \
-      dec_xattn_kernel<T, N, true, true, 0, true, 4><<<g, 256, 0, st>>>(P, KS, pcols, bias, kbase, \
+    if (kv8 && mfs)                            \
+      dec_xattn_kernel<T, N, true, true, 0, true><<<g, 256, 0, st>>>(P, KS, pcols, bias, kbase, \
           vbase, kscale8, vscale8, kv_index, active, n_keys, cap, R, o, H, scale, span);       \
     else if (kv8 && nt)                        \
       XL(N, true, true);                       \

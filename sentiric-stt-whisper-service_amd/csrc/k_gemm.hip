@@ -7,12 +7,12 @@
 // encoder, cross and decoder graphs — SURVEY.md §2.2 rows 2-11).
 //
 // Two kernels:
-//  * gemm_big:    128x128x64 tiles, 4 waves (2x2, 64x64 per wave), operands
-//                 staged through double-buffered LDS with an XOR swizzle (16-B
-//                 chunk ^= row & 7) so the ds_read_b128 fragment reads are
-//                 bank-conflict free; register-staged prefetch of tile k+1
-//                 during the MFMAs of tile k, one barrier per K tile.
-//                 Encoder / conv / cross-KV GEMMs (M = clips x 1500).
+//  * gemm_big:    256x256x64 tiles, 8 waves (2x4, 128x64 per wave), operands
+//                 DMA'd (global_load_lds) into double-buffered LDS with an XOR
+//                 swizzle (16-B chunk ^= (row >> 1) & 7) so the ds_read_b128
+//                 fragment reads are bank-conflict free; a 2-stage ring
+//                 (or an 8-phase schedule, MWX_GEMM_8PH=1). Encoder / conv / cross-KV GEMMs
+//                 (M = clips x 1500).
 //  * gemm_skinny: decode GEMMs (M <= 64 rows): weight-streaming, fragments
 //                 loaded straight to VGPRs (no LDS round trip), 4 waves split
 //                 K (or N for wide outputs), LDS reduction, one 16-column
@@ -160,7 +160,19 @@ constexpr int GFM = BM / GWM / 16, GFN = BN / GWN / 16;  // 8 x 4 fragments per 
 // 64 + 16*(l>>4) + [0,16) in bytes 16-31 -- exactly the 16-B chunks (l>>4)
 // and 4+(l>>4) of the row -- and its scale operand is that row's scale of
 // k block l>>4.
-template <typename T, int EPI, bool OUT16, bool MX = false>
+// PH8 (16-bit operands): the main loop as an 8-phase schedule (two 64-deep K
+// tiles per iteration, four phases per tile; MI355X guide §5 "256² 8-phase
+// template", T3 + T4): the waves of wave-row 1 run one barrier behind those
+// of wave-row 0, so on every SIMD one wave's 16-MFMA cluster overlaps the
+// other wave's LDS fragment reads and LDS-DMA issue. The LDS image of a K tile
+// is four half-tiles of 128 rows: HA0 / HA1 = the A rows of quadrant row 0 / 1
+// of both wave rows, HB0 / HB1 = the W rows of quadrant column 0 / 1 of all
+// four wave columns; each phase DMAs one half-tile (2 instructions per wave)
+// and waits with a counted vmcnt that keeps four half-tiles in flight. A
+// wave's quadrants are computed in the order (0,0), (0,1), (1,0), (1,1), each
+// output fragment still accumulating its K in the same order as the 2-stage
+// loop (tile by tile, 32-deep sub-steps 0, 1): bit-identical results.
+template <typename T, int EPI, bool OUT16, bool MX = false, bool PH8 = false>
 __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, long lda,
                                                    long a_bstride, const void* __restrict__ Wv,
                                                    long ldw, int M, int N, int K, EpiParams P) {
@@ -175,8 +187,12 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
   constexpr int RPI = 64 / CPR;                                  // rows per 1-KB DMA instruction
   constexpr int BKE = CPR * CE;                                  // K-tile depth (elements)
   constexpr int GDA = BM / RPI / 8, GDB = BN / RPI / 8;          // DMA instructions per wave per tile
-  // chunk swizzle: 16 consecutive rows read one chunk column conflict-free
-  auto swz = [](int row) { return CPR == 8 ? (row & 7) : ((row >> 2) & 3); };
+  // chunk swizzle: 16 consecutive rows read one chunk column conflict-free.
+  // 128-B rows: a 256-B bank row holds rows 2m and 2m + 1, so the slot is
+  // XORed with (row >> 1) & 7 -- rows 2m / 2m + 1 then take 16-B slots kc ^ m
+  // in the two halves of the bank row, 16 distinct slots for 16 rows (with
+  // (row & 7), rows r and r + 8 shared banks: 2-way conflicts on every read)
+  auto swz = [](int row) { return CPR == 8 ? ((row >> 1) & 7) : ((row >> 2) & 3); };
   span_start(P.span);
   const TE* A = reinterpret_cast<const TE*>(Av);
   const TE* W = reinterpret_cast<const TE*>(Wv);
@@ -222,7 +238,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
   A += (long)bz * a_bstride;
   // LDS DMA: one wave instruction fills 1 KB = 8 rows x 128 B of the tile
   // image linearly in lane order; the XOR swizzle (16-B chunk slot =
-  // kc ^ (row & 7), conflict-free fragment reads) is applied on the SOURCE
+  // kc ^ swz(row), conflict-free fragment reads) is applied on the SOURCE
   // address. Rows past M / N are clamped (their outputs are discarded).
   const int lr = lane / CPR, ls = lane % CPR;
   const TE* asrc[GDA];
@@ -270,6 +286,132 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
 #pragma unroll
     for (int j = 0; j < GFN; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
   const int nk = K / BKE;
+  if constexpr (PH8) {
+    static_assert(!MX && CPR == 8 && NSTG == 2, "8-phase schedule: 16-bit operands, 64-deep tiles");
+    constexpr int HT = 128 * 64;  // elements per half-tile (128 rows x 128 B)
+    // DMA sources: instruction i (0, 1) of this wave fills half-tile rows
+    // (2 wid + i) * 8 + lr; half-tile h: 0 = HA0, 1 = HA1, 2 = HB0, 3 = HB1
+    const TE* hs[4][2];
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int r = (wid * 2 + i) * 8 + lr, q = h & 1;
+        if (h < 2) {
+          const int gr = m0 + (r >> 6) * 128 + q * 64 + (r & 63);
+          hs[h][i] = A + (long)min(gr, M - 1) * lda + (ls ^ swz(r)) * CE;
+        } else {
+          const int gr = n0 + (r >> 5) * 64 + q * 32 + (r & 31);
+          hs[h][i] = W + (long)min(gr, N - 1) * ldw + (ls ^ swz(r)) * CE;
+        }
+      }
+    // stage s of the sequence: tile s / 4, half-tile HA0, HB0, HB1, HA1 by s % 4
+    // (K, the phase and the stage order are wave-uniform; H is compile-time)
+#define STAGE8(H, tile)                                                                     \
+    do {                                                                                    \
+      const int t_ = (tile);                                                                \
+      if (t_ < nk) {                                                                        \
+        _Pragma("unroll") for (int i = 0; i < 2; ++i) __builtin_amdgcn_global_load_lds(    \
+            (const void __attribute__((address_space(1)))*)(hs[H][i] + t_ * BKE),           \
+            (void __attribute__((address_space(3)))*)(&lds_raw[((t_ & 1) * 4 + (H)) * HT +  \
+                                                               (wid * 2 + i) * 8 * BKE]),   \
+            16, 0, 0);                                                                      \
+      }                                                                                     \
+    } while (0)
+    // outstanding stages allowed after phase P's wait: stages <= P + 2 must
+    // have landed (read from phase P + 1 on, after the barriers); issued so
+    // far: min(P + 7, 4 nk)
+    auto wait_stages = [&](int issued, int retire_upto) {
+      const int out = min(max(issued - (retire_upto + 1), 0), 4);
+      switch (out) {
+        case 4: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+      }
+    };
+    // prologue: tile 0 (all four) and tile 1's HA0 / HB0
+    STAGE8(0, 0);
+    STAGE8(2, 0);
+    STAGE8(3, 0);
+    STAGE8(1, 0);
+    STAGE8(0, 1);
+    STAGE8(2, 1);
+    wait_stages(min(6, 4 * nk), 1);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    // wave row 1 runs one barrier behind (a scalar branch: the condition is
+    // provably wave-uniform)
+    const bool lag = __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256;
+    if (lag) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    V8 af[2][4], b0[2][2], b1[2][2];
+    auto rd_a = [&](int h, int buf) {
+      const TE* base = &lds_raw[(buf * 4 + h) * HT];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int kc = s2 * 4 + (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = wm * 64 + i * 16 + (lane & 15);
+          af[s2][i] = *reinterpret_cast<const V8*>(base + row * BKE + ((kc ^ swz(row)) << 3));
+        }
+      }
+    };
+    auto rd_b = [&](V8 (&bb)[2][2], int h, int buf) {
+      const TE* base = &lds_raw[(buf * 4 + h) * HT];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int kc = s2 * 4 + (lane >> 4);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int row = wn * 32 + j * 16 + (lane & 15);
+          bb[s2][j] = *reinterpret_cast<const V8*>(base + row * BKE + ((kc ^ swz(row)) << 3));
+        }
+      }
+    };
+    auto mfma_q = [&](int qm, int qn, V8 (&bb)[2][2]) {
+      if (GEMM_PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[qm * 4 + i][qn * 2 + j] = Elt<T>::mfma(af[s2][i], bb[s2][j], acc[qm * 4 + i][qn * 2 + j]);
+      if (GEMM_PRIO) __builtin_amdgcn_s_setprio(0);
+    };
+    // one phase: fragment reads + one stage + counted wait | barrier |
+    // lgkmcnt(0) + the quadrant's 16 MFMAs | barrier
+#define PHASE8(PH, READS, SH, STILE, MF)                                  \
+    do {                                                                   \
+      READS;                                                               \
+      STAGE8(SH, STILE);                                                   \
+      wait_stages(min(phi + 7, 4 * nk), phi + 2);                          \
+      __builtin_amdgcn_sched_barrier(0);                                   \
+      __builtin_amdgcn_s_barrier();                                        \
+      __builtin_amdgcn_sched_barrier(0);                                   \
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                   \
+      MF;                                                                  \
+      __builtin_amdgcn_sched_barrier(0);                                   \
+      __builtin_amdgcn_s_barrier();                                        \
+      __builtin_amdgcn_sched_barrier(0);                                   \
+      ++phi;                                                               \
+    } while (0)
+    int phi = 0;  // phase index (4 per K tile)
+    for (int kt = 0; kt < nk; ++kt) {
+      const int buf = kt & 1;
+      PHASE8(0, (rd_a(0, buf), rd_b(b0, 2, buf)), 3, kt + 1, mfma_q(0, 0, b0));
+      PHASE8(1, rd_b(b1, 3, buf), 1, kt + 1, mfma_q(0, 1, b1));
+      PHASE8(2, rd_a(1, buf), 0, kt + 2, mfma_q(1, 0, b0));
+      PHASE8(3, (void)0, 2, kt + 2, mfma_q(1, 1, b1));
+    }
+#undef PHASE8
+#undef STAGE8
+    if (!lag) __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
 #pragma unroll
   for (int t = 0; t < NSTG - 1; ++t)
     if (t < nk) GLDS(t, t);
@@ -310,17 +452,17 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
 #pragma unroll
       for (int i = 0; i < GFM; ++i) {
         const int row = wm * (BM / GWM) + i * 16 + (lane & 15);
-        const uint4 lo = *reinterpret_cast<const uint4*>(&lds[cur][row * BKE + ((g ^ (row & 7)) << 4)]);
+        const uint4 lo = *reinterpret_cast<const uint4*>(&lds[cur][row * BKE + ((g ^ swz(row)) << 4)]);
         const uint4 hi =
-            *reinterpret_cast<const uint4*>(&lds[cur][row * BKE + (((4 + g) ^ (row & 7)) << 4)]);
+            *reinterpret_cast<const uint4*>(&lds[cur][row * BKE + (((4 + g) ^ swz(row)) << 4)]);
         af[i] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
       }
 #pragma unroll
       for (int j = 0; j < GFN; ++j) {
         const int row = BM + wn * (BN / GWN) + j * 16 + (lane & 15);
-        const uint4 lo = *reinterpret_cast<const uint4*>(&lds[cur][row * BKE + ((g ^ (row & 7)) << 4)]);
+        const uint4 lo = *reinterpret_cast<const uint4*>(&lds[cur][row * BKE + ((g ^ swz(row)) << 4)]);
         const uint4 hi =
-            *reinterpret_cast<const uint4*>(&lds[cur][row * BKE + (((4 + g) ^ (row & 7)) << 4)]);
+            *reinterpret_cast<const uint4*>(&lds[cur][row * BKE + (((4 + g) ^ swz(row)) << 4)]);
         bf[j] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
       }
 #pragma unroll
@@ -362,6 +504,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
     // this wave's reads of `cur` have returned before its next barrier
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
+  }  // (2-stage loop)
 #undef GLDS
   const int wr0 = m0 + wm * (BM / GWM), wc0 = n0 + wn * (BN / GWN);
   constexpr bool STAGED16 = EPI == EPI_GELU || EPI == EPI_ENC_QKV || EPI == EPI_CROSS_KV;
@@ -916,7 +1059,15 @@ static void gemm_dispatch(const T* A, long lda, long a_bstride, const T* W, long
   // weights per row tile; with the grouped order both take the remap)
   P.group_m = gemm_group_m();
   P.xcd_remap = xcd_remap_enabled() && (EPI != EPI_CROSS_KV || P.group_m > 0);
-  gemm_big<T, EPI, OUT16><<<g, 512, 0, st>>>(A, lda, a_bstride, W, ldw, M, N, K, P);
+  // MWX_GEMM_8PH=1: the 8-phase schedule (bit-identical; measured no faster
+  // than the 2-stage ring on the large-v3 encoder shapes: one lane 0.3633 vs
+  // 0.3647 of the dense peak, same box, r05f). Read per launch so a test can
+  // compare the two in one process.
+  const char* e8 = getenv("MWX_GEMM_8PH");
+  if (e8 && atoi(e8) == 1)
+    gemm_big<T, EPI, OUT16, false, true><<<g, 512, 0, st>>>(A, lda, a_bstride, W, ldw, M, N, K, P);
+  else
+    gemm_big<T, EPI, OUT16><<<g, 512, 0, st>>>(A, lda, a_bstride, W, ldw, M, N, K, P);
 }
 
 template <typename T>

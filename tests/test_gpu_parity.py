@@ -928,28 +928,39 @@ def test_mx_cross_attention_kernel_vs_f64(micro, sharp):
     assert errs[True] <= 1.5 * errs[False] + 1e-4, errs
 
 
-@pytest.mark.parametrize("nq", [1, 5, 7])
-def test_mx_cross_attention_v_depth_bit_identical(micro, nq, monkeypatch):
-    """The MFMA MX-fp8 cross-attention keeps 4 V tiles per wave in flight
-    (round 5) instead of 1 (MWX_XATTN_VD=1, the round-4 kernel): only the
-    load schedule differs, so the outputs are bit-identical (1500 and 777
-    keys: a last tile group with fewer tiles than slots)."""
+
+@pytest.mark.parametrize("M,N,K", [(300, 512, 64), (300, 512, 128), (513, 256, 192),
+                                   (256, 768, 1280), (1500, 1280, 5120)])
+def test_gemm_8phase_equals_2stage(micro, M, N, K, monkeypatch):
+    """The encoder GEMM's 8-phase main loop (MWX_GEMM_8PH=1) against the
+    2-stage loop (the default) on the same operands: bit-identical outputs
+    (every output fragment accumulates its K in the same order), for f16 and
+    bf16, K of 1 / 2 / 3 / 20 / 80 tiles (the prologue and the drained tail of
+    the stage pipeline) and partial 256-row tiles."""
     ctx, _, _ = micro
-    rng = np.random.default_rng(11 + nq)
-    H, G = 3, 2
-    R = G * nq
-    for n in (1500, 777):
-        rowscale = np.exp2(rng.uniform(-5, 3, size=(G, H, n, 1)))
-        k8, ks, _ = _mx_rows(rng.standard_normal((G, H, n, 64)) * 0.35 * rowscale)
-        v8, vs, _ = _mx_rows(rng.standard_normal((G, H, n, 64)) * rowscale)
-        q = (rng.standard_normal((R, H * 64)) * 0.5).astype(np.float32)
-        prev = mwx.set_xattn_mfs(True)
-        try:
-            monkeypatch.setenv("MWX_XATTN_VD", "1")
-            o1 = ctx.test_xattn_mx(q, k8, ks, v8, vs, nq)
-            monkeypatch.delenv("MWX_XATTN_VD")
-            o4 = ctx.test_xattn_mx(q, k8, ks, v8, vs, nq)
-        finally:
-            mwx.set_xattn_mfs(None if prev < 0 else bool(prev))
-        assert np.isfinite(o4).all()
-        assert np.array_equal(o1.view(np.uint32), o4.view(np.uint32)), (nq, n)
+    rng = np.random.default_rng(M + K)
+    a = rng.standard_normal((M, K)).astype(np.float32)
+    w = (rng.standard_normal((N, K)) / np.sqrt(K)).astype(np.float32)
+    bias = rng.uniform(-2, 2, N).astype(np.float32)
+    for bf16 in (False, True):
+        monkeypatch.delenv("MWX_GEMM_8PH", raising=False)
+        ref = ctx.test_gemm_gelu(a, w, bias, bf16, True)
+        monkeypatch.setenv("MWX_GEMM_8PH", "1")
+        out = ctx.test_gemm_gelu(a, w, bias, bf16, True)
+        assert np.array_equal(ref.view(np.uint32), out.view(np.uint32)), (bf16, np.abs(ref - out).max())
+
+
+@pytest.mark.parametrize("arch,wt", [("micro", mwx.GGML_F16), ("large-v3-l2", mwx.GGML_BF16),
+                                     ("base", mwx.GGML_F16)])
+def test_encoder_8phase_gemm_bit_identical(make_model, arch, wt, monkeypatch):
+    """Whole encoder (conv stem, every layer's QKV / out / FFN GEMMs with their
+    epilogues) and the all-layer cross-K/V GEMM: 8-phase == 2-stage, bit for bit."""
+    path = make_model(arch, wt)
+    pcm = pcm_clip(4, 30.0)
+    with mwx.Context.open(path) as ctx:
+        monkeypatch.delenv("MWX_GEMM_8PH", raising=False)
+        e0, k0, v0 = ctx.test_encode(pcm, state_index=0)
+        monkeypatch.setenv("MWX_GEMM_8PH", "1")
+        e1, k1, v1 = ctx.test_encode(pcm, state_index=1)
+    for x, y in ((e0, e1), (k0, k1), (v0, v1)):
+        assert np.array_equal(x.view(np.uint32), y.view(np.uint32)), float(np.abs(x - y).max())
