@@ -58,7 +58,7 @@ for s in "$@"; do
     ab*)  # A/B of builds on one box: ablib/libmwx_<build>.so, 2 lanes
       v=${s#ab}; [ "$v" = h ] && v=head
       run "${s}_$(date +%s)" 400 env MWX_LIB=$GRAFT_REPO_ROOT/ablib/libmwx_$v.so python -u bench.py --steps 12 --warmup 3 --no-cpu-baseline --no-one-lane ;;
-    tests) run tests 1150 python -u -m pytest tests -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
+    tests) run tests 1150 python -u -m pytest tests -m gpu -v -s -rf --timeout 600 --timeout-method thread ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python -u bench.py --steps 20 --warmup 5 ;;
     benchq) run benchq 400 python -u bench.py --steps 8 --warmup 2 --no-cpu-baseline ;;
@@ -86,6 +86,7 @@ for s in "$@"; do
     bench1g8) run bench1g8 400 env MWX_GEMM_8PH=1 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
     ptests) run ptests 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
     tr8) run tr8 120 ./scripts/probe/tr8_probe ;;
+    tr16) run tr16 120 ./scripts/probe/tr16_probe ;;
     mxtests) run mxtests 700 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shapes.py tests/test_gpu_prefill.py -k "mx or fp8" -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
     b5one) run b5one 500 python -u bench.py --beam 5 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
     bench1g16) run bench1g16 400 env MWX_GEMM_GROUP=16 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;

@@ -673,18 +673,18 @@ __device__ __forceinline__ f16x8 dequant_h8(uint2 raw, uint32_t e) {
   return f16x8{a[0], a[1], b[0], b[1], c[0], c[1], d[0], d[1]};
 }
 
-// MFS (MX-fp8 cache only, MWX_XATTN_MFS): the scores on MFMA instead of
-// v_dot2 chains. A 16-key tile is the A operand of two
+// MFS (MX-fp8 cache only, MWX_XATTN_MFS): scores and P.V on MFMA instead of
+// v_dot2 chains. Scores: a 16-key tile is the A operand of two chained
 // v_mfma_f32_16x16x32_f16 (one per 32-element scale half; lane l holds key
-// l&15's 8 codes at e = 8(l>>4) .. +7 of that half, widened to f16 unscaled:
-// e4m3 codes are f16-exact), the queries (f16, rows >= NQ zero) the B
-// operand; lane l receives query l&15's dot products with keys 4(l>>4) .. +3
-// of the tile per half, which the two E8M0 scales of each key combine:
-// score = (s0 * dot0 + s1 * dot1) * scale (scales are powers of two, so this
-// is the dot product of the dequantized values up to the order of the f32
-// sums). A query's scores depend only on its own row, so results do not depend
-// on the group size NQ. Each wave streams its tiles (wave w: w, w + 4, ...)
-// four at a time, two groups in flight. Softmax and P.V are the kernel's own.
+// l&15's 8 codes at e = 8(l>>4) .. +7 of that half, widened to f16 with that
+// key's half scale: exact, as in the v_dot2 path), the queries (f16, rows
+// >= NQ zero) the B operand; lane l receives query l&15's scores with keys
+// 4(l>>4) .. +3. P.V: the V tile staged in LDS as exactly widened f16, the
+// f16 P the A operand (below). A query's results depend only on its own row,
+// so they do not depend on the group size NQ. Each wave streams its key tiles
+// (wave w: w, w + 4, ...) four at a time, two groups in flight. Round 5: the
+// per-key scale arithmetic after the MFMAs (scores) and on P (P.V) cost ~2/3
+// of the kernel's VALU instructions (PMC, profiles/r05_pmc_xattn_raw.md).
 template <typename T, int NQ, bool KV8 = false, bool NTL = true, int NBC = 0, bool MFS = false>
 __global__ __launch_bounds__(256) void dec_xattn_kernel(
     const float* __restrict__ P, int KS, int pcols, const float* __restrict__ bias,
@@ -696,7 +696,11 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
   __shared__ __attribute__((aligned(16))) float sc[NQ][DEC_MAX_KEYS];
   __shared__ float redf[4][NQ];
   __shared__ double redd[4][NQ];
-  __shared__ float pv[4][64][9];
+  // the waves' P.V partials: [4][64][9] (v_dot2 path) or [4][NQ][64] (MFS,
+  // sized so three workgroups still fit a CU's LDS beside the f16 V tiles)
+  constexpr int PVN = MFS ? 4 * NQ * 64 : 4 * 64 * 9;
+  __shared__ float pvb[PVN];
+  auto pv = reinterpret_cast<float(*)[64][9]>(pvb);
   __shared__ float sq[NQ][64];
   const int g = blockIdx.y, h = blockIdx.x, row0 = g * NQ;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -768,34 +772,30 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
   // the bias is requested with the slabs (after the key loads, the query
   // would wait for them)
   const float bq = bias[h * 64 + (tid & 63)];
-  // MFS: key tiles in flight (TD tiles of 2 x 8 code bytes + 4 scale pairs)
+  // MFS: key tiles in flight (TD tiles of 2 x 8 code bytes + the scale pair
+  // of the lane's A-operand key)
   constexpr int TD = 4;
   const int ntile = (n + 15) >> 4;
   const int mrow = lane & 15, gq = lane >> 4;
   uint2 kr[MFS && KV8 ? 2 : 1][MFS && KV8 ? TD : 1][2];
-  uint32_t ksr[MFS && KV8 ? 2 : 1][MFS && KV8 ? TD : 1][2];
-  static_assert(!MFS || KV8, "MFMA scores: MX-fp8 caches only");
+  uint32_t ksr[MFS && KV8 ? 2 : 1][MFS && KV8 ? TD : 1];
+  f16x8 kh[MFS && !KV8 ? 2 : 1][MFS && !KV8 ? TD : 1][2];  // (f16 cache: the A operands as loaded)
   auto mfs_load = [&](int buf, int grp) {  // tiles wid + 4 * (TD * grp + i)
 #pragma unroll
     for (int i = 0; i < TD; ++i) {
       const int t = min(wid + 4 * (TD * grp + i), ntile - 1);
-      const uint8_t* row = K8 + (long)min(t * 16 + mrow, jmax) * 64 + 8 * gq;
-      const u32x2 a = ld_stream<NTL>(reinterpret_cast<const u32x2*>(row));
-      const u32x2 b = ld_stream<NTL>(reinterpret_cast<const u32x2*>(row + 32));
-      kr[buf][i][0] = uint2{a[0], a[1]};
-      kr[buf][i][1] = uint2{b[0], b[1]};
-      const int k0 = t * 16 + 4 * gq;  // the lane's 4 output keys (scale pairs)
-      if (k0 + 3 <= jmax) {
-        const u32x2 sp = *reinterpret_cast<const u32x2*>(KS8 + (long)k0 * 2);
-        ksr[buf][i][0] = sp[0];
-        ksr[buf][i][1] = sp[1];
+      const int key = min(t * 16 + mrow, jmax);
+      if constexpr (KV8) {
+        const uint8_t* row = K8 + (long)key * 64 + 8 * gq;
+        const u32x2 a = ld_stream<NTL>(reinterpret_cast<const u32x2*>(row));
+        const u32x2 b = ld_stream<NTL>(reinterpret_cast<const u32x2*>(row + 32));
+        kr[buf][i][0] = uint2{a[0], a[1]};
+        kr[buf][i][1] = uint2{b[0], b[1]};
+        ksr[buf][i] = *reinterpret_cast<const uint16_t*>(KS8 + (long)key * 2);
       } else {
-        uint32_t w[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          w[r] = *reinterpret_cast<const uint16_t*>(KS8 + (long)min(k0 + r, jmax) * 2);
-        ksr[buf][i][0] = w[0] | (w[1] << 16);
-        ksr[buf][i][1] = w[2] | (w[3] << 16);
+        const _Float16* row = K + (long)key * 64 + 8 * gq;
+        kh[buf][i][0] = ld_stream<NTL>(reinterpret_cast<const f16x8*>(row));
+        kh[buf][i][1] = ld_stream<NTL>(reinterpret_cast<const f16x8*>(row + 32));
       }
     }
   };
@@ -872,32 +872,31 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
     }
   };
   // MFS: P.V on MFMA as well. Wave w stages its 32-key V tiles (w, w + 4, ...)
-  // in LDS (fp8 codes, 16-B chunks XOR-swizzled by (row >> 3) so a 32-lane
-  // half's byte reads hit distinct banks) and reads each lane's B operand
-  // (8 keys at one e) from there; the A operand is the query's P times the V
-  // scale of each key (per scale half), so the codes enter the MFMA unscaled
-  __shared__ __attribute__((aligned(16))) uint8_t vtile[MFS && KV8 ? 4 : 1][MFS && KV8 ? 32 * 64 : 16];
+  // in LDS as f16, dequantized at staging: a lane's 32 codes are one half of
+  // one key row, so one E8M0 scale widens them exactly (the values are
+  // f16-representable, as in the v_dot2 path); the B operand (8 keys of one
+  // column) is two transposed 16-bit reads (ds_read_b64_tr_b16), and the A
+  // operand the query's f16 P itself (no per-key scale arithmetic). The
+  // 32-B column blocks of a row are XOR-swizzled by (row >> 1) & 3, so a
+  // 16-lane group's four rows hit distinct banks.
+  // (f16 cache: the lane's 32 values of row vrow are loaded as they are)
+  __shared__ __attribute__((aligned(16))) _Float16 vtile[MFS ? 4 : 1][MFS ? 32 * 64 : 8];
   const int nt32 = (n + 31) >> 5;
   const int vrow = lane >> 1, vch = 2 * (lane & 1);
-  u32x4 vr0, vr1, vsr;  // the next tile's bytes (rows vrow, chunks vch, vch + 1) and V scales
+  u32x4 vr0, vr1;  // the next tile's codes (row vrow, chunks vch, vch + 1)
+  uint32_t vse = 0;  // their E8M0 scale (row vrow, half lane & 1)
+  f16x8 vh[MFS && !KV8 ? 4 : 1];  // (f16 cache: row vrow, values 32 (lane & 1) .. + 31)
   auto v_load = [&](int t) {
-    const u32x4* src = reinterpret_cast<const u32x4*>(V8 + (long)min(t * 32 + vrow, jmax) * 64) + vch;
-    vr0 = ld_stream<NTL>(src);
-    vr1 = ld_stream<NTL>(src + 1);
-    const int k0 = t * 32 + 8 * gq;  // scales of the lane's 8 A-operand keys
-    if (k0 + 7 <= jmax) {
-      // (two 8-B reads: a (slot, head)'s scale rows start 3000 B apart, so a
-      // 16-B read here is only 8-B aligned)
-      const u32x2 lo = *reinterpret_cast<const u32x2*>(VS8 + (long)k0 * 2);
-      const u32x2 hi = *reinterpret_cast<const u32x2*>(VS8 + (long)k0 * 2 + 8);
-      vsr = u32x4{lo[0], lo[1], hi[0], hi[1]};
-    } else {
-      uint32_t w[4];
+    const int row = min(t * 32 + vrow, jmax);
+    if constexpr (KV8) {
+      const u32x4* src = reinterpret_cast<const u32x4*>(V8 + (long)row * 64) + vch;
+      vr0 = ld_stream<NTL>(src);
+      vr1 = ld_stream<NTL>(src + 1);
+      vse = VS8[(long)row * 2 + (lane & 1)];
+    } else if constexpr (MFS) {
+      const f16x8* src = reinterpret_cast<const f16x8*>(V + (long)row * 64 + 32 * (lane & 1));
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        w[i] = (uint32_t)*reinterpret_cast<const uint16_t*>(VS8 + (long)min(k0 + 2 * i, jmax) * 2) |
-               ((uint32_t)*reinterpret_cast<const uint16_t*>(VS8 + (long)min(k0 + 2 * i + 1, jmax) * 2) << 16);
-      vsr = u32x4{w[0], w[1], w[2], w[3]};
+      for (int i = 0; i < 4; ++i) vh[i] = ld_stream<NTL>(src + i);
     }
   };
   if constexpr (MFS) {
@@ -908,19 +907,26 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
       qb0[j] = mrow < NQ ? (_Float16)sq[min(mrow, NQ - 1)][8 * gq + j] : (_Float16)0.0f;
       qb1[j] = mrow < NQ ? (_Float16)sq[min(mrow, NQ - 1)][32 + 8 * gq + j] : (_Float16)0.0f;
     }
-    auto e8m0 = [](uint32_t e) { return e ? __uint_as_float(e << 23) : __uint_as_float(0x00400000u); };
+    // each lane widens its A-operand key's codes with that key's two
+    // scales (one per 32-element half; exact in f16, as the v_dot2 path
+    // widens them), and the two halves chain in one accumulator
     auto score_tile = [&](int buf, int i, int t) {
       f32x4 out;
-      if constexpr (KV8) {
-        const f16x8 a0 = dequant_h8(kr[buf][i][0], 127u), a1 = dequant_h8(kr[buf][i][1], 127u);
-        const f32x4 z = {0.0f, 0.0f, 0.0f, 0.0f};
-        const f32x4 d0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, qb0, z, 0, 0, 0);
-        const f32x4 d1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, qb1, z, 0, 0, 0);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const uint32_t sp = (ksr[buf][i][r >> 1] >> (16 * (r & 1))) & 0xffffu;
-          out[r] = (e8m0(sp & 0xffu) * d0[r] + e8m0(sp >> 8) * d1[r]) * scale;
+      {
+        f16x8 a0, a1;
+        if constexpr (KV8) {
+          const uint32_t sp = ksr[buf][i];
+          a0 = dequant_h8(kr[buf][i][0], sp & 0xffu);
+          a1 = dequant_h8(kr[buf][i][1], sp >> 8);
+        } else {
+          a0 = kh[buf][i][0];
+          a1 = kh[buf][i][1];
         }
+        const f32x4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+        f32x4 d = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, qb0, z, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, qb1, d, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[r] = d[r] * scale;
       }
       if (mrow < NQ && t < ntile)
         *reinterpret_cast<f32x4*>(&sc[min(mrow, NQ - 1)][t * 16 + 4 * gq]) = out;
@@ -1003,11 +1009,14 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
   for (int q = 0; q < NQ; ++q) {
     const double t = (redd[0][q] + redd[1][q]) + (redd[2][q] + redd[3][q]);
     const float inv = (float)(1.0 / t);
-    if constexpr (MFS && KV8) {
+    if constexpr (MFS) {
+      // f16 P over the score row's storage (zeros past n: the A operand of
+      // the last tile reads whole 8-key groups)
+      _Float16* ph = reinterpret_cast<_Float16*>(&sc[q][0]);
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
         const int j = tid + 256 * i;
-        if (j < n) sc[q][j] = (float)f16r(sv[q][i] * inv);
+        ph[j] = j < n ? f16r(sv[q][i] * inv) : (_Float16)0.0f;
       }
     } else {
       h2* pp = reinterpret_cast<h2*>(&sc[q][0]);
@@ -1022,82 +1031,66 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
     }
   }
   __syncthreads();
-  if constexpr (MFS && KV8) {
-    auto e8m0 = [](uint32_t e) { return e ? __uint_as_float(e << 23) : __uint_as_float(0x00400000u); };
-    uint8_t* vw = &vtile[0][0] + wid * (32 * 64);
+  if constexpr (MFS) {
+    _Float16* vw = &vtile[0][0] + wid * (32 * 64);
     f32x4 oacc[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) oacc[i] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     const int qrow = min(mrow, NQ - 1);
+    const _Float16* prow = reinterpret_cast<const _Float16*>(&sc[qrow][0]);
+    // this lane's transposed-read slot: row q = (lane >> 2) & 3 of the
+    // group's 4-row block, columns 4 (lane & 3) .. + 3 of the 16-column block
+    const int trq = (lane >> 2) & 3, trp = lane & 3;
 #pragma unroll 1
     for (int t = wid; t < nt32; t += 4) {
-      {  // stage the tile (this wave's region only: in-order LDS, no barrier)
-        const int sw = (vrow >> 3) & 3;
-        *reinterpret_cast<u32x4*>(vw + vrow * 64 + ((vch ^ sw) * 16)) = vr0;
-        *reinterpret_cast<u32x4*>(vw + vrow * 64 + (((vch + 1) ^ sw) * 16)) = vr1;
-      }
-      const u32x4 sv = vsr;
-      if (t + 4 < nt32) v_load(t + 4);
-      // A operands: P'[q][key] = P x 2^(s(key, half) - smax(half)), keys
-      // t*32 + 8(l>>4) + j, with smax the largest V scale exponent of the
-      // tile's 32 keys in that half; the tile's product is scaled by
-      // 2^smax in f32 below. (Folding the whole scale into P, as before,
-      // pushed typical weights p ~ 1/1500 x 2^-8 into f16 subnormals.)
-      const int kb = t * 32 + 8 * gq;
-      int smax0 = 0, smax1 = 0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t sp = (sv[j >> 1] >> (16 * (j & 1))) & 0xffffu;
-        if (kb + j < n) {
-          smax0 = max(smax0, (int)(sp & 0xffu));
-          smax1 = max(smax1, (int)(sp >> 8));
+      {  // stage the tile as f16 (this wave's region only: in-order LDS, no barrier)
+        f16x8 d0, d1, d2, d3;
+        if constexpr (KV8) {
+          d0 = dequant_h8(uint2{vr0[0], vr0[1]}, vse);
+          d1 = dequant_h8(uint2{vr0[2], vr0[3]}, vse);
+          d2 = dequant_h8(uint2{vr1[0], vr1[1]}, vse);
+          d3 = dequant_h8(uint2{vr1[2], vr1[3]}, vse);
+        } else {
+          d0 = vh[0];
+          d1 = vh[1];
+          d2 = vh[2];
+          d3 = vh[3];
         }
+        const int sw = (vrow >> 1) & 3, b0 = 2 * (lane & 1);  // the lane's two 16-column blocks
+        _Float16* rw = vw + vrow * 64;
+        *reinterpret_cast<f16x8*>(rw + ((b0 ^ sw) << 4)) = d0;
+        *reinterpret_cast<f16x8*>(rw + ((b0 ^ sw) << 4) + 8) = d1;
+        *reinterpret_cast<f16x8*>(rw + (((b0 + 1) ^ sw) << 4)) = d2;
+        *reinterpret_cast<f16x8*>(rw + (((b0 + 1) ^ sw) << 4) + 8) = d3;
       }
-      smax0 = max_xor16_i(smax0);
-      smax0 = max_xor32_i(smax0);
-      smax1 = max_xor16_i(smax1);
-      smax1 = max_xor32_i(smax1);
-      auto pow2 = [](int d) {  // 2^d for d <= 0 (0 below 2^-126)
-        return d < -126 ? 0.0f : __uint_as_float((uint32_t)(127 + d) << 23);
-      };
-      f16x8 pa[2];
-      // the lane's 8 weights in two 16-B reads (kb is a multiple of 8 and
-      // kb + 7 < 32 ceil(n / 32) <= DEC_MAX_KEYS; entries past n are
-      // replaced by 0 below)
-      const f32x4 pw0 = *reinterpret_cast<const f32x4*>(&sc[qrow][kb]);
-      const f32x4 pw1 = *reinterpret_cast<const f32x4*>(&sc[qrow][kb + 4]);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float p = j < 4 ? pw0[j] : pw1[j - 4];
-        if (mrow >= NQ || kb + j >= n) p = 0.0f;
-        const uint32_t sp = (sv[j >> 1] >> (16 * (j & 1))) & 0xffffu;
-        pa[0][j] = (_Float16)(p * pow2((int)(sp & 0xffu) - smax0));
-        pa[1][j] = (_Float16)(p * pow2((int)(sp >> 8) - smax1));
-      }
-      const float tscale[2] = {e8m0((uint32_t)smax0), e8m0((uint32_t)smax1)};
+      if (t + 4 < nt32) v_load(t + 4);
+      // A operand: P of query mrow (rows >= NQ zero) at keys t*32 + 8 gq .. + 7
+      // (zero past n, written so by the softmax)
+      const int kb = t * 32 + 8 * gq;
+      f16x8 pa = *reinterpret_cast<const f16x8*>(prow + kb);
+      if (mrow >= NQ) pa = f16x8{};
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
-        // the lane's B operand: column e = 16 nt + mrow of the tile's rows
-        // 8 gq .. 8 gq + 7 (their chunk nt ^ gq in the swizzled image), one
-        // byte per row, by a transposed LDS read: ds_read_b64_tr_b8 gives
-        // lane 16 g + i column i of the 8 rows whose 16-byte blocks the
-        // group's lanes 2 q + p address (row q, bytes 8 p .. 8 p + 7;
-        // mapping pinned on the GPU, scripts/probe/tr8_probe.hip). EXEC is
-        // all ones here (the tile loop is wave-uniform).
-        typedef int v2i_t __attribute__((ext_vector_type(2)));
-        const uint8_t* src = vw + (8 * gq + (mrow >> 1)) * 64 + ((nt ^ gq) * 16) + 8 * (mrow & 1);
-        const v2i_t tw = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
-            (__attribute__((address_space(3))) v2i_t*)(src));
-        const uint32_t w0 = (uint32_t)tw[0], w1 = (uint32_t)tw[1];
-        const f16x8 vb = dequant_h8(uint2{w0, w1}, 127u);
-        const f32x4 z = {0.0f, 0.0f, 0.0f, 0.0f};
-        const f32x4 tp = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa[nt >> 1], vb, z, 0, 0, 0);
+        // B operand: column 16 nt + mrow of keys 8 gq .. 8 gq + 7, as two
+        // 4-row transposed reads (rows 8 gq + 4 h + trq, this lane's 4 columns)
+        typedef short v4s_t __attribute__((ext_vector_type(4)));
+        u32x2 tw[2];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) oacc[nt][r] += tp[r] * tscale[nt >> 1];
+        for (int h = 0; h < 2; ++h) {
+          const int row = 8 * gq + 4 * h + trq;
+          const _Float16* src = vw + row * 64 + ((nt ^ ((row >> 1) & 3)) << 4) + 4 * trp;
+          // (the whole 64-bit result reinterpreted at once: per-element
+          // extraction of the v4i16 miscompiled here, only element 0 of each
+          // read reached the operand)
+          tw[h] = __builtin_bit_cast(u32x2, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                                                (__attribute__((address_space(3))) v4s_t*)(src)));
+        }
+        const f16x8 vb = __builtin_bit_cast(f16x8, u32x4{tw[0][0], tw[0][1], tw[1][0], tw[1][1]});
+        oacc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa, vb, oacc[nt], 0, 0, 0);
       }
     }
     // the four waves' partial sums: (w0 + w1) + (w2 + w3)
-    float* op = &pv[0][0][0];  // [4][NQ][64] floats (pv holds 4 x 64 x 9)
+    float* op = pvb;  // [4][NQ][64] floats
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
@@ -1212,11 +1205,11 @@ bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float*
                                  const void* kbase, const void* vbase, const int* kv_index,
                                  const int* active, int n_keys, int cap, T* o, int R, int H,
                                  float scale, int nq, hipStream_t st, const uint8_t* kscale8,
-                                 const uint8_t* vscale8, unsigned long long* span) {
+                                 const uint8_t* vscale8, unsigned long long* span, bool mfma) {
   if (n_keys > DEC_MAX_KEYS || KS > 8) return false;
   const dim3 g(H, (R + nq - 1) / nq);
   const bool kv8 = kscale8 != nullptr;
-  if (!kv8 && nq == 1) return false;  // (f16 single rows: dec_attention)
+  if (!kv8 && nq == 1 && !mfma) return false;  // (f16 single rows: dec_attention)
   // MWX_XATTN_NT=0: default-policy K/V loads (A/B of the non-temporal stream)
   static const bool nt = !(getenv("MWX_XATTN_NT") && atoi(getenv("MWX_XATTN_NT")) == 0);
   // 1500 keys: the constant-batch-count load stream, opt-in (MWX_XATTN_NBC=1):
@@ -1242,7 +1235,10 @@ bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float*
   switch (nq) {
 #define XQ(N)                                  \
   case N:                                      \
-    if (kv8 && mfs)                            \
+    if (!kv8 && mfma)                          \
+      dec_xattn_kernel<T, N, false, true, 0, true><<<g, 256, 0, st>>>(P, KS, pcols, bias, kbase, \
+          vbase, kscale8, vscale8, kv_index, active, n_keys, cap, R, o, H, scale, span);       \
+    else if (kv8 && mfs)                       \
       dec_xattn_kernel<T, N, true, true, 0, true><<<g, 256, 0, st>>>(P, KS, pcols, bias, kbase, \
           vbase, kscale8, vscale8, kv_index, active, n_keys, cap, R, o, H, scale, span);       \
     else if (kv8 && nt)                        \
@@ -1264,12 +1260,12 @@ template bool dec_cross_attention_grouped<_Float16>(const float*, int, int, cons
                                                     const void*, const void*, const int*,
                                                     const int*, int, int, _Float16*, int, int,
                                                     float, int, hipStream_t, const uint8_t*,
-                                                    const uint8_t*, unsigned long long*);
+                                                    const uint8_t*, unsigned long long*, bool);
 template bool dec_cross_attention_grouped<__bf16>(const float*, int, int, const float*,
                                                   const void*, const void*, const int*,
                                                   const int*, int, int, __bf16*, int, int, float,
                                                   int, hipStream_t, const uint8_t*,
-                                                  const uint8_t*, unsigned long long*);
+                                                  const uint8_t*, unsigned long long*, bool);
 
 // Prompt prefill: the self-attention K / V of every (virtual) row appended
 // to its cache row crow[row] at position pos[row] before the self-attention
