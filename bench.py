@@ -470,11 +470,12 @@ def stream_bench(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     wt = mwx.GGML_BF16 if args.wtype == "bf16" else mwx.GGML_F16
     d = os.environ.get("TMPDIR", "/tmp")
-    name = f"mwx_bench_{args.arch}_{args.wtype}.bin"
+    march = args.arch + ("-rich" if args.rich else "")
+    name = f"mwx_bench_{march}_{args.wtype}.bin"
     path = os.path.join(d, name)
     if not os.path.exists(path):
         tmp = path + f".tmp{os.getpid()}"
-        mwx.write_synthetic_model(tmp, args.arch, wt, 0)
+        mwx.write_synthetic_model(tmp, march, wt, 0)
         os.replace(tmp, path)
     L = C.CDLL(os.path.join(ROOT, "sentiric-stt-whisper-service_amd", "libmwx_stt.so"))
     L.mwx_stt_new_ex.restype = C.c_void_p
@@ -507,6 +508,10 @@ def stream_bench(args):
                 lat.append((t1 - t0) * 1e3)
         L.mwx_stt_stream_feed(s, b"", 0, out, cap)  # end of speech (final, not timed)
         L.mwx_stt_stream_free(s)
+        part = lat[-60:] if rep >= args.warmup else []
+        print(f"stream {rep}: {len(part)} timed partials, p50 "
+              f"{np.percentile(part, 50) if len(part) else float('nan'):.2f} ms", file=sys.stderr,
+              flush=True)
     L.mwx_stt_free(eng)
     lat = np.array(lat)
     line = {"metric": "streaming partial latency (0.5-s cadence, re-transcription of the growing "
@@ -516,7 +521,7 @@ def stream_bench(args):
             "partials": int(len(lat)), "streams": args.steps, "n_gpus": 1,
             "dtype": args.wtype, "data": "synthetic (seeded 16 kHz PCM16 stream, seeded weights)",
             "mel_cache": os.environ.get("MWX_NO_MEL_CACHE") is None,
-            "config": {"workload": f"whisper-{args.arch} {args.wtype}: one 30-s stream in 0.5-s "
+            "config": {"workload": f"whisper-{march} {args.wtype}: one 30-s stream in 0.5-s "
                                    f"chunks through SttEngine/StreamSession, "
                                    f"{'beam-%d' % beam if beam > 1 else 'greedy'} decode until "
                                    f"the model stops"}}

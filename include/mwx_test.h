@@ -91,13 +91,6 @@ int mwx_test_sample_draws(struct mwx_context* ctx, const float* probs, const flo
  * previous setting. */
 int mwx_test_set_xattn_mfs(int on);
 
-/* The test decodes (mwx_test_decode, _decode_last, _decode_last_prefill)
- * compute the cross-attention with a decoder group's arithmetic (on != 0:
- * beam / best-of rows and their prompt prefill, f16 caches: scores and P.V on
- * MFMA) or a single greedy row's (0, the default). Returns the previous
- * setting. */
-int mwx_test_set_xattn_group_mfma(int on);
-
 /* The MX-fp8 grouped cross-attention kernel on given data: q [R][H*64] f32
  * queries (rounded to f16 by the kernel), K / V as e4m3 codes [R/nq][H][n][64]
  * with E8M0 scales [R/nq][H][n][2] (one per 32-element half), rows

@@ -10,7 +10,9 @@
 #   bench1     C3 on one lane
 #   c2         C2: base f16, one clip per request
 #   c2nt       C2 with the cross K/V streamed non-temporally (A/B of the MALL-resident default)
-#   b5one      beam 5 on one lane
+#   b5one      beam 5 on one lane (b5onenog: decoder groups' f16 cross-attention on v_dot2)
+#   stream / streamr / streamv3r  streaming partial latency: base (220-token windows + fallbacks),
+#              base-rich (EOT / timestamps, r02's workload), large-v3-rich
 #   bench1nts / benchqnts  C3 one lane / 2 lanes with token_timestamps off (A/B of the round-3 regression)
 #   probe      the decode-chain probe (scripts/probe/dec_chain_probe): fused seams bit-exact + per-layer times
 #   mfstest    the MX-fp8 tests with the MFMA-score cross-attention (MWX_XATTN_MFS=1)
@@ -69,6 +71,8 @@ for s in "$@"; do
     c5mfs) run c5mfs 700 env MWX_XATTN_MFS=1 python -u bench.py --fp8 --beam 5 --clip-seconds 600 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline ;;
     c5onevd1) run c5onevd1 700 env MWX_XATTN_VD=1 python -u bench.py --fp8 --beam 5 --clip-seconds 600 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline ;;
     vdtests) run vdtests 400 python -u -m pytest tests/test_gpu_parity.py -k "v_depth or mx_cross or mxfp8" -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
+    torchgemm) run torchgemm 300 python -u scripts/probe/enc_gemm_torch.py ;;
+    c5onevb1) run c5onevb1 700 env MWX_LIB=$GRAFT_REPO_ROOT/ablib/libmwx_vb1.so python -u bench.py --fp8 --beam 5 --clip-seconds 600 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline ;;
     c5one) run c5one 700 python -u bench.py --fp8 --beam 5 --clip-seconds 600 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline ;;
     bench1np) run bench1np 400 env MWX_PREFILL_MIN=0 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
     bench1g0) run bench1g0 400 env MWX_GEMM_GROUP=0 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
@@ -81,6 +85,8 @@ for s in "$@"; do
     c5tests) run c5tests 1100 python -u -m pytest tests/test_gpu_c5.py -m gpu -v -s -rf --timeout 1000 --timeout-method thread ;;
     probelaunch) for k in launch "empty 512" res_ splitk skinny ln_dec; do run "probe_$(echo $k | tr -d ' ')" 200 env PROBE_ONLY="$k" ./scripts/probe/dec_chain_probe 32 10 || exit 6; done ;;
     stream) run stream 300 python -u bench.py --stream --arch base --wtype f16 --steps 3 --warmup 1 ;;
+    streamr) run streamr 300 python -u bench.py --stream --rich --arch base --wtype f16 --steps 3 --warmup 1 ;;
+    streamv3r) run streamv3r 500 python -u bench.py --stream --rich --arch large-v3 --wtype bf16 --steps 1 --warmup 1 ;;
     streamv3) run streamv3 400 python -u bench.py --stream --arch large-v3 --wtype bf16 --steps 2 --warmup 1 ;;
     g8tests) run g8tests 300 python -u -m pytest tests/test_gpu_parity.py -k "8phase or gemm_gelu or encoder_and_cross" -m gpu -v -s -rf --timeout 120 --timeout-method thread ;;
     bench1g8) run bench1g8 400 env MWX_GEMM_8PH=1 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
@@ -88,6 +94,7 @@ for s in "$@"; do
     tr8) run tr8 120 ./scripts/probe/tr8_probe ;;
     tr16) run tr16 120 ./scripts/probe/tr16_probe ;;
     mxtests) run mxtests 700 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shapes.py tests/test_gpu_prefill.py -k "mx or fp8" -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
+    b5onenog) run b5onenog 500 env MWX_XATTN_GMFMA=0 python -u bench.py --beam 5 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
     b5one) run b5one 500 python -u bench.py --beam 5 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
     bench1g16) run bench1g16 400 env MWX_GEMM_GROUP=16 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
     bench1g32) run bench1g32 400 env MWX_GEMM_GROUP=32 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;

@@ -791,17 +791,6 @@ struct Driver {
   // rows per clip in the current decode run (beam_size / best_of decoders are
   // consecutive rows of one clip); decode groups never split such a run
   int xgroup = 1;
-  // cross-attention arithmetic of the run (f16 caches): groups of decoders
-  // (beam / best-of: xgroup > 1) and their prompt prefill compute scores and
-  // P.V on MFMA (dec_xattn_kernel MFS), single greedy rows keep the v_dot2
-  // kernel (the arithmetic closest to ggml's f32 dot products; greedy is the
-  // token-exact parity path). MWX_XATTN_GMFMA=0: v_dot2 for groups too (A/B).
-  bool gmfma = false;
-  void set_group(int n) {
-    static const bool on = !(getenv("MWX_XATTN_GMFMA") && atoi(getenv("MWX_XATTN_GMFMA")) == 0);
-    xgroup = n;
-    gmfma = on && n > 1;
-  }
 
   Driver(Context& c, State& s, const mwx_full_params& p)
       : C(c), S(s), st(s.stream), P(p), hp(c.hp) {
@@ -1118,7 +1107,6 @@ struct Driver {
     const int *kvmap = nullptr, *kvown = nullptr;
     int map_row0 = 0;
     int xgroup = 1;
-    bool gmfma = false;  // (Driver::gmfma)
     // prefill: the K/V of every virtual row are appended to the self cache
     // before the self-attention (a position reads the prompt positions before
     // it, which other virtual rows of the same launch produce), and the
@@ -1211,13 +1199,6 @@ struct Driver {
               (const uint8_t*)S.cross_ks.p + l * layer_xs,
               (const uint8_t*)S.cross_vs.p + l * layer_xs, sp))
         throw std::runtime_error("mwx: unsupported fp8 cross-attention group");
-    } else if (rw.gmfma) {
-      if (!dec_cross_attention_grouped<T>(rw.Pq, c.k3, d, W.cq_b,
-                                          (const _Float16*)S.cross_k.p + l * layer_cross,
-                                          (const _Float16*)S.cross_v.p + l * layer_cross,
-                                          rw.xidx, rw.act, hp.n_audio_ctx, hp.n_audio_ctx, rw.od,
-                                          n, H, kqs, nq, s, nullptr, nullptr, sp, true))
-        throw std::runtime_error("mwx: unsupported cross-attention group");
     } else if (nq < 2 ||
                !dec_cross_attention_grouped<T>(rw.Pq, c.k3, d, W.cq_b,
                                                (const _Float16*)S.cross_k.p + l * layer_cross,
@@ -1324,7 +1305,6 @@ struct Driver {
     rw.vself = (_Float16*)S.vself.p;
     rw.prefill = true;
     rw.xgroup = q;
-    rw.gmfma = gmfma;
     // host inputs of every chunk in one array (no reallocation while its
     // uploads are queued): the pass is queued without a synchronize, so the
     // host goes on to capture / launch the decode steps behind it
@@ -1413,7 +1393,6 @@ struct Driver {
     rw.kvown = (const int*)S.kvown.p;
     rw.map_row0 = 0;
     rw.xgroup = xgroup;
-    rw.gmfma = gmfma;
     return rw;
   }
 

@@ -664,6 +664,9 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
 // on f16 exactly as for the f16 cache. Each lane loads the scale pair of one
 // of its wave's 64 rows per batch; the pair a row needs is read from the lane
 // that loaded it (__shfl).
+#ifndef XATTN_VB
+#define XATTN_VB 2
+#endif
 __device__ __forceinline__ f16x8 dequant_h8(uint2 raw, uint32_t e) {
   const float sc = e ? __uint_as_float(e << 23) : __uint_as_float(0x00400000u);
   const h2 a = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(raw.x, sc, false);
@@ -692,6 +695,7 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
     const uint8_t* __restrict__ kscale8, const uint8_t* __restrict__ vscale8,
     const int* __restrict__ kv_index, const int* __restrict__ active, int n, int cap, int R,
     T* __restrict__ o, int H, float scale, unsigned long long* span = nullptr) {
+  static_assert(!MFS || KV8, "MFS: MX-fp8 caches only");
   span_start(span);
   __shared__ __attribute__((aligned(16))) float sc[NQ][DEC_MAX_KEYS];
   __shared__ float redf[4][NQ];
@@ -777,26 +781,19 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
   constexpr int TD = 4;
   const int ntile = (n + 15) >> 4;
   const int mrow = lane & 15, gq = lane >> 4;
-  uint2 kr[MFS && KV8 ? 2 : 1][MFS && KV8 ? TD : 1][2];
-  uint32_t ksr[MFS && KV8 ? 2 : 1][MFS && KV8 ? TD : 1];
-  f16x8 kh[MFS && !KV8 ? 2 : 1][MFS && !KV8 ? TD : 1][2];  // (f16 cache: the A operands as loaded)
+  uint2 kr[MFS ? 2 : 1][MFS ? TD : 1][2];
+  uint32_t ksr[MFS ? 2 : 1][MFS ? TD : 1];
   auto mfs_load = [&](int buf, int grp) {  // tiles wid + 4 * (TD * grp + i)
 #pragma unroll
     for (int i = 0; i < TD; ++i) {
       const int t = min(wid + 4 * (TD * grp + i), ntile - 1);
       const int key = min(t * 16 + mrow, jmax);
-      if constexpr (KV8) {
-        const uint8_t* row = K8 + (long)key * 64 + 8 * gq;
-        const u32x2 a = ld_stream<NTL>(reinterpret_cast<const u32x2*>(row));
-        const u32x2 b = ld_stream<NTL>(reinterpret_cast<const u32x2*>(row + 32));
-        kr[buf][i][0] = uint2{a[0], a[1]};
-        kr[buf][i][1] = uint2{b[0], b[1]};
-        ksr[buf][i] = *reinterpret_cast<const uint16_t*>(KS8 + (long)key * 2);
-      } else {
-        const _Float16* row = K + (long)key * 64 + 8 * gq;
-        kh[buf][i][0] = ld_stream<NTL>(reinterpret_cast<const f16x8*>(row));
-        kh[buf][i][1] = ld_stream<NTL>(reinterpret_cast<const f16x8*>(row + 32));
-      }
+      const uint8_t* row = K8 + (long)key * 64 + 8 * gq;
+      const u32x2 a = ld_stream<NTL>(reinterpret_cast<const u32x2*>(row));
+      const u32x2 b = ld_stream<NTL>(reinterpret_cast<const u32x2*>(row + 32));
+      kr[buf][i][0] = uint2{a[0], a[1]};
+      kr[buf][i][1] = uint2{b[0], b[1]};
+      ksr[buf][i] = *reinterpret_cast<const uint16_t*>(KS8 + (long)key * 2);
     }
   };
   const int ngrp = ((ntile + 3) / 4 + TD - 1) / TD;  // (tile groups per wave, upper bound)
@@ -879,24 +876,20 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
   // operand the query's f16 P itself (no per-key scale arithmetic). The
   // 32-B column blocks of a row are XOR-swizzled by (row >> 1) & 3, so a
   // 16-lane group's four rows hit distinct banks.
-  // (f16 cache: the lane's 32 values of row vrow are loaded as they are)
   __shared__ __attribute__((aligned(16))) _Float16 vtile[MFS ? 4 : 1][MFS ? 32 * 64 : 8];
   const int nt32 = (n + 31) >> 5;
   const int vrow = lane >> 1, vch = 2 * (lane & 1);
-  u32x4 vr0, vr1;  // the next tile's codes (row vrow, chunks vch, vch + 1)
-  uint32_t vse = 0;  // their E8M0 scale (row vrow, half lane & 1)
-  f16x8 vh[MFS && !KV8 ? 4 : 1];  // (f16 cache: row vrow, values 32 (lane & 1) .. + 31)
-  auto v_load = [&](int t) {
+  // VB tiles in flight per wave (build constant XATTN_VB)
+  constexpr int VB = MFS ? XATTN_VB : 1;
+  u32x4 vr[VB][2];     // the next tiles' codes (row vrow, chunks vch, vch + 1)
+  uint32_t vse[VB];    // their E8M0 scale (row vrow, half lane & 1)
+  auto v_load = [&](int t, int b) {
     const int row = min(t * 32 + vrow, jmax);
     if constexpr (KV8) {
       const u32x4* src = reinterpret_cast<const u32x4*>(V8 + (long)row * 64) + vch;
-      vr0 = ld_stream<NTL>(src);
-      vr1 = ld_stream<NTL>(src + 1);
-      vse = VS8[(long)row * 2 + (lane & 1)];
-    } else if constexpr (MFS) {
-      const f16x8* src = reinterpret_cast<const f16x8*>(V + (long)row * 64 + 32 * (lane & 1));
-#pragma unroll
-      for (int i = 0; i < 4; ++i) vh[i] = ld_stream<NTL>(src + i);
+      vr[b][0] = ld_stream<NTL>(src);
+      vr[b][1] = ld_stream<NTL>(src + 1);
+      vse[b] = VS8[(long)row * 2 + (lane & 1)];
     }
   };
   if constexpr (MFS) {
@@ -913,15 +906,9 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
     auto score_tile = [&](int buf, int i, int t) {
       f32x4 out;
       {
-        f16x8 a0, a1;
-        if constexpr (KV8) {
-          const uint32_t sp = ksr[buf][i];
-          a0 = dequant_h8(kr[buf][i][0], sp & 0xffu);
-          a1 = dequant_h8(kr[buf][i][1], sp >> 8);
-        } else {
-          a0 = kh[buf][i][0];
-          a1 = kh[buf][i][1];
-        }
+        const uint32_t sp = ksr[buf][i];
+        const f16x8 a0 = dequant_h8(kr[buf][i][0], sp & 0xffu);
+        const f16x8 a1 = dequant_h8(kr[buf][i][1], sp >> 8);
         const f32x4 z = {0.0f, 0.0f, 0.0f, 0.0f};
         f32x4 d = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, qb0, z, 0, 0, 0);
         d = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, qb1, d, 0, 0, 0);
@@ -942,7 +929,8 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
         for (int i = 0; i < TD; ++i) score_tile(1, i, wid + 4 * (TD * (grp + 1) + i));
       }
     }
-    if (wid < nt32) v_load(wid);  // (in flight across the softmax)
+    if (wid < nt32) v_load(wid, 0);  // (in flight across the softmax)
+    if (VB > 1 && wid + 4 < nt32) v_load(wid + 4, VB - 1);
   } else if constexpr (NBC > 0) {
 #pragma unroll 1
     for (int b = 0; b < NBC - 1; ++b) k_trip(b, false);
@@ -1041,21 +1029,12 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
     // this lane's transposed-read slot: row q = (lane >> 2) & 3 of the
     // group's 4-row block, columns 4 (lane & 3) .. + 3 of the 16-column block
     const int trq = (lane >> 2) & 3, trp = lane & 3;
-#pragma unroll 1
-    for (int t = wid; t < nt32; t += 4) {
+    auto pv_tile = [&](int t, int b) {
       {  // stage the tile as f16 (this wave's region only: in-order LDS, no barrier)
-        f16x8 d0, d1, d2, d3;
-        if constexpr (KV8) {
-          d0 = dequant_h8(uint2{vr0[0], vr0[1]}, vse);
-          d1 = dequant_h8(uint2{vr0[2], vr0[3]}, vse);
-          d2 = dequant_h8(uint2{vr1[0], vr1[1]}, vse);
-          d3 = dequant_h8(uint2{vr1[2], vr1[3]}, vse);
-        } else {
-          d0 = vh[0];
-          d1 = vh[1];
-          d2 = vh[2];
-          d3 = vh[3];
-        }
+        const f16x8 d0 = dequant_h8(uint2{vr[b][0][0], vr[b][0][1]}, vse[b]);
+        const f16x8 d1 = dequant_h8(uint2{vr[b][0][2], vr[b][0][3]}, vse[b]);
+        const f16x8 d2 = dequant_h8(uint2{vr[b][1][0], vr[b][1][1]}, vse[b]);
+        const f16x8 d3 = dequant_h8(uint2{vr[b][1][2], vr[b][1][3]}, vse[b]);
         const int sw = (vrow >> 1) & 3, b0 = 2 * (lane & 1);  // the lane's two 16-column blocks
         _Float16* rw = vw + vrow * 64;
         *reinterpret_cast<f16x8*>(rw + ((b0 ^ sw) << 4)) = d0;
@@ -1063,7 +1042,7 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
         *reinterpret_cast<f16x8*>(rw + (((b0 + 1) ^ sw) << 4)) = d2;
         *reinterpret_cast<f16x8*>(rw + (((b0 + 1) ^ sw) << 4) + 8) = d3;
       }
-      if (t + 4 < nt32) v_load(t + 4);
+      if (t + 4 * VB < nt32) v_load(t + 4 * VB, b);
       // A operand: P of query mrow (rows >= NQ zero) at keys t*32 + 8 gq .. + 7
       // (zero past n, written so by the softmax)
       const int kb = t * 32 + 8 * gq;
@@ -1088,6 +1067,11 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
         const f16x8 vb = __builtin_bit_cast(f16x8, u32x4{tw[0][0], tw[0][1], tw[1][0], tw[1][1]});
         oacc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa, vb, oacc[nt], 0, 0, 0);
       }
+    };
+#pragma unroll 1
+    for (int t = wid; t < nt32; t += 4 * VB) {
+      pv_tile(t, 0);
+      if (VB > 1 && t + 4 < nt32) pv_tile(t + 4, VB - 1);
     }
     // the four waves' partial sums: (w0 + w1) + (w2 + w3)
     float* op = pvb;  // [4][NQ][64] floats
@@ -1205,11 +1189,11 @@ bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float*
                                  const void* kbase, const void* vbase, const int* kv_index,
                                  const int* active, int n_keys, int cap, T* o, int R, int H,
                                  float scale, int nq, hipStream_t st, const uint8_t* kscale8,
-                                 const uint8_t* vscale8, unsigned long long* span, bool mfma) {
+                                 const uint8_t* vscale8, unsigned long long* span) {
   if (n_keys > DEC_MAX_KEYS || KS > 8) return false;
   const dim3 g(H, (R + nq - 1) / nq);
   const bool kv8 = kscale8 != nullptr;
-  if (!kv8 && nq == 1 && !mfma) return false;  // (f16 single rows: dec_attention)
+  if (!kv8 && nq == 1) return false;  // (f16 single rows: dec_attention)
   // MWX_XATTN_NT=0: default-policy K/V loads (A/B of the non-temporal stream)
   static const bool nt = !(getenv("MWX_XATTN_NT") && atoi(getenv("MWX_XATTN_NT")) == 0);
   // 1500 keys: the constant-batch-count load stream, opt-in (MWX_XATTN_NBC=1):
@@ -1235,10 +1219,7 @@ bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float*
   switch (nq) {
 #define XQ(N)                                  \
   case N:                                      \
-    if (!kv8 && mfma)                          \
-      dec_xattn_kernel<T, N, false, true, 0, true><<<g, 256, 0, st>>>(P, KS, pcols, bias, kbase, \
-          vbase, kscale8, vscale8, kv_index, active, n_keys, cap, R, o, H, scale, span);       \
-    else if (kv8 && mfs)                       \
+    if (kv8 && mfs)                            \
       dec_xattn_kernel<T, N, true, true, 0, true><<<g, 256, 0, st>>>(P, KS, pcols, bias, kbase, \
           vbase, kscale8, vscale8, kv_index, active, n_keys, cap, R, o, H, scale, span);       \
     else if (kv8 && nt)                        \
@@ -1260,12 +1241,12 @@ template bool dec_cross_attention_grouped<_Float16>(const float*, int, int, cons
                                                     const void*, const void*, const int*,
                                                     const int*, int, int, _Float16*, int, int,
                                                     float, int, hipStream_t, const uint8_t*,
-                                                    const uint8_t*, unsigned long long*, bool);
+                                                    const uint8_t*, unsigned long long*);
 template bool dec_cross_attention_grouped<__bf16>(const float*, int, int, const float*,
                                                   const void*, const void*, const int*,
                                                   const int*, int, int, __bf16*, int, int, float,
                                                   int, hipStream_t, const uint8_t*,
-                                                  const uint8_t*, unsigned long long*, bool);
+                                                  const uint8_t*, unsigned long long*);
 
 // Prompt prefill: the self-attention K / V of every (virtual) row appended
 // to its cache row crow[row] at position pos[row] before the self-attention

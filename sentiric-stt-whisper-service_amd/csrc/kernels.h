@@ -237,10 +237,7 @@ bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float*
                                  float scale, int nq, hipStream_t st,
                                  const uint8_t* kscale8 = nullptr,
                                  const uint8_t* vscale8 = nullptr,
-                                 unsigned long long* span = nullptr, bool mfma = false);
-// (mfma, f16 caches: scores and P.V on MFMA -- the arithmetic of beam /
-// best-of groups and their prompt prefill, any group size incl. 1; the
-// v_dot2 path otherwise, which single rows share with dec_attention)
+                                 unsigned long long* span = nullptr);
 
 struct RowCtl {
   int active;        // row participates in this step

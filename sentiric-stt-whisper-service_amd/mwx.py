@@ -217,8 +217,6 @@ def lib() -> C.CDLL:
     L.mwx_test_runahead_fallbacks.argtypes = [P, C.c_int]
     L.mwx_test_set_xattn_mfs.restype = C.c_int
     L.mwx_test_set_xattn_mfs.argtypes = [C.c_int]
-    L.mwx_test_set_xattn_group_mfma.restype = C.c_int
-    L.mwx_test_set_xattn_group_mfma.argtypes = [C.c_int]
     u8p = C.POINTER(C.c_uint8)
     L.mwx_test_xattn_mx.restype = C.c_int
     L.mwx_test_xattn_mx.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, fpp, u8p, u8p,
@@ -631,11 +629,7 @@ class Context:
         return o
 
     def test_decode_last(self, tokens: Sequence[int], out: Optional[np.ndarray] = None,
-                         state_index: int = 0, group: bool = False) -> np.ndarray:
-        """Logits of the last token of `tokens` decoded on one row; group=True
-        with a decoder group's cross-attention arithmetic (the logits a beam /
-        best-of row sees in a run: mwx_test_set_xattn_group_mfma)."""
-        lib().mwx_test_set_xattn_group_mfma(1 if group else 0)
+                         state_index: int = 0) -> np.ndarray:
         toks = np.ascontiguousarray(tokens, dtype=np.int32)
         if out is None:
             out = np.empty(self.hparam("n_vocab"), dtype=np.float32)

@@ -32,7 +32,7 @@ import pytest
 
 import mwx
 import orc
-from test_gpu_parity import assert_same, beam_opt, beam_params, group_pass, pcm_clip, run_fresh
+from test_gpu_parity import assert_same, beam_opt, beam_params, pcm_clip, run_fresh
 
 pytestmark = pytest.mark.gpu
 
@@ -64,7 +64,7 @@ def replay_traced(ctx, o, pcm, opt):
         ctx.test_encode(pcm, seek=seek, cross=False, state_index=idx)
 
     def logits(tokens):
-        lg = ctx.test_decode_last(tokens, state_index=idx, group=group_pass(opt)).copy()
+        lg = ctx.test_decode_last(tokens, state_index=idx).copy()
         log.append((cur["seek"], list(tokens), lg, orc.trace_ctx()))
         return lg
 

@@ -359,27 +359,12 @@ def beam_opt(temperature_inc):
     return opt
 
 
-def group_pass(opt):
-    """Whether the decode pass the oracle is in (inside a full_external
-    callback) runs a decoder group -- beam, or best_of sampled decoders at
-    t > 0 -- whose rows the engine computes with the group cross-attention
-    arithmetic (scores and P.V on MFMA; engine.cpp Driver::gmfma)."""
-    it = orc.trace_ctx()[1]
-    t = opt.temperature + it * opt.temperature_inc
-    if opt.strategy == 1:
-        n = opt.best_of if t > 0 else opt.beam_size
-    else:
-        n = opt.best_of if t > 0 else 1
-    return n > 1
-
-
 def replay(ctx, o, pcm, opt):
     """The oracle's whisper_full logic (logits rules, draws, beam ranking,
     fallback, segments) run on logits the device computes for each prefix
-    (teacher-forced through the C ABI, with the arithmetic of the pass's rows:
-    group_pass): isolates the token-loop logic from the f16 noise of the
-    logits, which can reorder beam hypotheses whose summed log-probs differ
-    by less than ~1e-2."""
+    (teacher-forced through the C ABI): isolates the token-loop logic from the
+    f16 noise of the logits, which can reorder beam hypotheses whose summed
+    log-probs differ by less than ~1e-2."""
     idx = len(ctx.states)
     ctx.state(idx)
 
@@ -387,7 +372,7 @@ def replay(ctx, o, pcm, opt):
         ctx.test_encode(pcm, seek=seek, cross=False, state_index=idx)
 
     def logits(tokens):
-        return ctx.test_decode_last(tokens, state_index=idx, group=group_pass(opt))
+        return ctx.test_decode_last(tokens, state_index=idx)
 
     _, segs, _, _ = o.full_external(pcm, opt, enc, logits)
     return segs
