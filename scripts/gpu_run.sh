@@ -54,6 +54,9 @@ run() {  # name, seconds, command...
 }
 for s in "$@"; do
   case $s in
+    b5e_*)  # beam 5 on one lane with one engine knob: b5e_<VAR>_<value> (MWX_<VAR>=<value>)
+      kv=${s#b5e_}; var=MWX_${kv%_*}; val=${kv##*_}
+      run "$s" 500 env "$var=$val" python -u bench.py --beam 5 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
     abb*)  # the same for beam 5 (ablib/libmwx_<build>.so, 2 lanes)
       v=${s#abb}; [ "$v" = h ] && v=head
       run "${s}_$(date +%s)" 500 env MWX_LIB=$GRAFT_REPO_ROOT/ablib/libmwx_$v.so python -u bench.py --beam 5 --steps 4 --warmup 1 --no-cpu-baseline --no-one-lane ;;
@@ -72,6 +75,7 @@ for s in "$@"; do
     c5onevd1) run c5onevd1 700 env MWX_XATTN_VD=1 python -u bench.py --fp8 --beam 5 --clip-seconds 600 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline ;;
     vdtests) run vdtests 400 python -u -m pytest tests/test_gpu_parity.py -k "v_depth or mx_cross or mxfp8" -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
     torchgemm) run torchgemm 300 python -u scripts/probe/enc_gemm_torch.py ;;
+    c5onevb4) run c5onevb4 700 env MWX_LIB=$GRAFT_REPO_ROOT/ablib/libmwx_vb4.so python -u bench.py --fp8 --beam 5 --clip-seconds 600 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline ;;
     c5onevb1) run c5onevb1 700 env MWX_LIB=$GRAFT_REPO_ROOT/ablib/libmwx_vb1.so python -u bench.py --fp8 --beam 5 --clip-seconds 600 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline ;;
     c5one) run c5one 700 python -u bench.py --fp8 --beam 5 --clip-seconds 600 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline ;;
     bench1np) run bench1np 400 env MWX_PREFILL_MIN=0 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
@@ -94,6 +98,9 @@ for s in "$@"; do
     tr8) run tr8 120 ./scripts/probe/tr8_probe ;;
     tr16) run tr16 120 ./scripts/probe/tr16_probe ;;
     mxtests) run mxtests 700 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shapes.py tests/test_gpu_prefill.py -k "mx or fp8" -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
+    b5onenw4) run b5onenw4 500 env MWX_SELF_NW=4 python -u bench.py --beam 5 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    bench1nw4) run bench1nw4 400 env MWX_SELF_NW=4 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
+    c2nw4) run c2nw4 300 env MWX_SELF_NW=4 python -u bench.py --arch base --wtype f16 --clips 1 --lanes 1 --steps 20 --warmup 3 --no-cpu-baseline ;;
     b5onenog) run b5onenog 500 env MWX_XATTN_GMFMA=0 python -u bench.py --beam 5 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
     b5one) run b5one 500 python -u bench.py --beam 5 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
     bench1g16) run bench1g16 400 env MWX_GEMM_GROUP=16 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;

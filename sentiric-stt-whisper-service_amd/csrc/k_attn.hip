@@ -929,8 +929,9 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
         for (int i = 0; i < TD; ++i) score_tile(1, i, wid + 4 * (TD * (grp + 1) + i));
       }
     }
-    if (wid < nt32) v_load(wid, 0);  // (in flight across the softmax)
-    if (VB > 1 && wid + 4 < nt32) v_load(wid + 4, VB - 1);
+#pragma unroll
+    for (int b = 0; b < VB; ++b)  // (in flight across the softmax)
+      if (wid + 4 * b < nt32) v_load(wid + 4 * b, b);
   } else if constexpr (NBC > 0) {
 #pragma unroll 1
     for (int b = 0; b < NBC - 1; ++b) k_trip(b, false);
@@ -1070,8 +1071,9 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
     };
 #pragma unroll 1
     for (int t = wid; t < nt32; t += 4 * VB) {
-      pv_tile(t, 0);
-      if (VB > 1 && t + 4 < nt32) pv_tile(t + 4, VB - 1);
+#pragma unroll
+      for (int b = 0; b < VB; ++b)
+        if (t + 4 * b < nt32) pv_tile(t + 4 * b, b);
     }
     // the four waves' partial sums: (w0 + w1) + (w2 + w3)
     float* op = pvb;  // [4][NQ][64] floats
