@@ -87,6 +87,7 @@ for s in "$@"; do
     bench3l) run bench3l 600 python -u bench.py --lanes 3 --steps 9 --warmup 3 --no-cpu-baseline --no-one-lane ;;
     beamorc) run beamorc 900 python -u -m pytest tests/test_gpu_beam_oracle.py -m gpu -v -s -rf --timeout 800 --timeout-method thread ;;
     c5tests) run c5tests 1100 python -u -m pytest tests/test_gpu_c5.py -m gpu -v -s -rf --timeout 1000 --timeout-method thread ;;
+    probe160) for k in self_attn skinny_fc1 splitk_ ln_dec; do run "probe160_$k" 200 env PROBE_ONLY="$k" ./scripts/probe/dec_chain_probe 160 10 || exit 6; done ;;
     probelaunch) for k in launch "empty 512" res_ splitk skinny ln_dec; do run "probe_$(echo $k | tr -d ' ')" 200 env PROBE_ONLY="$k" ./scripts/probe/dec_chain_probe 32 10 || exit 6; done ;;
     stream) run stream 300 python -u bench.py --stream --arch base --wtype f16 --steps 3 --warmup 1 ;;
     streamr) run streamr 300 python -u bench.py --stream --rich --arch base --wtype f16 --steps 3 --warmup 1 ;;

@@ -37,8 +37,12 @@ def load(path):
 
 def main():
     root, tag = sys.argv[1], sys.argv[2]
-    fetch = load(os.path.join(root, f"pmc_{tag}_FETCH_SIZE"))
-    write = load(os.path.join(root, f"pmc_{tag}_WRITE_SIZE"))
+    # (gpu_run.sh names its pass directories <tag>_pmc_<counter>; older runs pmc_<tag>_<counter>)
+    def pdir(c):
+        new = os.path.join(root, f"{tag}_pmc_{c}")
+        return new if os.path.isdir(new) else os.path.join(root, f"pmc_{tag}_{c}")
+    fetch = load(pdir("FETCH_SIZE"))
+    write = load(pdir("WRITE_SIZE"))
     out = {}
     for cls in sorted(set(fetch) | set(write)):
         f = fetch.get(cls, [])
