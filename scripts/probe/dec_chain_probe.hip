@@ -310,7 +310,7 @@ int main(int argc, char** argv) {
     chain(l, 2, ffd, wl(l, 5), 4 * d, wl((l + 1) % L, 0), 3 * d, false, slab2);  // FFN2 -> LN1 -> QKV
   };
   // ---- bit-exactness: each fused seam == its three launches (same inputs) ----
-  {
+  if (R <= 64) {  // (the fused seams support <= 64 rows)
     fill_kernel<<<1024, 256>>>((uint16_t*)od, R64 * d, 21);
     fill_kernel<<<1024, 256>>>((uint16_t*)ffd, R64 * 4 * d, 22);
     // slab rows of the producer must be finite garbage-free: the producers write them
@@ -503,6 +503,7 @@ int main(int argc, char** argv) {
   printf("%-38s %10s %12s\n", "chain", "us/launch", "us/layer");
   for (auto& op : ops) {
     if (only && op.name.find(only) == std::string::npos) continue;
+    if (R > 64 && op.name.find("CHAIN") != std::string::npos) continue;
     hipGraph_t g;
     hipGraphExec_t ge;
     CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));

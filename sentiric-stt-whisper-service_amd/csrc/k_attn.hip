@@ -334,6 +334,18 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
   const int p_row = SELF ? pos[row] : 0;
   const int slot = kv_index ? kv_index[row] : row;
   const int own0 = SELF && own_from ? own_from[row] : 0;
+  // self: the position-map words of this lane's batch-0 rows are requested
+  // with the control words, not after them (indices unclamped: a row past the
+  // end is never read for its value, and only rows below own_from, all below
+  // the new position, use their map word), so the batch-0 K / V addresses
+  // wait for one memory round trip instead of two
+  int mraw[SELF ? UBX : 1];
+  if constexpr (SELF) {
+    const int* mr = kvmap ? kvmap + (long)row * cap : nullptr;
+    const int kgl = (threadIdx.x & 63) >> 3, wdl = threadIdx.x >> 6;
+#pragma unroll
+    for (int u = 0; u < UBX; ++u) mraw[u] = mr ? mr[min(wdl * (8 * UBX) + u * 8 + kgl, cap - 1)] : 0;
+  }
   asm volatile("" ::"s"(act_r), "s"(p_row), "s"(slot), "s"(own0));
   if (!act_r) {
     span_end(span);
@@ -371,15 +383,15 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
     buf[u] = ld_stream<NTL>(reinterpret_cast<const f16x8*>(src));                 \
   }
   // self (beam search): the history rows of batch 0 are resolved through the
-  // position map once, before anything else is loaded, and the row deltas are
-  // kept in registers for both the K and the V loads of that batch (the map
-  // read is one round trip ahead of K only, none ahead of V)
+  // position map once (its words requested with the control words, above),
+  // and the row deltas are kept in registers for both the K and the V loads
+  // of that batch
   int mdel[SELF ? UB : 1];
   if constexpr (SELF) {
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
-      const int j = min(wid * (8 * UB) + u * 8 + kg, jmax);
-      mdel[u] = (mrow && j < own0) ? mrow[j] - map_row0 - slot : 0;
+      const int idx = wid * (8 * UB) + u * 8 + kg;
+      mdel[u] = (mrow && idx < own0) ? mraw[u] - map_row0 - slot : 0;
     }
   }
 #define LOADROWS0(buf, base)                                                      \
