@@ -91,6 +91,11 @@ int mwx_test_sample_draws(struct mwx_context* ctx, const float* probs, const flo
  * previous setting. */
 int mwx_test_set_xattn_mfs(int on);
 
+/* Decode GEMMs at more than 64 rows (beam / best-of decoders of many clips):
+ * the shared-A kernels (1, the default) or the per-strip grids (0); -1
+ * restores the MWX_DEC_SHARED default. Returns the previous setting. */
+int mwx_test_set_dec_shared(int on);
+
 /* The MX-fp8 grouped cross-attention kernel on given data: q [R][H*64] f32
  * queries (rounded to f16 by the kernel), K / V as e4m3 codes [R/nq][H][n][64]
  * with E8M0 scales [R/nq][H][n][2] (one per 32-element half), rows

@@ -58,6 +58,10 @@ for s in "$@"; do
     b5e_*)  # beam 5 on one lane with one engine knob: b5e_<VAR>_<value> (MWX_<VAR>=<value>)
       kv=${s#b5e_}; var=MWX_${kv%_*}; val=${kv##*_}
       run "$s" 500 env "$var=$val" python -u bench.py --beam 5 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    c5e_*)  # C5 on one lane with one engine knob: c5e_<VAR>_<value> (MWX_<VAR>=<value>)
+      kv=${s#c5e_}; var=MWX_${kv%_*}; val=${kv##*_}
+      run "$s" 700 env "$var=$val" python -u bench.py --fp8 --beam 5 --clip-seconds 600 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline ;;
+    sharedtests) run sharedtests 900 python -u -m pytest tests/test_gpu_shapes.py -k "row_block or beam_batch or group_of_7" -m gpu -v -s -rf --timeout 600 --timeout-method thread ;;
     abb*)  # the same for beam 5 (ablib/libmwx_<build>.so, 2 lanes)
       v=${s#abb}; [ "$v" = h ] && v=head
       run "${s}_$(date +%s)" 500 env MWX_LIB=$GRAFT_REPO_ROOT/ablib/libmwx_$v.so python -u bench.py --beam 5 --steps 4 --warmup 1 --no-cpu-baseline --no-one-lane ;;

@@ -18,6 +18,7 @@
 //                 K (or N for wide outputs), LDS reduction, one 16-column
 //                 strip per wave.
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <stdexcept>
 #include <type_traits>
@@ -851,6 +852,161 @@ __global__ __launch_bounds__(1024) void gemm_skinny(int epi, const T* __restrict
     }
 }
 
+// ---------------------------------------------------------------------------
+// Decode GEMMs at M > 64 rows (beam / best-of decoders: 160 rows at beam 5):
+// the A block of a workgroup (16*MT rows x its K range, fragment tiles) is
+// DMA'd into LDS once and shared by the workgroup's 4 waves, each of which
+// owns one 16-column strip over the whole K range. gemm_skinny / gemm_splitk
+// give every 16-column strip its own workgroup, which re-reads the whole A
+// block from L2: at 160 rows that is N / 16 reads of it (FFN1: ~130 MB of L2
+// traffic per launch, 13 us with warm weights in the chain probe).
+// Each output is formed exactly as there: NG k-groups of KCH k-steps, one
+// MFMA chain per group (the k-steps of wave g of gemm_skinny / gemm_splitk),
+// summed in wave order -- COMB 0: sequentially (gemm_skinny), COMB 1 (NG 4):
+// (g0 + g1) + (g2 + g3) (gemm_splitk) -- so the results are bit-identical.
+// 1-D grid: the nrb row-block workgroups of one (strip group, K slice) are
+// dispatched within a window of 8 * nrb ids with equal id % 8 (one XCD under
+// the round-robin placement), so they share the strips' weights in its L2.
+// ---------------------------------------------------------------------------
+template <typename T, int MT, int KCH, int NG, int COMB, bool W8>
+__global__ __launch_bounds__(256) void gemm_dec_shared(int epi, const T* __restrict__ Ap,
+                                                       const void* __restrict__ Wv,
+                                                       const uint8_t* __restrict__ Ws, int KT,
+                                                       int M, int N, int nsg, int nks, int nrb,
+                                                       float* __restrict__ Pslab, EpiParams P) {
+  static_assert(COMB == 0 || NG == 4, "split-K partials: four k-groups");
+  using V8 = typename Elt<T>::v8;
+  constexpr int KS = NG * KCH;  // k-steps of this workgroup's K range
+  __shared__ __attribute__((aligned(16))) T ash[MT * KS * 512];
+  const int L = blockIdx.x, Wd = 8 * nrb;
+  const int rb = (L % Wd) / 8, g = (L / Wd) * 8 + L % 8;
+  if (g >= nsg * nks) return;  // (workgroup-uniform: before any barrier)
+  const int ks = g / nsg, sg = g - ks * nsg;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int kt0 = ks * KS;  // first k-step of the range
+  // A block -> LDS: fragment (mt, k) of row tile rb*MT + mt is 1 KB at
+  // Ap + ((rb*MT + mt) * KT + kt0 + k) * 512; one DMA instruction per fragment
+#pragma unroll
+  for (int f = wid; f < MT * KS; f += 4) {
+    const int mt = f / KS, k = f - mt * KS;
+    const T* src = Ap + ((long)(rb * MT + mt) * KT + kt0 + k) * 512 + lane * 8;
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                     (void __attribute__((address_space(3)))*)&ash[f * 512], 16,
+                                     0, 0);
+  }
+  const int strip = sg * 4 + wid;
+  const bool live = strip * 16 < N;
+  const long f0 = (long)strip * KT + kt0;  // this wave's first weight fragment
+  V8 wb[2][KCH];
+  uint2 wraw[2][W8 ? KCH : 1];
+  uint32_t wsc[2][W8 ? KCH : 1];
+  auto load_w = [&](int buf, int grp) {
+    if (!live) return;
+    if constexpr (W8) {
+      const uint8_t* wq = reinterpret_cast<const uint8_t*>(Wv) + (f0 + grp * KCH) * 512 + lane * 8;
+#pragma unroll
+      for (int c = 0; c < KCH; ++c) {
+        wraw[buf][c] = *reinterpret_cast<const uint2*>(wq + c * 512);
+        wsc[buf][c] = Ws[(f0 + grp * KCH + c) * 16 + (lane & 15)];
+      }
+    } else {
+      const T* wt = reinterpret_cast<const T*>(Wv) + (f0 + grp * KCH) * 512 + lane * 8;
+#pragma unroll
+      for (int c = 0; c < KCH; ++c) wb[buf][c] = ld8(wt + c * 512);
+    }
+  };
+  load_w(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (this wave's A fragments have landed)
+  __syncthreads();
+  if (!live) return;  // (no barrier below)
+  if (NG > 1) load_w(1, 1);
+  f32x4 sum[MT], s23[MT];
+#pragma unroll
+  for (int grp = 0; grp < NG; ++grp) {
+    const int buf = grp & 1;
+    if constexpr (W8) {
+#pragma unroll
+      for (int c = 0; c < KCH; ++c) wb[buf][c] = dequant8<T>(wraw[buf][c], e8m0_to_f32(wsc[buf][c]));
+    }
+    f32x4 acc[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      acc[mt] = f32x4{0, 0, 0, 0};
+#pragma unroll
+      for (int c = 0; c < KCH; ++c) {
+        const V8 a = *reinterpret_cast<const V8*>(&ash[((mt * KS) + grp * KCH + c) * 512 + lane * 8]);
+        acc[mt] = Elt<T>::mfma(a, wb[buf][c], acc[mt]);
+      }
+    }
+    if (grp + 2 < NG) load_w(buf, grp + 2);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      if constexpr (COMB == 0) {
+        sum[mt] = grp == 0 ? acc[mt] : sum[mt] + acc[mt];
+      } else {
+        if (grp == 0 || grp == 2) {
+          (grp == 0 ? sum[mt] : s23[mt]) = acc[mt];
+        } else if (grp == 1) {
+          sum[mt] = sum[mt] + acc[mt];
+        } else {
+          s23[mt] = s23[mt] + acc[mt];
+        }
+      }
+    }
+  }
+  const int n = strip * 16 + (lane & 15);
+  if (n >= N) return;
+  float* Pk = COMB == 1 ? Pslab + (long)ks * M * N : nullptr;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const f32x4 v = COMB == 1 ? sum[mt] + s23[mt] : sum[mt];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = (rb * MT + mt) * 16 + (lane >> 4) * 4 + r;
+      if (m >= M) continue;
+      if constexpr (COMB == 1) {
+        Pk[(long)m * N + n] = v[r];
+      } else {
+        switch (epi) {
+          case EPI_GELU: skinny_store<EPI_GELU, T, false>(P, m, n, v[r]); break;
+          case EPI_RES: skinny_store<EPI_RES, T, false>(P, m, n, v[r]); break;
+          case EPI_F32: skinny_store<EPI_F32, T, false>(P, m, n, v[r]); break;
+          case EPI_DEC_QKV: skinny_store<EPI_DEC_QKV, T, false>(P, m, n, v[r]); break;
+          case EPI_STORE16: skinny_store<EPI_STORE16, T, false>(P, m, n, v[r]); break;
+          default: break;
+        }
+      }
+    }
+  }
+}
+
+// M > 64: the shared-A kernels (MWX_DEC_SHARED=0 or dec_shared_set(0): the
+// per-strip grids, for the A/B and the bit-identity test)
+static std::atomic<int>& dec_shared_mode() {
+  static std::atomic<int> m{-1};
+  return m;
+}
+static bool dec_shared() {
+  int v = dec_shared_mode().load();
+  if (v < 0) {
+    v = (getenv("MWX_DEC_SHARED") && atoi(getenv("MWX_DEC_SHARED")) == 0) ? 0 : 1;
+    dec_shared_mode().store(v);
+  }
+  return v != 0;
+}
+int dec_shared_set(int on) { return dec_shared_mode().exchange(on < 0 ? -1 : (on ? 1 : 0)); }
+template <typename T, int KCH, int NG, int COMB, bool W8>
+static void dec_shared_launch(int epi, const T* Ap, const void* Wp, const uint8_t* Ws, int KT,
+                              int M, int N, int nks, float* Pslab, const EpiParams& P,
+                              hipStream_t st) {
+  constexpr int MT = 2;
+  const int nsg = ((N + 15) / 16 + 3) / 4, nrb = (M + 16 * MT - 1) / (16 * MT);
+  const int groups = nsg * nks;
+  const dim3 g((groups + 7) / 8 * 8 * nrb);
+  gemm_dec_shared<T, MT, KCH, NG, COMB, W8><<<g, 256, 0, st>>>(epi, Ap, Wp, Ws, KT, M, N, nsg,
+                                                               nks, nrb, Pslab, P);
+}
+
 // (waves, k-steps per wave) for a K: all 32-deep k-steps split evenly over at
 // most 16 waves with at most 10 k-steps each. want_nw > 0: exactly that many
 // waves (FFN1 runs 4, as the chained seam's skinny consumer does, k_chain.hip)
@@ -876,6 +1032,16 @@ static bool skinny_launch(int epi, const T* Ap, const void* Wp, const uint8_t* W
                           int K, const EpiParams& P, hipStream_t st) {
   int nw = 0, kch = 0;
   if (!skinny_split(K, nw, kch, P.nw)) return false;
+  if (M > 64 && dec_shared()) {
+    // (the k-group splits of the model widths: d 1280 / 1024 / 768 / 512 / 384)
+#define DS(NWV, C)                                                                              \
+  if (nw == NWV && kch == C) {                                                                  \
+    dec_shared_launch<T, C, NWV, 0, W8>(epi, Ap, Wp, Ws, K / 32, M, N, 1, nullptr, P, st);      \
+    return true;                                                                                \
+  }
+    DS(10, 4) DS(16, 2) DS(12, 2) DS(16, 1) DS(12, 1)
+#undef DS
+  }
   const int nrb = (M + 16 * MT - 1) / (16 * MT), nx = (N + 15) / 16;
   const dim3 g(nx, nrb), b(64 * nw);
   switch (kch) {
@@ -987,6 +1153,18 @@ int gemm_splitk_partials(const T* Ap, const DecW<T>& Wd, int M, int N, int K, fl
   static const bool mt1 = !(getenv("MWX_DEC_MT1") && atoi(getenv("MWX_DEC_MT1")) == 0);
   if (mt1 && M <= 64) MT = 1;  // 16-row blocks (greedy +3%; MWX_DEC_MT1=0 for A/B)
   const int nrb = (M + 16 * MT - 1) / (16 * MT), nx = (N + 15) / 16;
+  if (M > 64 && dec_shared()) {
+#define DSK(C)                                                                                   \
+  if (kch == C) {                                                                                \
+    if (w8)                                                                                      \
+      dec_shared_launch<T, C, 4, 1, true>(0, Ap, Wp, Ws, K / 32, M, N, ks, P, EpiParams{}, st);  \
+    else                                                                                         \
+      dec_shared_launch<T, C, 4, 1, false>(0, Ap, Wp, Ws, K / 32, M, N, ks, P, EpiParams{}, st); \
+    return ks;                                                                                   \
+  }
+    DSK(1) DSK(2) DSK(3) DSK(4) DSK(5)
+#undef DSK
+  }
   const dim3 g(nx, ks, nrb);
 #define SKL(MTV, C)                                                                         \
   if (MT == MTV && kch == C) {                                                              \

@@ -230,6 +230,9 @@ void kv_append(const float* P, int KS, int pcols, const float* bias, float kscal
 // MX-fp8 grouped cross-attention on MFMA (1, default) or v_dot2 (0); -1:
 // MWX_XATTN_MFS. Returns the previous setting (the A/B tests).
 int xattn_mfs_set(int on);
+// decode GEMMs at M > 64 rows: shared-A kernels (1) or per-strip grids (0);
+// -1 restores the MWX_DEC_SHARED default. Returns the previous setting.
+int dec_shared_set(int on);
 template <typename T>
 bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float* bias,
                                  const void* kbase, const void* vbase, const int* kv_index,

@@ -217,6 +217,8 @@ def lib() -> C.CDLL:
     L.mwx_test_runahead_fallbacks.argtypes = [P, C.c_int]
     L.mwx_test_set_xattn_mfs.restype = C.c_int
     L.mwx_test_set_xattn_mfs.argtypes = [C.c_int]
+    L.mwx_test_set_dec_shared.restype = C.c_int
+    L.mwx_test_set_dec_shared.argtypes = [C.c_int]
     u8p = C.POINTER(C.c_uint8)
     L.mwx_test_xattn_mx.restype = C.c_int
     L.mwx_test_xattn_mx.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, fpp, u8p, u8p,
@@ -274,6 +276,13 @@ def set_xattn_mfs(on: Optional[bool]) -> int:
     """mwx_test_set_xattn_mfs: the MX-fp8 grouped cross-attention on MFMA
     (True) or v_dot2 (False); None: the MWX_XATTN_MFS default."""
     return lib().mwx_test_set_xattn_mfs(-1 if on is None else int(bool(on)))
+
+
+def set_dec_shared(on: Optional[bool]) -> int:
+    """mwx_test_set_dec_shared: decode GEMMs at > 64 rows through the
+    shared-A kernels (True) or the per-strip grids (False); None: the
+    MWX_DEC_SHARED default."""
+    return lib().mwx_test_set_dec_shared(-1 if on is None else int(bool(on)))
 
 
 def dequantize(qtype: int, raw: bytes, n: int) -> np.ndarray:

@@ -85,8 +85,8 @@ _RUN_BATCH = r'''
 import json, sys
 sys.path.insert(0, "sentiric-stt-whisper-service_amd")
 import mwx
-path, n, beam = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
-ctx = mwx.Context.open(path)
+path, n, beam, fp8 = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
+ctx = mwx.Context.open(path, compute=mwx.COMPUTE_MXFP8 if fp8 else mwx.COMPUTE_MODEL)
 p = ctx.default_params(mwx.SAMPLING_BEAM_SEARCH if beam > 1 else mwx.SAMPLING_GREEDY)
 if beam > 1:
     p.beam_search.beam_size = beam
@@ -100,25 +100,28 @@ print(json.dumps(out))
 '''
 
 
-@pytest.mark.parametrize("clips,beam", [(32, 1), (13, 5)])
-def test_v3_geometry_row_block_layouts_identical(v3, clips, beam):
+@pytest.mark.parametrize("clips,beam,fp8", [(32, 1, 0), (13, 5, 0), (13, 5, 1)])
+def test_v3_geometry_row_block_layouts_identical(v3, clips, beam, fp8):
     """Every decode GEMM row-block layout gives the same bits: 16-row blocks
     (MWX_DEC_MT1=1, the default at <= 64 rows) vs 32-row blocks, and for 65
-    beam rows (13 clips x beam 5: 32 + 32 + 1 rows) 32- vs 64-row blocks."""
+    beam rows (13 clips x beam 5: 32 + 32 + 1 rows) the shared-A kernels (the
+    default above 64 rows) vs the per-strip grids with 32- and 64-row blocks,
+    for 16-bit and MX-fp8 weights."""
     _, _, path = v3
     envs = [{"MWX_DEC_MT1": "1"}, {"MWX_DEC_MT1": "0"}]
     if clips * beam > 64:
-        envs = [{"MWX_SPLITK_MT": "2", "MWX_SKINNY_MT": "2"},
-                {"MWX_SPLITK_MT": "4", "MWX_SKINNY_MT": "4"}]
+        envs = [{"MWX_DEC_SHARED": "1"},
+                {"MWX_DEC_SHARED": "0", "MWX_SPLITK_MT": "2", "MWX_SKINNY_MT": "2"},
+                {"MWX_DEC_SHARED": "0", "MWX_SPLITK_MT": "4", "MWX_SKINNY_MT": "4"}]
     res = []
     for extra in envs:
         env = dict(os.environ)
         env.update(extra)
-        r = subprocess.run([sys.executable, "-c", _RUN_BATCH, path, str(clips), str(beam)],
+        r = subprocess.run([sys.executable, "-c", _RUN_BATCH, path, str(clips), str(beam), str(fp8)],
                            cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-2000:]
         res.append(json.loads(r.stdout.strip().splitlines()[-1]))
-    assert res[0] == res[1]
+    assert all(r == res[0] for r in res[1:])
     assert all(len(t) == 24 for t in res[0])
 
 
