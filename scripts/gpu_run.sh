@@ -58,9 +58,13 @@ for s in "$@"; do
     b5e_*)  # beam 5 on one lane with one engine knob: b5e_<VAR>_<value> (MWX_<VAR>=<value>)
       kv=${s#b5e_}; var=MWX_${kv%_*}; val=${kv##*_}
       run "$s" 500 env "$var=$val" python -u bench.py --beam 5 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    b1e_*)  # C3 on one lane with one engine knob: b1e_<VAR>_<value> (MWX_<VAR>=<value>)
+      kv=${s#b1e_}; var=MWX_${kv%_*}; val=${kv##*_}
+      run "$s" 400 env "$var=$val" python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
     c5e_*)  # C5 on one lane with one engine knob: c5e_<VAR>_<value> (MWX_<VAR>=<value>)
       kv=${s#c5e_}; var=MWX_${kv%_*}; val=${kv##*_}
       run "$s" 700 env "$var=$val" python -u bench.py --fp8 --beam 5 --clip-seconds 600 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline ;;
+    sharedgreedy) run sharedgreedy 600 env MWX_DEC_SHARED_MIN=17 python -u -m pytest tests/test_gpu_shapes.py -k "batch32_equals_single or row_block" -m gpu -v -s -rf --timeout 500 --timeout-method thread ;;
     sharedtests) run sharedtests 900 python -u -m pytest tests/test_gpu_shapes.py -k "row_block or beam_batch or group_of_7" -m gpu -v -s -rf --timeout 600 --timeout-method thread ;;
     abb*)  # the same for beam 5 (ablib/libmwx_<build>.so, 2 lanes)
       v=${s#abb}; [ "$v" = h ] && v=head

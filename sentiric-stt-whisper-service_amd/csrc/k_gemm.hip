@@ -980,8 +980,11 @@ __global__ __launch_bounds__(256) void gemm_dec_shared(int epi, const T* __restr
   }
 }
 
-// M > 64: the shared-A kernels (MWX_DEC_SHARED=0 or dec_shared_set(0): the
-// per-strip grids, for the A/B and the bit-identity test)
+// M > 64 (MWX_DEC_SHARED_MIN: the row threshold): the shared-A kernels
+// (MWX_DEC_SHARED=0 or dec_shared_set(0): the per-strip grids, for the A/B and
+// the bit-identity test). Row blocks of 32 (16- and 64-row blocks measured
+// slower: beam 5 849.9 / 858.5 vs 891-894, C5 957.4 / 900.0 vs 982.2; 8 strips
+// per workgroup instead of 4 neutral: 893.4 vs 892.1; r05y, r05z, r05aa)
 static std::atomic<int>& dec_shared_mode() {
   static std::atomic<int> m{-1};
   return m;
@@ -995,6 +998,10 @@ static bool dec_shared() {
   return v != 0;
 }
 int dec_shared_set(int on) { return dec_shared_mode().exchange(on < 0 ? -1 : (on ? 1 : 0)); }
+static bool dec_shared_rows(int M) {
+  static const int mn = getenv("MWX_DEC_SHARED_MIN") ? atoi(getenv("MWX_DEC_SHARED_MIN")) : 65;
+  return M >= mn && dec_shared();
+}
 template <typename T, int KCH, int NG, int COMB, bool W8>
 static void dec_shared_launch(int epi, const T* Ap, const void* Wp, const uint8_t* Ws, int KT,
                               int M, int N, int nks, float* Pslab, const EpiParams& P,
@@ -1032,7 +1039,7 @@ static bool skinny_launch(int epi, const T* Ap, const void* Wp, const uint8_t* W
                           int K, const EpiParams& P, hipStream_t st) {
   int nw = 0, kch = 0;
   if (!skinny_split(K, nw, kch, P.nw)) return false;
-  if (M > 64 && dec_shared()) {
+  if (dec_shared_rows(M)) {
     // (the k-group splits of the model widths: d 1280 / 1024 / 768 / 512 / 384)
 #define DS(NWV, C)                                                                              \
   if (nw == NWV && kch == C) {                                                                  \
@@ -1153,7 +1160,7 @@ int gemm_splitk_partials(const T* Ap, const DecW<T>& Wd, int M, int N, int K, fl
   static const bool mt1 = !(getenv("MWX_DEC_MT1") && atoi(getenv("MWX_DEC_MT1")) == 0);
   if (mt1 && M <= 64) MT = 1;  // 16-row blocks (greedy +3%; MWX_DEC_MT1=0 for A/B)
   const int nrb = (M + 16 * MT - 1) / (16 * MT), nx = (N + 15) / 16;
-  if (M > 64 && dec_shared()) {
+  if (dec_shared_rows(M)) {
 #define DSK(C)                                                                                   \
   if (kch == C) {                                                                                \
     if (w8)                                                                                      \
