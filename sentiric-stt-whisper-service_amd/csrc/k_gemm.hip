@@ -884,24 +884,19 @@ __global__ __launch_bounds__(256) void gemm_dec_shared(int epi, const T* __restr
   const int ks = g / nsg, sg = g - ks * nsg;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int kt0 = ks * KS;  // first k-step of the range
-  // A block -> LDS: fragment (mt, k) of row tile rb*MT + mt is 1 KB at
-  // Ap + ((rb*MT + mt) * KT + kt0 + k) * 512; one DMA instruction per fragment
-#pragma unroll
-  for (int f = wid; f < MT * KS; f += 4) {
-    const int mt = f / KS, k = f - mt * KS;
-    const T* src = Ap + ((long)(rb * MT + mt) * KT + kt0 + k) * 512 + lane * 8;
-    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
-                                     (void __attribute__((address_space(3)))*)&ash[f * 512], 16,
-                                     0, 0);
-  }
   const int strip = sg * 4 + wid;
   const bool live = strip * 16 < N;
-  const long f0 = (long)strip * KT + kt0;  // this wave's first weight fragment
-  V8 wb[2][KCH];
-  uint2 wraw[2][W8 ? KCH : 1];
-  uint32_t wsc[2][W8 ? KCH : 1];
+  // (a wave past the last strip loads the last strip's weights: straight-line
+  // loads keep the compiler's wait counts exact; it stores nothing)
+  const long f0 = (long)min(strip, (N - 1) >> 4) * KT + kt0;  // this wave's first weight fragment
+  // WB k-groups of weights in flight per wave, the first WB issued before the
+  // A DMA (their latencies overlap). MX-fp8 weights: 4 (C5 one lane 985.6 ->
+  // 994.8 against 2, same box, r05ad); 16-bit: 2 (4 measured 891.6 -> 887.0)
+  constexpr int WB = NG < (W8 ? 4 : 2) ? NG : (W8 ? 4 : 2);
+  V8 wb[WB][KCH];
+  uint2 wraw[WB][W8 ? KCH : 1];
+  uint32_t wsc[WB][W8 ? KCH : 1];
   auto load_w = [&](int buf, int grp) {
-    if (!live) return;
     if constexpr (W8) {
       const uint8_t* wq = reinterpret_cast<const uint8_t*>(Wv) + (f0 + grp * KCH) * 512 + lane * 8;
 #pragma unroll
@@ -915,15 +910,30 @@ __global__ __launch_bounds__(256) void gemm_dec_shared(int epi, const T* __restr
       for (int c = 0; c < KCH; ++c) wb[buf][c] = ld8(wt + c * 512);
     }
   };
-  load_w(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (this wave's A fragments have landed)
-  __syncthreads();
+#pragma unroll
+  for (int b = 0; b < WB; ++b) load_w(b, b);
+  // A block -> LDS: fragment (mt, k) of row tile rb*MT + mt is 1 KB at
+  // Ap + ((rb*MT + mt) * KT + kt0 + k) * 512; one DMA instruction per fragment
+#pragma unroll
+  for (int f = wid; f < MT * KS; f += 4) {
+    const int mt = f / KS, k = f - mt * KS;
+    const T* src = Ap + ((long)(rb * MT + mt) * KT + kt0 + k) * 512 + lane * 8;
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                     (void __attribute__((address_space(3)))*)&ash[f * 512], 16,
+                                     0, 0);
+  }
+  // this wave's A fragments have landed (and its first weight groups: the
+  // two streams' latencies overlap)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // (every wave has waited for its own DMA; then a raw barrier)
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
   if (!live) return;  // (no barrier below)
-  if (NG > 1) load_w(1, 1);
   f32x4 sum[MT], s23[MT];
 #pragma unroll
   for (int grp = 0; grp < NG; ++grp) {
-    const int buf = grp & 1;
+    const int buf = grp % WB;
     if constexpr (W8) {
 #pragma unroll
       for (int c = 0; c < KCH; ++c) wb[buf][c] = dequant8<T>(wraw[buf][c], e8m0_to_f32(wsc[buf][c]));
@@ -938,7 +948,7 @@ __global__ __launch_bounds__(256) void gemm_dec_shared(int epi, const T* __restr
         acc[mt] = Elt<T>::mfma(a, wb[buf][c], acc[mt]);
       }
     }
-    if (grp + 2 < NG) load_w(buf, grp + 2);
+    if (grp + WB < NG) load_w(buf, grp + WB);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       if constexpr (COMB == 0) {
