@@ -892,6 +892,8 @@ __global__ __launch_bounds__(256) void gemm_dec_shared(int epi, const T* __restr
   // WB k-groups of weights in flight per wave, the first WB issued before the
   // A DMA (their latencies overlap). MX-fp8 weights: 4 (C5 one lane 985.6 ->
   // 994.8 against 2, same box, r05ad); 16-bit: 2 (4 measured 891.6 -> 887.0)
+  // (all NG groups in flight measured slower: FFN1 at 160 rows 13.96 vs 11.47
+  // µs, beam 5 878.9 vs 898.1, C5 983.6 vs 991.5; r05ah)
   constexpr int WB = NG < (W8 ? 4 : 2) ? NG : (W8 ? 4 : 2);
   V8 wb[WB][KCH];
   uint2 wraw[WB][W8 ? KCH : 1];
