@@ -102,6 +102,7 @@ for s in "$@"; do
     probewb) for k in logits skinny_fc1 splitk_; do run "probewb_$k" 200 env LD_LIBRARY_PATH=$GRAFT_REPO_ROOT/ablib/wball PROBE_ONLY="$k" ./scripts/probe/dec_chain_probe 160 10 || exit 6; done ;;
     b5w) run b5w 500 env MWX_LIB=$GRAFT_REPO_ROOT/ablib/wball/libmwx.so python -u bench.py --beam 5 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
     c5w) run c5w 700 env MWX_LIB=$GRAFT_REPO_ROOT/ablib/wball/libmwx.so python -u bench.py --fp8 --beam 5 --clip-seconds 600 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline ;;
+    probehalf) for v in 1 0; do for k in logits skinny_fc1; do run "probehalf_${v}_$k" 200 env MWX_DEC_SHARED_HALF=$v PROBE_ONLY="$k" ./scripts/probe/dec_chain_probe 160 10 || exit 6; done; done ;;
     probelaunch) for k in launch "empty 512" res_ splitk skinny ln_dec; do run "probe_$(echo $k | tr -d ' ')" 200 env PROBE_ONLY="$k" ./scripts/probe/dec_chain_probe 32 10 || exit 6; done ;;
     stream) run stream 300 python -u bench.py --stream --arch base --wtype f16 --steps 3 --warmup 1 ;;
     streamr) run streamr 300 python -u bench.py --stream --rich --arch base --wtype f16 --steps 3 --warmup 1 ;;
