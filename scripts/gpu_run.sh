@@ -138,6 +138,12 @@ for s in "$@"; do
     pmcb5)  # instruction mix / stall counters of the beam-5 (and fp8) kernels
       (cd /tmp && run pmcb5 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d "$O/${TAG}_pmcb5" -o pmc -- $B --beam 5 --lanes 1 --steps 1 --warmup 0 --decode-steps 8 --no-cpu-baseline) || exit 5
       (cd /tmp && run pmcc5 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d "$O/${TAG}_pmcc5" -o pmc -- $B --fp8 --beam 5 --lanes 1 --steps 1 --warmup 0 --decode-steps 8 --no-cpu-baseline) || exit 5 ;;
+    pmcb)  # beam 5 bf16 only: mix, LDS / MFMA, fetch (the 160-row decode chain)
+      for x in "mix:SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY" "lds:SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE" "fetch:FETCH_SIZE"; do
+        n=${x%%:*}; c=${x#*:}
+        (cd /tmp && run pmcb_$n 400 rocprofv3 --pmc $c --output-format csv -d "$O/${TAG}_pmcb_$n" -o pmc -- $B --beam 5 --lanes 1 --steps 1 --warmup 0 --decode-steps 24 --no-cpu-baseline) || exit 5
+        python3 scripts/pmc_mix.py "$O/${TAG}_pmcb_$n" 14 > "$O/${TAG}_pmcb_$n.md" || exit 5
+      done ;;
     pmcx)  # the grouped cross-attentions (beam 5 bf16, C5 MX-fp8): mix, LDS / MFMA / occupancy, FETCH
       for leg in b5 c5; do
         F=""; [ $leg = c5 ] && F="--fp8"
