@@ -66,6 +66,8 @@ for s in "$@"; do
       kv=${s#c5e_}; var=MWX_${kv%_*}; val=${kv##*_}
       run "$s" 700 env "$var=$val" python -u bench.py --fp8 --beam 5 --clip-seconds 600 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline ;;
     sharedgreedy) run sharedgreedy 600 env MWX_DEC_SHARED_MIN=17 python -u -m pytest tests/test_gpu_shapes.py -k "batch32_equals_single or row_block" -m gpu -v -s -rf --timeout 500 --timeout-method thread ;;
+    sharedkh2) run sharedkh2 600 env MWX_DEC_SHARED_KH=2 python -u -m pytest tests/test_gpu_shapes.py -k "row_block or beam_batch" -m gpu -v -s -rf --timeout 500 --timeout-method thread ;;
+    probekh) for v in 1 2; do for k in logits skinny_fc1; do run "probekh_${v}_$k" 200 env MWX_DEC_SHARED_KH=$v PROBE_ONLY="$k" ./scripts/probe/dec_chain_probe 160 10 || exit 6; done; done ;;
     sharedtests) run sharedtests 900 python -u -m pytest tests/test_gpu_shapes.py -k "row_block or beam_batch or group_of_7" -m gpu -v -s -rf --timeout 600 --timeout-method thread ;;
     abb*)  # the same for beam 5 (ablib/libmwx_<build>.so, 2 lanes)
       v=${s#abb}; [ "$v" = h ] && v=head
