@@ -54,6 +54,7 @@ run() {  # name, seconds, command...
 }
 for s in "$@"; do
   case $s in
+    c5pad) run c5pad 700 env MWX_LIB=$GRAFT_REPO_ROOT/ablib/pad/libmwx.so python -u bench.py --fp8 --beam 5 --clip-seconds 600 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline ;;
     c5h) run c5h 700 env MWX_LIB=$GRAFT_REPO_ROOT/ablib/libmwx_head.so python -u bench.py --fp8 --beam 5 --clip-seconds 600 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline ;;
     b5h) run b5h 500 env MWX_LIB=$GRAFT_REPO_ROOT/ablib/libmwx_head.so python -u bench.py --beam 5 --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
     b5e_*)  # beam 5 on one lane with one engine knob: b5e_<VAR>_<value> (MWX_<VAR>=<value>)

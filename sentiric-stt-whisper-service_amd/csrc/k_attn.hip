@@ -888,7 +888,8 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
   // operand the query's f16 P itself (no per-key scale arithmetic). The
   // 32-B column blocks of a row are XOR-swizzled by (row >> 1) & 3, so a
   // 16-lane group's four rows hit distinct banks.
-  __shared__ __attribute__((aligned(16))) _Float16 vtile[MFS ? 4 : 1][MFS ? 32 * 64 : 8];
+  // (256-B aligned: the block swizzle assumes a tile row starts at bank 0)
+  __shared__ __attribute__((aligned(256))) _Float16 vtile[MFS ? 4 : 1][MFS ? 32 * 64 : 8];
   const int nt32 = (n + 31) >> 5;
   const int vrow = lane >> 1, vch = 2 * (lane & 1);
   // VB tiles in flight per wave (build constant XATTN_VB)
