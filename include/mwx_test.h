@@ -52,6 +52,12 @@ int mwx_test_dequantize(int type, const void* src, long n, float* dst);
 int mwx_test_decode_counters(struct mwx_state* state, long* steps, long* prefill_positions,
                              int reset);
 
+/* Window counters of a state (the first state of a batch drives it): clip
+ * windows decoded and decode attempts run (one per window and temperature
+ * tried, so attempts - windows = temperature-fallback re-runs) since the
+ * last reset. reset != 0 zeroes them after reading. */
+int mwx_test_window_counters(struct mwx_state* state, long* windows, long* attempts, int reset);
+
 /* Run-ahead decode attempts a state redid on the host-driven token loop
  * because the device's advance and the host's replay disagreed (or
  * MWX_TEST_RA_MISMATCH=k forced it at step k). reset != 0 zeroes it. */
@@ -95,6 +101,17 @@ int mwx_test_set_xattn_mfs(int on);
  * the shared-A kernels (1, the default) or the per-strip grids (0); -1
  * restores the MWX_DEC_SHARED default. Returns the previous setting. */
 int mwx_test_set_dec_shared(int on);
+
+/* The encoder GEMM's 8-phase main loop (bit-identical to the default 2-stage
+ * ring) on (1) / off (0) / back to the MWX_GEMM_8PH environment default (-1).
+ * Returns the previous mode. */
+int mwx_test_set_gemm_8ph(int on);
+
+/* Fault injection of the run-ahead safety net: run-ahead step `step` of every
+ * later attempt is treated as a device/host disagreement (-1: none; -2: back
+ * to the MWX_TEST_RA_MISMATCH environment default). Returns the previous
+ * setting. */
+long mwx_test_set_ra_mismatch(long step);
 
 /* The MX-fp8 grouped cross-attention kernel on given data: q [R][H*64] f32
  * queries (rounded to f16 by the kernel), K / V as e4m3 codes [R/nq][H][n][64]

@@ -30,6 +30,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <sys/stat.h>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -151,6 +152,7 @@ struct Model {
   int num_languages = 0;
   std::map<std::string, Tensor> t;
   int flags = 0;
+  std::string key;  // file identity + flags: the encoder / cross-K/V caches' key
 
   const float* w(const std::string& n) const {
     auto it = t.find(n);
@@ -703,6 +705,32 @@ static void attention(const Model& m, const float* Q, const float* K, const floa
 // < 0 runs all layers.
 static int g_enc_layer_limit = -1;
 
+// Results cache of the oracle's most expensive pure functions (the encoder
+// and the cross K/V of a window): at large-v3 depth one encode costs a minute
+// of CPU and the GPU test suite asks for the same window (same model file,
+// same mel frames) in several tests. Keyed by the model's identity and an
+// FNV-1a hash of the exact input bytes; a few entries, oldest dropped first.
+static uint64_t fnv1a(const void* p, size_t n, uint64_t h = 1469598103934665603ull) {
+  const unsigned char* b = (const unsigned char*)p;
+  for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
+  return h;
+}
+template <class V>
+struct ResultCache {
+  size_t cap;
+  std::vector<std::pair<std::string, V>> e;
+  const V* get(const std::string& k) const {
+    for (const auto& x : e)
+      if (x.first == k) return &x.second;
+    return nullptr;
+  }
+  void put(const std::string& k, const V& v) {
+    if (e.size() >= cap) e.erase(e.begin());
+    e.emplace_back(k, v);
+  }
+};
+static ResultCache<std::vector<float>> g_enc_cache{8, {}};
+
 // Encodes the 2*n_ctx mel frames starting at `seek`; out = embd_enc [n_ctx][D].
 static void encode(const Model& m, const Mel& mel, int seek, std::vector<float>& out) {
   const int n_ctx = m.n_audio_ctx, D = m.n_audio_state, H = m.n_audio_head;
@@ -711,6 +739,12 @@ static void encode(const Model& m, const Mel& mel, int seek, std::vector<float>&
   const int i0 = std::min(seek, mel.n_len), i1 = std::min(seek + T, mel.n_len);
   for (int j = 0; j < m.n_mels; ++j)
     for (int i = i0; i < i1; ++i) x[(size_t)j * T + (i - i0)] = mel.data[(size_t)j * mel.n_len + i];
+  const std::string ckey = m.key + "|enc|" + std::to_string(g_enc_layer_limit) + "|" +
+                           std::to_string(fnv1a(x.data(), x.size() * sizeof(float)));
+  if (const auto* hit = m.key.empty() ? nullptr : g_enc_cache.get(ckey)) {
+    out = *hit;
+    return;
+  }
   std::vector<float> h1((size_t)T * D), h2((size_t)n_ctx * D);
   conv1d(m, m.w("encoder.conv1.weight"), m.w("encoder.conv1.bias"), x.data(), m.n_mels, T, D, 1, h1.data());
   for (auto& v : h1) v = gelu(m, v);
@@ -752,13 +786,28 @@ static void encode(const Model& m, const Mel& mel, int seek, std::vector<float>&
   }
   out.resize((size_t)M * D);
   layer_norm(inp.data(), m.w("encoder.ln_post.weight"), m.w("encoder.ln_post.bias"), M, D, out.data());
+  if (!m.key.empty()) g_enc_cache.put(ckey, out);
 }
 
 // kv_cross: per decoder layer K = f16(Kscale * Wk enc), V = f16(Wv enc + b)
 struct Cross {
   std::vector<float> k, v;  // [n_layer][n_ctx][D]
 };
+static ResultCache<Cross> g_cross_cache{2, {}};
 static void cross(const Model& m, const std::vector<float>& enc, Cross& c) {
+  const std::string ckey = m.key + "|cross|" + std::to_string(fnv1a(enc.data(), enc.size() * sizeof(float)));
+  if (const auto* hit = m.key.empty() ? nullptr : g_cross_cache.get(ckey)) {
+    c = *hit;
+    return;
+  }
+  struct Put {
+    const std::string& k;
+    Cross& c;
+    const bool on;
+    ~Put() {
+      if (on) g_cross_cache.put(k, c);
+    }
+  } put{ckey, c, !m.key.empty()};
   const int M = m.n_audio_ctx, D = m.n_text_state, L = m.n_text_layer;
   const float Kscale = powf((float)(D / m.n_text_head), -0.25f);
   c.k.resize((size_t)L * M * D);
@@ -932,29 +981,103 @@ enum TraceKind {
                     // (upstream std::sort leaves their order unspecified: DESIGN §2 D5)
   TR_STATUS = 9,    // decoder state after a step: a = completed + 2 failed, b = result_len
 };
+// a, b: the outcome taken. Follow mode (below) may override the oracle's own
+// outcome: then forced = 1, (own_a, own_b) is what the oracle's arithmetic
+// decided and fmargin how far that arithmetic is from the taken outcome (in
+// the kind's own units: cumulative probability for draws, log-prob for argmax
+// / ts_mass, summed log-prob for assign, score for best, the threshold
+// quantity for fallback / no_speech). Draws also record [lo, hi), the taken
+// id's interval of the normalised cumulative probabilities.
 struct TraceEv {
   int kind, seek, it, step, dec, a, b;
   double margin, v;
+  int forced = 0, own_a = 0, own_b = 0;
+  double fmargin = 0.0, lo = 0.0, hi = 0.0;
 };
 static bool g_trace_on = false;
 static std::vector<TraceEv> g_trace;
 static struct { int seek = 0, it = 0, step = -1, dec = 0; } g_tctx;
-static void trace(int kind, int a, int b, double margin, double v = 0.0) {
-  if (g_trace_on)
-    g_trace.push_back({kind, g_tctx.seek, g_tctx.it, g_tctx.step, g_tctx.dec, a, b, margin, v});
+static TraceEv& trace(int kind, int a, int b, double margin, double v = 0.0) {
+  static TraceEv sink;
+  if (!g_trace_on) return sink = TraceEv{};
+  g_trace.push_back({kind, g_tctx.seek, g_tctx.it, g_tctx.step, g_tctx.dec, a, b, margin, v});
+  return g_trace.back();
 }
-// margin of a libstdc++ discrete_distribution draw: rng is the generator
-// state BEFORE the draw (its uniform is generate_canonical<double, 53>, the
-// search lower_bound over the normalised partial sums)
-static void trace_draw(const std::vector<float>& probs, std::mt19937 rng, int k, int id) {
-  if (!g_trace_on) return;
+
+// Follow mode (test hook, orc_trace_follow): full() runs on its own logits but
+// takes, at every traced decision, the outcome a guide trace recorded — the
+// oracle's loop replayed on the device's logits. Where the two outcomes differ
+// the event is marked forced, so the run continues on the device's path and
+// every later decision is still compared against the oracle's own arithmetic
+// on that path (tests/test_gpu_beam_oracle.py). A guide event of another kind
+// or place, or a structural event (status, exact tie) that differs, ends
+// following: g_follow_break = that event's index.
+static bool g_follow_on = false;
+static std::vector<TraceEv> g_follow;
+static long g_follow_break = -1;
+static const TraceEv* follow(int kind) {
+  if (!g_follow_on || !g_trace_on) return nullptr;
+  const size_t i = g_trace.size();  // the index the event about to be traced gets
+  const TraceEv* g = i < g_follow.size() ? &g_follow[i] : nullptr;
+  if (!g || g->kind != kind || g->seek != g_tctx.seek || g->it != g_tctx.it ||
+      g->step != g_tctx.step || g->dec != g_tctx.dec) {
+    g_follow_on = false;
+    g_follow_break = (long)i;
+    return nullptr;
+  }
+  return g;
+}
+static void follow_structural(int a, int b) {  // after tracing a status / tie event
+  if (!g_follow_on) return;
+  const TraceEv& e = g_trace.back();
+  const TraceEv& g = g_follow[g_trace.size() - 1];
+  if (g.a != a || g.b != b) {
+    g_follow_on = false;
+    g_follow_break = (long)g_trace.size() - 1;
+    (void)e;
+  }
+}
+static void mark_forced(TraceEv& e, int own_a, int own_b, double fmargin) {
+  e.forced = 1;
+  e.own_a = own_a;
+  e.own_b = own_b;
+  e.fmargin = fmargin;
+}
+
+// The decision of a libstdc++ discrete_distribution draw. rng is the
+// generator state BEFORE the draw (its uniform is generate_canonical<double,
+// 53>, the search lower_bound over the normalised partial sums), id the
+// oracle's own outcome. Traces the draw (margin = distance of u to the nearest
+// boundary of id's interval) and returns the id to take: in follow mode the
+// guide's, with fmargin = the distance of u to that id's interval.
+static int trace_draw(const std::vector<float>& probs, std::mt19937 rng, int k, int id) {
+  if (!g_trace_on) return id;
+  const TraceEv* g = follow(TR_DRAW);
+  const int take = g ? g->b : id;
   const double u = std::generate_canonical<double, std::numeric_limits<double>::digits>(rng);
   double sum = 0.0;
   for (float p : probs) sum += p;
-  double lo = 0.0;
-  for (int i = 0; i < id; ++i) lo += probs[i] / sum;
-  const double hi = lo + probs[id] / sum;
-  trace(TR_DRAW, k, id, std::min(u - lo, hi - u), u);
+  auto interval = [&](int j, double& lo, double& hi) {
+    lo = 0.0;
+    for (int i = 0; i < j; ++i) lo += probs[i] / sum;
+    hi = lo + probs[j] / sum;
+  };
+  double lo, hi;
+  interval(id, lo, hi);
+  const double margin = std::min(u - lo, hi - u);
+  if (take == id) {
+    TraceEv& e = trace(TR_DRAW, k, id, margin, u);
+    e.lo = lo;
+    e.hi = hi;
+    return id;
+  }
+  double flo, fhi;
+  interval(take, flo, fhi);
+  TraceEv& e = trace(TR_DRAW, k, take, margin, u);
+  e.lo = flo;
+  e.hi = fhi;
+  mark_forced(e, k, id, u < flo ? flo - u : u - fhi);
+  return take;
 }
 
 static const std::vector<std::string> kNonSpeech = {
@@ -1051,8 +1174,18 @@ static void process_logits(const Model& m, const Params& P, Decoder& dec, const 
       if (lse > 0.0f) ts_logprob = logf(lse) + lmax;
     }
     const float max_text = *std::max_element(dec.logprobs.begin(), dec.logprobs.begin() + m.beg);
-    trace(TR_TSMASS, ts_logprob > max_text, 0, fabs((double)ts_logprob - (double)max_text));
-    if (ts_logprob > max_text) {
+    bool forced_ts = ts_logprob > max_text;
+    {
+      const TraceEv* g = follow(TR_TSMASS);
+      const double mg = fabs((double)ts_logprob - (double)max_text);
+      if (g && g->a != (int)forced_ts) {
+        mark_forced(trace(TR_TSMASS, g->a, 0, mg), forced_ts, 0, mg);
+        forced_ts = g->a != 0;
+      } else {
+        trace(TR_TSMASS, forced_ts, 0, mg);
+      }
+    }
+    if (forced_ts) {
       for (int i = 0; i < m.beg; ++i) {
         logits[i] = -INFINITY;
         dec.logprobs[i] = -INFINITY;
@@ -1093,13 +1226,22 @@ static TokenData sample_token(const Model& m, Decoder& dec, bool best) {
       float second = -INFINITY;
       for (int i = 0; i < n; ++i)
         if (i != r.id && lp[i] > second) second = lp[i];
-      trace(TR_ARGMAX, 0, r.id, (double)r.plog - (double)second);
+      const TraceEv* g = follow(TR_ARGMAX);
+      if (g && g->b != r.id) {
+        mark_forced(trace(TR_ARGMAX, 0, g->b, (double)r.plog - (double)second), 0, r.id,
+                    (double)r.plog - (double)lp[g->b]);
+        r.id = g->b;
+        r.p = probs[r.id];
+        r.plog = lp[r.id];
+      } else {
+        trace(TR_ARGMAX, 0, r.id, (double)r.plog - (double)second);
+      }
     }
   } else {
     std::discrete_distribution<> dist(probs.begin(), probs.end());
     const std::mt19937 before = dec.rng;
     r.id = dist(dec.rng);
-    trace_draw(probs, before, 0, r.id);
+    r.id = trace_draw(probs, before, 0, r.id);
     r.p = probs[r.id];
     r.plog = lp[r.id];
   }
@@ -1140,7 +1282,7 @@ static std::vector<TokenData> sample_topk(const Model& m, Decoder& dec, int k) {
     TokenData r;
     const std::mt19937 before = dec.rng;
     r.id = dist(dec.rng);
-    trace_draw(probs, before, i, r.id);
+    r.id = trace_draw(probs, before, i, r.id);
     r.tid = tid;
     r.p = probs[r.id];
     r.plog = lp[r.id];
@@ -1404,6 +1546,13 @@ typedef void (*ExtLogitsFn)(void* user, const int* tokens, int n, float* logits_
 static ExtEncodeFn g_ext_encode = nullptr;
 static ExtLogitsFn g_ext_logits = nullptr;
 static void* g_ext_user = nullptr;
+// Logits tap (test hook): full() on its own logits hands every decoded row
+// (the context it was decoded for, its last-position logits) to this callback,
+// so a test measures the oracle-vs-device logits error on exactly the prefixes
+// both runs decoded.
+typedef void (*TapFn)(void* user, const int* tokens, int n, const float* logits_last);
+static TapFn g_tap = nullptr;
+static void* g_tap_user = nullptr;
 
 static int full(const Model& m, Params P, const float* samples, int n_samples, Result& R) {
   R.segs.clear();
@@ -1514,6 +1663,7 @@ static int full(const Model& m, Params P, const float* samples, int n_samples, R
       } else {
         decode(m, cr, decs[0].kv, prompt.data(), (int)prompt.size(), 0, logits);
         last = logits.data() + (size_t)(prompt.size() - 1) * m.n_vocab;
+        if (g_tap) g_tap(g_tap_user, prompt.data(), (int)prompt.size(), last);
       }
       {
         std::vector<float> l(last, last + m.n_vocab), lp(m.n_vocab), pr(m.n_vocab);
@@ -1560,8 +1710,14 @@ static int full(const Model& m, Params P, const float* samples, int n_samples, R
             for (size_t c = 1; c < cands.size(); ++c)
               if (cands[c].seq.sum_logprobs_all == cands[c - 1].seq.sum_logprobs_all &&
                   cands[c].decoder_idx == cands[c - 1].decoder_idx &&
-                  !tokens_equal(cands[c].seq, cands[c - 1].seq))
-                trace(TR_EXACT_TIE, cands[c].decoder_idx, cands[c].seq.tokens.back().id, 0.0);
+                  !tokens_equal(cands[c].seq, cands[c - 1].seq)) {
+                if (follow(TR_EXACT_TIE)) {
+                  trace(TR_EXACT_TIE, cands[c].decoder_idx, cands[c].seq.tokens.back().id, 0.0);
+                  follow_structural(cands[c].decoder_idx, cands[c].seq.tokens.back().id);
+                } else {
+                  trace(TR_EXACT_TIE, cands[c].decoder_idx, cands[c].seq.tokens.back().id, 0.0);
+                }
+              }
           }
           // distance in sum_logprobs_all from candidate c to the nearest
           // candidate before / after it that is a different sequence
@@ -1586,10 +1742,34 @@ static int full(const Model& m, Params P, const float* samples, int n_samples, R
             if (d.completed || d.failed) continue;
             if (cur_c >= cands.size()) cur_c = 0;
             const size_t cur_pos = cur_c;
-            const BeamCand& cur = cands[cur_c++];
             g_tctx.dec = j;
-            trace(TR_ASSIGN, cur.decoder_idx, cur.seq.tokens.back().id, assign_margin(cur_pos),
-                  cur.seq.sum_logprobs_all);
+            const double own_margin = assign_margin(cur_pos);
+            const TraceEv* g = follow(TR_ASSIGN);
+            if (g && (g->a != cands[cur_pos].decoder_idx || g->b != cands[cur_pos].seq.tokens.back().id)) {
+              // the guide took another candidate here: the first one after this
+              // position with its (source decoder, last token) moves up to it
+              // (the device ranked it higher: a reorder within the logits noise)
+              size_t f = cur_pos + 1;
+              while (f < cands.size() &&
+                     !(cands[f].decoder_idx == g->a && cands[f].seq.tokens.back().id == g->b))
+                ++f;
+              if (f < cands.size()) {
+                const int oa = cands[cur_pos].decoder_idx, ob = cands[cur_pos].seq.tokens.back().id;
+                const double gap = cands[cur_pos].seq.sum_logprobs_all - cands[f].seq.sum_logprobs_all;
+                std::rotate(cands.begin() + cur_pos, cands.begin() + f, cands.begin() + f + 1);
+                mark_forced(trace(TR_ASSIGN, g->a, g->b, own_margin, cands[cur_pos].seq.sum_logprobs_all),
+                            oa, ob, gap);
+              } else {  // not among this step's candidates: a structural difference
+                trace(TR_ASSIGN, cands[cur_pos].decoder_idx, cands[cur_pos].seq.tokens.back().id,
+                      own_margin, cands[cur_pos].seq.sum_logprobs_all);
+                g_follow_on = false;
+                g_follow_break = (long)g_trace.size() - 1;
+              }
+            } else {
+              trace(TR_ASSIGN, cands[cur_pos].decoder_idx, cands[cur_pos].seq.tokens.back().id,
+                    own_margin, cands[cur_pos].seq.sum_logprobs_all);
+            }
+            const BeamCand& cur = cands[cur_c++];
             while (cands.size() > cur_c && tokens_equal(cands[cur_c].seq, cur.seq) && i > 0) ++cur_c;
             d.seek_delta = cur.seek_delta;
             d.has_ts = cur.has_ts;
@@ -1650,7 +1830,10 @@ static int full(const Model& m, Params P, const float* samples, int n_samples, R
         for (int j = 0; j < n_cur; ++j) {
           if (!(decs[j].completed || decs[j].failed)) all = false;
           g_tctx.dec = j;
-          trace(TR_STATUS, decs[j].completed + 2 * decs[j].failed, decs[j].seq.result_len, INFINITY);
+          const int st = decs[j].completed + 2 * decs[j].failed;
+          const bool fl = follow(TR_STATUS) != nullptr;
+          trace(TR_STATUS, st, decs[j].seq.result_len, INFINITY);
+          if (fl) follow_structural(st, decs[j].seq.result_len);
         }
         if (all) break;
         const int n_past = (int)prompt.size() + i;
@@ -1666,6 +1849,11 @@ static int full(const Model& m, Params P, const float* samples, int n_samples, R
             g_ext_logits(g_ext_user, ctxt.data(), (int)ctxt.size(), logits.data());
           } else {
             decode(m, cr, d.kv, &tok, 1, n_past, logits);
+            if (g_tap) {
+              std::vector<int> ctxt(prompt);
+              for (const auto& t : d.seq.tokens) ctxt.push_back(t.id);
+              g_tap(g_tap_user, ctxt.data(), (int)ctxt.size(), logits.data());
+            }
           }
           process_logits(m, P, d, logits.data(), t_cur);
         }
@@ -1692,7 +1880,20 @@ static int full(const Model& m, Params P, const float* samples, int n_samples, R
         for (int j = 0; j < n_cur; ++j)
           if (!decs[j].failed && j != best_id && !tokens_equal(decs[j].seq, decs[best_id].seq))
             runner = std::max(runner, decs[j].seq.score);
-        trace(TR_BEST, best_id, decs[best_id].seq.result_len, best_score - runner, best_score);
+        const TraceEv* g = follow(TR_BEST);
+        if (g && g->a != best_id && g->a >= 0 && g->a < n_cur && !decs[g->a].failed) {
+          const int own = best_id;
+          best_id = g->a;
+          mark_forced(trace(TR_BEST, best_id, decs[best_id].seq.result_len, best_score - runner,
+                            decs[best_id].seq.score),
+                      own, decs[own].seq.result_len, best_score - decs[best_id].seq.score);
+        } else {
+          trace(TR_BEST, best_id, decs[best_id].seq.result_len, best_score - runner, best_score);
+          if (g && g->a != best_id) {  // the guide's best decoder failed here
+            g_follow_on = false;
+            g_follow_break = (long)g_trace.size() - 1;
+          }
+        }
       }
       bool success = true;
       if (it != (int)temps.size() - 1) {
@@ -1702,9 +1903,20 @@ static int full(const Model& m, Params P, const float* samples, int n_samples, R
         if (g_trace_on) {
           const double ga = (double)P.logprob_thold - d.seq.avg_logprobs;  // > 0: below
           const double gn = (double)P.no_speech_thold - no_speech_prob;
-          trace(TR_FALLBACK, success, d.failed,
-                d.failed ? INFINITY : (success ? std::max(ga > 0 ? 0.0 : -ga, gn > 0 ? 0.0 : -gn)
-                                               : std::min(ga, gn)));
+          const double mg = d.failed ? INFINITY
+                                     : (success ? std::max(ga > 0 ? 0.0 : -ga, gn > 0 ? 0.0 : -gn)
+                                                : std::min(ga, gn));
+          const TraceEv* g = follow(TR_FALLBACK);
+          if (g && g->a != (int)success && !d.failed) {
+            mark_forced(trace(TR_FALLBACK, g->a, d.failed, mg), success, d.failed, mg);
+            success = g->a != 0;
+          } else {
+            trace(TR_FALLBACK, success, d.failed, mg);
+            if (g && g->a != (int)success) {
+              g_follow_on = false;
+              g_follow_break = (long)g_trace.size() - 1;
+            }
+          }
         }
       }
       if (success) break;
@@ -1719,12 +1931,19 @@ static int full(const Model& m, Params P, const float* samples, int n_samples, R
         for (const auto& t : toks) ids.push_back(t.id);
         R.window_tokens.push_back(ids);
       }
-      const bool is_no_speech = no_speech_prob > P.no_speech_thold && best.seq.avg_logprobs < P.logprob_thold;
+      bool is_no_speech = no_speech_prob > P.no_speech_thold && best.seq.avg_logprobs < P.logprob_thold;
       if (g_trace_on) {
         const double gn = (double)no_speech_prob - P.no_speech_thold;  // > 0: above
         const double ga = (double)P.logprob_thold - best.seq.avg_logprobs;
-        trace(TR_NOSPEECH, is_no_speech, 0,
-              is_no_speech ? std::min(gn, ga) : std::max(gn > 0 ? 0.0 : -gn, ga > 0 ? 0.0 : -ga));
+        const double mg =
+            is_no_speech ? std::min(gn, ga) : std::max(gn > 0 ? 0.0 : -gn, ga > 0 ? 0.0 : -ga);
+        const TraceEv* g = follow(TR_NOSPEECH);
+        if (g && g->a != (int)is_no_speech) {
+          mark_forced(trace(TR_NOSPEECH, g->a, 0, mg), is_no_speech, 0, mg);
+          is_no_speech = g->a != 0;
+        } else {
+          trace(TR_NOSPEECH, is_no_speech, 0, mg);
+        }
       }
       prompt_past.clear();
       if (prompt.front() == m.prev)
@@ -1788,6 +2007,13 @@ extern "C" {
 void* orc_load(const char* path, int flags) {
   auto* m = new Model();
   m->flags = flags;
+  {
+    struct stat st;
+    if (stat(path, &st) == 0)
+      m->key = std::string(path) + "|" + std::to_string((long long)st.st_size) + "|" +
+               std::to_string((long long)st.st_mtim.tv_sec) + "." +
+               std::to_string((long long)st.st_mtim.tv_nsec) + "|" + std::to_string(flags);
+  }
   if (!load(path, *m)) {
     delete m;
     return nullptr;
@@ -1847,13 +2073,32 @@ void orc_trace_ctx(int* out) {
   out[2] = g_tctx.step;
   out[3] = g_tctx.dec;
 }
-// ints[7] = {kind, seek, it, step, dec, a, b}; dbls[2] = {margin, v}
+// ints[10] = {kind, seek, it, step, dec, a, b, forced, own_a, own_b};
+// dbls[5] = {margin, v, fmargin, lo, hi}
 void orc_trace_get(int i, int* ints, double* dbls) {
   const TraceEv& e = g_trace.at(i);
-  int v[7] = {e.kind, e.seek, e.it, e.step, e.dec, e.a, e.b};
-  for (int k = 0; k < 7; ++k) ints[k] = v[k];
-  dbls[0] = e.margin;
-  dbls[1] = e.v;
+  int v[10] = {e.kind, e.seek, e.it, e.step, e.dec, e.a, e.b, e.forced, e.own_a, e.own_b};
+  for (int k = 0; k < 10; ++k) ints[k] = v[k];
+  double d[5] = {e.margin, e.v, e.fmargin, e.lo, e.hi};
+  for (int k = 0; k < 5; ++k) dbls[k] = d[k];
+}
+// follow mode: the guide trace, 7 ints per event {kind, seek, it, step, dec,
+// a, b}; n = 0 turns following off. Takes effect for the next traced run.
+void orc_trace_follow(const int* ints, int n) {
+  g_follow.clear();
+  for (int i = 0; i < n; ++i) {
+    const int* e = ints + 7 * i;
+    TraceEv ev{e[0], e[1], e[2], e[3], e[4], e[5], e[6], 0.0, 0.0};
+    g_follow.push_back(ev);
+  }
+  g_follow_on = n > 0;
+  g_follow_break = -1;
+}
+// index of the event where following ended (-1: followed to the end)
+long orc_trace_follow_break() { return g_follow_break; }
+void orc_set_logits_tap(TapFn fn, void* user) {
+  g_tap = fn;
+  g_tap_user = user;
 }
 void orc_set_external(ExtEncodeFn enc, ExtLogitsFn lg, void* user) {
   g_ext_encode = enc;

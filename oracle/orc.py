@@ -25,6 +25,7 @@ ORC_MXFP8 = 2  # encoder / cross-K/V matmuls on MX-fp8 operands (engine MWX_COMP
 _lib = None
 EXT_ENC = C.CFUNCTYPE(None, C.c_void_p, C.c_int)
 EXT_LOGITS = C.CFUNCTYPE(None, C.c_void_p, C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_float))
+TAP_LOGITS = EXT_LOGITS  # (user, tokens, n, logits_last): the oracle's own decoded rows
 
 
 def build() -> None:
@@ -87,6 +88,9 @@ def lib() -> C.CDLL:
     L.orc_trace_count.restype = C.c_int
     L.orc_trace_get.argtypes = [C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_double)]
     L.orc_trace_ctx.argtypes = [C.POINTER(C.c_int)]
+    L.orc_trace_follow.argtypes = [C.POINTER(C.c_int), C.c_int]
+    L.orc_trace_follow_break.restype = C.c_long
+    L.orc_set_logits_tap.argtypes = [C.c_void_p, C.c_void_p]
     L.orc_prosody.restype = None
     L.orc_prosody.argtypes = [fp, C.c_int64, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, P]
     L.orc_resample.restype = C.c_long
@@ -177,9 +181,31 @@ class TraceEv:
     b: int
     margin: float
     v: float
+    forced: int = 0  # follow mode: the guide's outcome was taken over the oracle's own
+    own_a: int = 0  # the oracle's own outcome (forced events)
+    own_b: int = 0
+    fmargin: float = 0.0  # how far the oracle's arithmetic is from the taken outcome
+    lo: float = 0.0  # draws: the taken id's cumulative-probability interval [lo, hi)
+    hi: float = 0.0
 
     def key(self):
         return (self.kind, self.seek, self.it, self.step, self.dec, self.a, self.b)
+
+
+KIND_IDS = {v: k for k, v in TRACE_KINDS.items()}
+
+
+def _read_trace() -> List[TraceEv]:
+    L = lib()
+    evs = []
+    ints = (C.c_int * 10)()
+    dbl = (C.c_double * 5)()
+    for i in range(L.orc_trace_count()):
+        L.orc_trace_get(i, ints, dbl)
+        v = list(ints)
+        evs.append(TraceEv(TRACE_KINDS[v[0]], *v[1:7], dbl[0], dbl[1], v[7], v[8], v[9],
+                           dbl[2], dbl[3], dbl[4]))
+    return evs
 
 
 def trace_ctx():
@@ -321,15 +347,42 @@ class Oracle:
         L.orc_trace_enable(1)
         try:
             out = fn(*args, **kw)
-            evs = []
-            ints = (C.c_int * 7)()
-            dbl = (C.c_double * 2)()
-            for i in range(L.orc_trace_count()):
-                L.orc_trace_get(i, ints, dbl)
-                evs.append(TraceEv(TRACE_KINDS[ints[0]], *list(ints)[1:], dbl[0], dbl[1]))
-            return out, evs
+            return out, _read_trace()
         finally:
             L.orc_trace_enable(0)
+
+    def traced_follow(self, guide: List[TraceEv], pcm: np.ndarray, opt: FullOptions, tap=None):
+        """full() on the oracle's own logits in follow mode: at every traced
+        decision it takes the outcome `guide` recorded (events whose outcome
+        differs come back forced, with the oracle's own outcome and its
+        distance to the guide's). tap(tokens, logits_last) sees every row the
+        oracle decodes. Returns ((rc, segs, lang, windows), [TraceEv], break)
+        where break is the index at which the run stopped following (None:
+        followed to the end)."""
+        L = lib()
+        flat = (C.c_int * (7 * len(guide)))(*[x for e in guide for x in
+                                              (KIND_IDS[e.kind], e.seek, e.it, e.step, e.dec,
+                                               e.a, e.b)])
+        cb = None
+        if tap is not None:
+            V = self.n_vocab
+
+            def _tap(user, toks, n, lg):
+                tap([toks[i] for i in range(n)],
+                    np.ctypeslib.as_array(lg, shape=(V,)).copy())
+
+            cb = TAP_LOGITS(_tap)
+            L.orc_set_logits_tap(C.cast(cb, C.c_void_p), None)
+        L.orc_trace_follow(flat, len(guide))
+        L.orc_trace_enable(1)
+        try:
+            out = self.full(pcm, opt)
+            brk = L.orc_trace_follow_break()
+            return out, _read_trace(), (None if brk < 0 else int(brk))
+        finally:
+            L.orc_trace_enable(0)
+            L.orc_trace_follow(None, 0)
+            L.orc_set_logits_tap(None, None)
 
     def full_external(self, pcm: np.ndarray, opt: FullOptions, encode_fn, logits_fn):
         """full() with every decode answered by callbacks: encode_fn(seek) and

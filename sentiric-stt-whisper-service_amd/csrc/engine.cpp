@@ -216,6 +216,9 @@ struct State {
   // counters (mwx_test_decode_counters): decode steps launched, prompt
   // positions prefilled
   long n_steps = 0, n_prefill = 0;
+  // (mwx_test_window_counters): clip windows decoded, decode attempts run
+  // (one per window and temperature tried: attempts - windows = fallbacks)
+  long n_windows = 0, n_attempts = 0;
   // run-ahead attempts redone on the host loop (mwx_test_runahead_fallbacks)
   long n_ra_fallback = 0;
   DBuf lpflt, lpparts, lpres;  // logits-processing scratch

@@ -671,8 +671,10 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
 // KV8 (MWX_COMPUTE_MXFP8): the cross K/V cache holds MX-fp8 rows (64 e4m3
 // codes per (time, head) and two E8M0 scales, one per 32-element half), half
 // the bytes of the f16 cache. A lane's 8 codes lie in one half, so they are
-// widened to f16 with that half's scale (v_cvt_scalef32_pk_f16_fp8: exact,
-// the values are f16-representable) and every score / P.V operation then runs
+// widened to f16 with that half's scale (v_cvt_scalef32_pk_f16_fp8: exact
+// while code x scale is f16-representable — the cache's values are f16 values
+// MX-rounded, so they are; a block scale outside f16's range would saturate
+// or flush) and every score / P.V operation then runs
 // on f16 exactly as for the f16 cache. Each lane loads the scale pair of one
 // of its wave's 64 rows per batch; the pair a row needs is read from the lane
 // that loaded it (__shfl).
@@ -692,7 +694,8 @@ __device__ __forceinline__ f16x8 dequant_h8(uint2 raw, uint32_t e) {
 // v_dot2 chains. Scores: a 16-key tile is the A operand of two chained
 // v_mfma_f32_16x16x32_f16 (one per 32-element scale half; lane l holds key
 // l&15's 8 codes at e = 8(l>>4) .. +7 of that half, widened to f16 with that
-// key's half scale: exact, as in the v_dot2 path), the queries (f16, rows
+// key's half scale: exact while code x scale is f16-representable, as in the
+// v_dot2 path), the queries (f16, rows
 // >= NQ zero) the B operand; lane l receives query l&15's scores with keys
 // 4(l>>4) .. +3. P.V: the V tile staged in LDS as exactly widened f16, the
 // f16 P the A operand (below). A query's results depend only on its own row,
@@ -882,8 +885,8 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
   };
   // MFS: P.V on MFMA as well. Wave w stages its 32-key V tiles (w, w + 4, ...)
   // in LDS as f16, dequantized at staging: a lane's 32 codes are one half of
-  // one key row, so one E8M0 scale widens them exactly (the values are
-  // f16-representable, as in the v_dot2 path); the B operand (8 keys of one
+  // one key row, so one E8M0 scale widens them exactly while code x scale is
+  // f16-representable, as in the v_dot2 path; the B operand (8 keys of one
   // column) is two transposed 16-bit reads (ds_read_b64_tr_b16), and the A
   // operand the query's f16 P itself (no per-key scale arithmetic). The
   // 32-B column blocks of a row are XOR-swizzled by (row >> 1) & 3, so a
@@ -914,8 +917,9 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
       qb1[j] = mrow < NQ ? (_Float16)sq[min(mrow, NQ - 1)][32 + 8 * gq + j] : (_Float16)0.0f;
     }
     // each lane widens its A-operand key's codes with that key's two
-    // scales (one per 32-element half; exact in f16, as the v_dot2 path
-    // widens them), and the two halves chain in one accumulator
+    // scales (one per 32-element half; exact while code x scale is
+    // f16-representable, as the v_dot2 path widens them), and the two halves
+    // chain in one accumulator
     auto score_tile = [&](int buf, int i, int t) {
       f32x4 out;
       {

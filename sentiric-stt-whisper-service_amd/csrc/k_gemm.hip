@@ -877,6 +877,9 @@ __global__ __launch_bounds__(256) void gemm_dec_shared(int epi, const T* __restr
   static_assert(COMB == 0 || NG == 4, "split-K partials: four k-groups");
   using V8 = typename Elt<T>::v8;
   constexpr int KS = NG * KCH;  // k-steps of this workgroup's K range
+  // the whole A block in LDS: 80 KB for the DS(10, 4) case (d = 1280,
+  // 16-bit) fits gfx950's 160 KB of LDS per workgroup (not gfx942's 64 KB)
+  static_assert(MT * KS * 512 * sizeof(T) <= 160 * 1024, "gemm_dec_shared: A block exceeds gfx950 LDS");
   __shared__ __attribute__((aligned(16))) T ash[MT * KS * 512];
   const int L = blockIdx.x, Wd = 8 * nrb;
   const int rb = (L % Wd) / 8, g = (L / Wd) * 8 + L % 8;
@@ -1245,6 +1248,22 @@ static int gemm_group_m() {
   return g;
 }
 
+// the encoder GEMM's main-loop schedule: env MWX_GEMM_8PH read once, a test
+// switches it with gemm_8ph_set (mwx_test_set_gemm_8ph)
+static std::atomic<int>& gemm_8ph_mode() {
+  static std::atomic<int> m{-1};
+  return m;
+}
+static bool gemm_8ph() {
+  int v = gemm_8ph_mode().load();
+  if (v < 0) {
+    v = (getenv("MWX_GEMM_8PH") && atoi(getenv("MWX_GEMM_8PH")) == 1) ? 1 : 0;
+    gemm_8ph_mode().store(v);
+  }
+  return v != 0;
+}
+int gemm_8ph_set(int on) { return gemm_8ph_mode().exchange(on < 0 ? -1 : (on ? 1 : 0)); }
+
 template <typename T, int EPI, bool OUT16>
 static void gemm_dispatch(const T* A, long lda, long a_bstride, const T* W, long ldw, int M,
                           int N, int K, int batch, const EpiParams& P0, hipStream_t st) {
@@ -1256,12 +1275,10 @@ static void gemm_dispatch(const T* A, long lda, long a_bstride, const T* W, long
   // weights per row tile; with the grouped order both take the remap)
   P.group_m = gemm_group_m();
   P.xcd_remap = xcd_remap_enabled() && (EPI != EPI_CROSS_KV || P.group_m > 0);
-  // MWX_GEMM_8PH=1: the 8-phase schedule (bit-identical; measured no faster
-  // than the 2-stage ring on the large-v3 encoder shapes: one lane 0.3633 vs
-  // 0.3647 of the dense peak, same box, r05f). Read per launch so a test can
-  // compare the two in one process.
-  const char* e8 = getenv("MWX_GEMM_8PH");
-  if (e8 && atoi(e8) == 1)
+  // MWX_GEMM_8PH=1 (or gemm_8ph_set(1)): the 8-phase schedule (bit-identical;
+  // measured no faster than the 2-stage ring on the large-v3 encoder shapes:
+  // one lane 0.3633 vs 0.3647 of the dense peak, same box, r05f)
+  if (gemm_8ph())
     gemm_big<T, EPI, OUT16, false, true><<<g, 512, 0, st>>>(A, lda, a_bstride, W, ldw, M, N, K, P);
   else
     gemm_big<T, EPI, OUT16><<<g, 512, 0, st>>>(A, lda, a_bstride, W, ldw, M, N, K, P);

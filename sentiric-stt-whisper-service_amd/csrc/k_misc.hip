@@ -134,7 +134,11 @@ __global__ __launch_bounds__(256) void ln_dec_kernel(float* __restrict__ x,
   float* xr = x + (long)row * N + i0;
   f32x4 xa, xc;
   if (emb.te) {
-    // x = te[tok] + pe[pos] (ggml_get_rows(d_te) + ggml_get_rows(d_pe)), the ids first
+    // x = te[tok] + pe[pos] (ggml_get_rows(d_te) + ggml_get_rows(d_pe)), the ids first.
+    // The clamp keeps inactive rows' stale ids / positions in bounds (they
+    // are requested before the activity flag); active rows' ids are in range
+    // by construction (sampled ids, host-validated prompts: driver.inc
+    // tokens_valid) and positions < n_text_ctx (the token loop's cap)
     const int tk = min(max(emb.tok[row], 0), emb.n_tok - 1);
     const int ps = min(max(emb.pos[row], 0), emb.n_pos - 1);
     const typename Elt<T>::v8 er =

@@ -233,6 +233,8 @@ int xattn_mfs_set(int on);
 // decode GEMMs at M > 64 rows: shared-A kernels (1) or per-strip grids (0);
 // -1 restores the MWX_DEC_SHARED default. Returns the previous setting.
 int dec_shared_set(int on);
+// the encoder GEMM's 8-phase main loop on / off (-1: back to MWX_GEMM_8PH)
+int gemm_8ph_set(int on);
 template <typename T>
 bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float* bias,
                                  const void* kbase, const void* vbase, const int* kv_index,

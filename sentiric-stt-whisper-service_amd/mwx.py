@@ -213,12 +213,18 @@ def lib() -> C.CDLL:
     L.mwx_test_dequantize.argtypes = [C.c_int, C.c_void_p, C.c_long, C.POINTER(C.c_float)]
     L.mwx_test_decode_counters.restype = C.c_int
     L.mwx_test_decode_counters.argtypes = [P, C.POINTER(C.c_long), C.POINTER(C.c_long), C.c_int]
+    L.mwx_test_window_counters.restype = C.c_int
+    L.mwx_test_window_counters.argtypes = [P, C.POINTER(C.c_long), C.POINTER(C.c_long), C.c_int]
     L.mwx_test_runahead_fallbacks.restype = C.c_long
     L.mwx_test_runahead_fallbacks.argtypes = [P, C.c_int]
     L.mwx_test_set_xattn_mfs.restype = C.c_int
     L.mwx_test_set_xattn_mfs.argtypes = [C.c_int]
     L.mwx_test_set_dec_shared.restype = C.c_int
     L.mwx_test_set_dec_shared.argtypes = [C.c_int]
+    L.mwx_test_set_gemm_8ph.restype = C.c_int
+    L.mwx_test_set_gemm_8ph.argtypes = [C.c_int]
+    L.mwx_test_set_ra_mismatch.restype = C.c_long
+    L.mwx_test_set_ra_mismatch.argtypes = [C.c_long]
     u8p = C.POINTER(C.c_uint8)
     L.mwx_test_xattn_mx.restype = C.c_int
     L.mwx_test_xattn_mx.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, fpp, u8p, u8p,
@@ -283,6 +289,18 @@ def set_dec_shared(on: Optional[bool]) -> int:
     shared-A kernels (True) or the per-strip grids (False); None: the
     MWX_DEC_SHARED default."""
     return lib().mwx_test_set_dec_shared(-1 if on is None else int(bool(on)))
+
+
+def set_gemm_8ph(on: Optional[bool]) -> int:
+    """mwx_test_set_gemm_8ph: the encoder GEMM's 8-phase main loop (True) or
+    the 2-stage ring (False); None: the MWX_GEMM_8PH default."""
+    return lib().mwx_test_set_gemm_8ph(-1 if on is None else int(bool(on)))
+
+
+def set_ra_mismatch(step: Optional[int]) -> int:
+    """mwx_test_set_ra_mismatch: treat run-ahead step `step` of later attempts
+    as a device/host disagreement (None: back to MWX_TEST_RA_MISMATCH, -1: off)."""
+    return lib().mwx_test_set_ra_mismatch(-2 if step is None else int(step))
 
 
 def dequantize(qtype: int, raw: bytes, n: int) -> np.ndarray:
@@ -615,6 +633,14 @@ class Context:
         lib().mwx_test_decode_counters(self.state(state_index), C.byref(st), C.byref(pf),
                                        1 if reset else 0)
         return st.value, pf.value
+
+    def window_counters(self, state_index: int = 0, reset: bool = True):
+        """(clip windows decoded, decode attempts run) on a state since the last
+        reset (mwx_test_window_counters); attempts - windows = fallbacks."""
+        w, a = C.c_long(), C.c_long()
+        lib().mwx_test_window_counters(self.state(state_index), C.byref(w), C.byref(a),
+                                       1 if reset else 0)
+        return w.value, a.value
 
     def runahead_fallbacks(self, state_index: int = 0, reset: bool = True) -> int:
         """Run-ahead attempts redone on the host loop (mwx_test_runahead_fallbacks)."""

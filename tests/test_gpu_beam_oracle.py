@@ -1,37 +1,29 @@
 """Beam search — the service's default decode mode (beam_size 5:
 /root/reference/src/config.h:52, src/stt_engine.cpp:204-212,235-236) — against
-the oracle's OWN arithmetic, not only against the oracle's loop replayed on the
-device's logits.
+the oracle's OWN arithmetic over the whole run, not only against the oracle's
+loop replayed on the device's logits.
 
 The two sides compute the logits with different rounding (f16/bf16 GPU GEMMs
 and attention vs the oracle's f32 loops), so their decisions can differ where
 the reference arithmetic itself is within that noise of a tie. Every
-float-sensitive decision of whisper_full_with_state is recorded on both sides
-by the oracle's decision trace (mwx_oracle.cpp TraceKind): the oracle on its
-own logits (A), and the oracle's loop on the device's logits (B, which the
-device's own run equals exactly — asserted). A and B must agree up to their
-first differing decision, and at that decision the oracle's margin must lie
-within what the measured logits error can move (bounds per decision kind in
-`noise_bound`). A differing rule would show as a structural event (a decoder's
-completed/failed state, an exact tie) or a decision taken by a margin far
-outside the noise; neither is allowed.
-
-Bounds, with eps = max |device - oracle| over the raw logits of the prefixes
-of the diverging window: a log-prob moves by at most 2 eps (logit + log-sum-
-exp), so
-  draw      cumulative-probability boundary: <= 2 eps
-  argmax    top-1 - top-2 log-prob:          <= 4 eps
-  ts_mass   log sum p(ts) - max text lp:     <= 4 eps
-  assign    difference of two sums of n = step + 1 log-probs: <= 4 eps n
-  best      difference of two length-normalised scores:       <= 4 eps
-  fallback / no_speech: avg log-prob or p(no speech) vs its threshold: <= 2 eps
-and the test allows 2x each (as test_gpu_fulldepth.py allows 2 x err).
+float-sensitive decision of whisper_full_with_state is recorded by the oracle's
+decision trace (mwx_oracle.cpp TraceKind). B is the oracle's loop on the
+device's logits (the device's own run equals it exactly — asserted). The oracle
+then runs on its own logits in follow mode: at every decision it takes B's
+outcome, and where its own arithmetic decided otherwise the event is a forced
+flip whose distance (the oracle's distance to B's outcome; for draws the
+movement of the cumulative-probability boundary across the shared uniform) must
+lie within what the logits error measured on that window's rows can move
+(tests/beam_follow.py). So every decision of every window is compared, not only
+those before the first near-tie; a differing rule would show as a structural
+difference (decoder status, exact tie, a candidate missing) or a flip far
+outside the noise, and fails.
 """
-import numpy as np
 import pytest
 
 import mwx
 import orc
+from beam_follow import follow_compare
 from test_gpu_parity import assert_same, beam_opt, beam_params, pcm_clip, run_fresh
 
 pytestmark = pytest.mark.gpu
@@ -41,23 +33,17 @@ pytestmark = pytest.mark.gpu
 # activations as test_decoder_logits_parity's 2e-2 on plain micro weights, but
 # micro-rich's lifted final-LN bias makes its logits larger (0.017-0.023
 # measured over a window's beam prefixes)
-LOGITS_TOL = {"micro-rich": 5e-2, "large-v3": 0.25}
-
-
-def noise_bound(ev: orc.TraceEv, eps: float) -> float:
-    per = {"draw": 2 * eps, "argmax": 4 * eps, "ts_mass": 4 * eps,
-           "assign": 4 * eps * (ev.step + 1), "best": 4 * eps, "fallback": 2 * eps,
-           "no_speech": 2 * eps}
-    return 2 * per.get(ev.kind, 0.0)  # structural kinds (status, exact_tie): 0
+LOGITS_TOL = {"micro-rich": 5e-2, "large-v3": 0.25, "large-v3-mx": 2.0}
+FULL_DEPTH_STEPS = 64
 
 
 def replay_traced(ctx, o, pcm, opt):
     """The oracle's loop on the device's logits (every prefix decoded by the
-    device), with the decision trace and the (seek, prefix, logits) log."""
+    device): its segments, decision trace and {(seek, prefix): logits} rows."""
     idx = len(ctx.states)
     ctx.state(idx)
     cur = {"seek": 0}
-    log = []
+    rows = {}
 
     def enc(seek):
         cur["seek"] = seek
@@ -65,114 +51,27 @@ def replay_traced(ctx, o, pcm, opt):
 
     def logits(tokens):
         lg = ctx.test_decode_last(tokens, state_index=idx).copy()
-        log.append((cur["seek"], list(tokens), lg, orc.trace_ctx()))
+        rows[(cur["seek"], tuple(tokens))] = lg
         return lg
 
     (_, segs, _, _), tr = o.traced(o.full_external, pcm, opt, enc, logits)
-    return segs, tr, log
+    return segs, tr, rows
 
 
-def logits_error(o, pcm, log, seek, step, cap):
-    """max |device - oracle| over the raw logits of the prefixes the window
-    decoded up to the diverging step (prompt + step tokens). The oracle
-    decodes each hypothesis once on its own encoder output at that seek and
-    every logged prefix of it is read off that pass; with more than `cap`
-    hypotheses, the longest `cap` are measured (the oracle pays ~0.1 s per
-    position at large-v3 depth)."""
-    ent = [(toks, lg) for s, toks, lg, _ in log if s == seek]
-    max_len = len(ent[0][0]) + step
-    ent = [e for e in ent if len(e[0]) <= max_len]
-    leaves = []
-    for toks, _ in sorted(ent, key=lambda e: -len(e[0])):
-        if not any(lf[:len(toks)] == toks for lf in leaves):
-            leaves.append(toks)
-    leaves = leaves[:cap]
-    mel, _ = o.mel(pcm)
-    k, v = o.cross(o.encode(mel, seek=seek))
-    err = 0.0
-    for lf in leaves:
-        ref = o.decode_seq(k, v, lf)
-        for toks, lg in ent:
-            if lf[:len(toks)] == toks:
-                err = max(err, float(np.abs(lg - ref[len(toks) - 1]).max()))
-    return err
-
-
-def explain_draw(o, pcm, log, ev, opt):
-    """For a draw both runs took with the same uniform u but a different id:
-    the cumulative-probability boundary between the two ids under the
-    oracle's own probabilities and under the device's, for the decoder's
-    exact prefix (the logits the replay asked for at step - 1). The flip is a
-    tie exactly when u lies between the two boundaries. (First temperature
-    only, where the rules run at t = 0.)"""
-    if ev.it != 0:
-        return None
-    want = (ev.seek, ev.it, ev.step - 1, ev.dec if ev.step > 0 else 0)
-    prompt = next(t for s, t, _, c in log if c[:3] == (ev.seek, ev.it, -1))
-    toks, lg_dev = next((t, lg) for s, t, lg, c in log if c == want)
-    hist = toks[len(prompt):]
-    has_ts, seek_delta = False, 3000
-    for t in hist:
-        if t > o.beg:
-            has_ts, seek_delta = True, 2 * (t - o.beg)
-    mel, _ = o.mel(pcm)
-    k, v = o.cross(o.encode(mel, seek=ev.seek))
-    lg_orc = o.decode_seq(k, v, toks)[-1]
-    cums = []
-    for lg in (lg_orc, lg_dev):
-        _, _, pr, _ = o.process_logits(lg, hist, has_ts, seek_delta,
-                                       suppress_nst=opt.suppress_nst,
-                                       bench_fixed_steps=opt.bench_fixed_steps)
-        pr = pr.astype(np.float64)
-        cums.append(np.cumsum(pr / pr.sum()))
-    return cums
-
-
-def compare(ctx, o, pcm, p, opt, model, cap=10**6):
+def compare(ctx, o, pcm, p, opt, model):
+    """Device run == the oracle's loop on the device's logits (B), then the
+    oracle on its own logits follows B decision for decision over the whole
+    run (tests/beam_follow.py): every decision agrees or is a forced near-tie
+    flip within the noise bound of the logits error measured on exactly that
+    window's rows, and the followed run ends on the device's tokens."""
     segs = run_fresh(ctx, pcm, p)
-    rsegs, tb, log = replay_traced(ctx, o, pcm, opt)
+    rsegs, tb, rows = replay_traced(ctx, o, pcm, opt)
     assert_same(segs, rsegs, p_tol=1e-4)  # device loop == oracle loop on the device's logits
-    (_, osegs, _, _), ta = o.traced(o.full, pcm, opt)
-    assert not [e for e in ta + tb if e.kind == "exact_tie"]  # D5 never decides here
+    r = follow_compare(o, pcm, opt, tb, rows)
     ids = [t.id for s in segs for t in s.tokens]
-    oids = [t.id for s in osegs for t in s.tokens]
-    i = orc.first_divergence(ta, tb)
-    if i is None:
-        assert ids == oids
-        return {"events": len(ta), "first": None, "tokens": (len(ids), len(oids))}
-    ea, eb = ta[i], tb[i] if i < len(tb) else None
-    eps = logits_error(o, pcm, log, ea.seek, max(ea.step, 0), cap)
-    bound = noise_bound(ea, eps)
-    info = {"events": len(ta), "first": i, "tokens": (len(ids), len(oids)), "oracle": ea,
-            "device": eb, "eps": eps, "bound": bound}
-    assert eb is not None and ea.kind == eb.kind, info  # same decision, different outcome
-    assert eps < LOGITS_TOL[model], info
-    assert ea.margin <= bound, info
-    if ea.kind == "draw":
-        cums = explain_draw(o, pcm, log, ea, opt)
-        if cums is not None:
-            # both sides' ids rebuilt from the two probability vectors and u
-            ca, cb = cums
-            u = ea.v
-            assert int(np.searchsorted(ca, u, side="left")) == ea.b, info
-            assert int(np.searchsorted(cb, u, side="left")) == eb.b, info
-            j = min(ea.b, eb.b)  # the boundary between the two ids moved across u
-            info["boundary"] = (float(ca[j]), float(cb[j]))
-            assert min(ca[j], cb[j]) <= u <= max(ca[j], cb[j]), info
-    return info
-
-
-def fmt(k, r):
-    if r["first"] is None:
-        return f"clip {k}: {r['events']} decisions, token-identical ({r['tokens'][0]} tokens)"
-    a, b = r["oracle"], r["device"]
-    return (f"clip {k}: {r['tokens'][0]} / {r['tokens'][1]} tokens; first differing decision "
-            f"#{r['first']} of {r['events']}: {a.kind} at seek {a.seek} step {a.step} decoder "
-            f"{a.dec}: oracle ({a.a}, {a.b}) vs device ({b.a}, {b.b}); oracle margin "
-            f"{a.margin:.3g} (v {a.v:.6g} / {b.v:.6g}); logits err {r['eps']:.3g}, "
-            f"bound {r['bound']:.3g}"
-            + (f"; u {a.v:.7f} between the boundaries {r['boundary'][0]:.7f} (oracle) / "
-               f"{r['boundary'][1]:.7f} (device)" if "boundary" in r else ""))
+    assert r.tokens == ids
+    assert r.eps_max < LOGITS_TOL[model], r.eps_max
+    return r
 
 
 @pytest.fixture(scope="module")
@@ -187,31 +86,44 @@ def rich(make_model):
 def test_beam5_vs_oracle_arithmetic(rich, temperature_inc):
     """Beam 5 at the service's parameters on 4 clips (14-26 s: window seeks,
     segment splits, EOT): device == the oracle's loop on the device's logits,
-    and that run agrees with the oracle on its own logits up to a decision the
-    oracle takes within the logits noise (printed per clip)."""
+    and the oracle's own arithmetic agrees with it at every decision of every
+    window, up to forced near-tie flips within the logits noise (printed per
+    clip: decisions checked, forced flips, the largest flip distance)."""
     ctx, o = rich
-    same = 0
     for k in range(4):
         pcm = pcm_clip(50 + k, 14.0 + 4 * k)
         r = compare(ctx, o, pcm, beam_params(ctx, temperature_inc), beam_opt(temperature_inc),
                     "micro-rich")
-        same += r["first"] is None
-        print(fmt(k, r))
-    print(f"beam 5 vs oracle arithmetic (temperature_inc {temperature_inc}): {same} of 4 clips "
-          f"identical decision for decision")
+        print(r.summary(f"clip {k} (temperature_inc {temperature_inc})"))
+
+
+def full_depth(path, compute, model, steps=FULL_DEPTH_STEPS, mxfp8=False):
+    o = orc.Oracle(path, mxfp8=mxfp8)
+    with mwx.Context.open(path, compute=compute) as ctx:
+        p = beam_params(ctx, 0.0)
+        p.bench_fixed_steps = steps
+        opt = beam_opt(0.0)
+        opt.bench_fixed_steps = steps
+        r = compare(ctx, o, pcm_clip(0), p, opt, model)
+    o.close()
+    return r
 
 
 def test_full_depth_large_v3_beam5_vs_oracle_arithmetic(make_model):
     """The benched model (large-v3, 32 + 32 layers, bf16) in the service's
     default decode mode, beam 5, on the bench workload's rules
-    (bench_fixed_steps: every step a text token; 32 steps to bound the
-    oracle's CPU time): as above."""
+    (bench_fixed_steps: every step a text token; 64 steps to bound the
+    oracle's CPU time): every decision of the window as above."""
     path = make_model("large-v3", mwx.GGML_BF16)
-    o = orc.Oracle(path)
-    with mwx.Context.open(path) as ctx:
-        p = beam_params(ctx, 0.0)
-        p.bench_fixed_steps = 32
-        opt = beam_opt(0.0)
-        opt.bench_fixed_steps = 32
-        r = compare(ctx, o, pcm_clip(0), p, opt, "large-v3", cap=12)
-        print(fmt(0, r))
+    r = full_depth(path, mwx.COMPUTE_MODEL, "large-v3")
+    print(r.summary(f"large-v3 bf16 beam 5, {FULL_DEPTH_STEPS} steps"))
+
+
+def test_full_depth_mxfp8_beam5_vs_mx_oracle_arithmetic(make_model):
+    """C5's own decode mode (BASELINE.json configs[4]): the full-depth model in
+    the MX-fp8 compute mode, beam 5, against the MX oracle's arithmetic
+    decision for decision (the MX oracle: the same e4m3 / E8M0 rounding
+    points, f32 elsewhere)."""
+    path = make_model("large-v3", mwx.GGML_BF16)
+    r = full_depth(path, mwx.COMPUTE_MXFP8, "large-v3-mx", mxfp8=True)
+    print(r.summary(f"large-v3 MX-fp8 beam 5, {FULL_DEPTH_STEPS} steps"))

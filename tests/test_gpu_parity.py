@@ -819,7 +819,7 @@ def test_beam_runahead_equals_host_loop(rich, temperature_inc, monkeypatch):
 @pytest.mark.parametrize("beam,fault_step", [(5, 0), (5, 3), (1, 2)])
 def test_runahead_mismatch_falls_back_to_host_loop(rich, beam, fault_step, monkeypatch):
     """A disagreement between the device's run-ahead advance and the host's
-    replay (forced at run-ahead step `fault_step` by MWX_TEST_RA_MISMATCH)
+    replay (forced at run-ahead step `fault_step` by mwx_test_set_ra_mismatch)
     does not fail the request: the attempt is redone on the host-driven loop
     and the batch's token records equal a run on the host loop throughout
     (beam 5, the service default, and greedy)."""
@@ -838,8 +838,11 @@ def test_runahead_mismatch_falls_back_to_host_loop(rich, beam, fault_step, monke
     monkeypatch.setenv("MWX_NO_RUNAHEAD", "1")
     host, n0 = run()
     monkeypatch.delenv("MWX_NO_RUNAHEAD")
-    monkeypatch.setenv("MWX_TEST_RA_MISMATCH", str(fault_step))
-    redone, n1 = run()
+    mwx.set_ra_mismatch(fault_step)
+    try:
+        redone, n1 = run()
+    finally:
+        mwx.set_ra_mismatch(-1)
     print(f"beam {beam}, fault at step {fault_step}: {n1} attempt(s) redone on the host loop, "
           f"{sum(len(x) for x in host)} tokens")
     assert n0 == 0 and n1 >= 1
@@ -929,10 +932,57 @@ def test_mx_cross_attention_kernel_vs_f64(micro, sharp):
 
 
 
+def test_mx_cross_attention_kernel_extreme_scales(micro):
+    """Block scales at the edge of f16's range: V rows whose
+    code x scale values fall into f16's subnormal range (scales 2^-30 ..
+    2^-22). Both kernel paths widen the codes to f16 before the arithmetic,
+    so the pinned behaviour is attention over the f16-ROUNDED dequantized
+    values (subnormals kept, not flushed): within 3e-3 of max |o| per row of
+    float64 attention over np.float16(values), for the MFMA and the v_dot2
+    path alike; the distance to the unrounded values is printed."""
+    ctx, _, _ = micro
+    rng = np.random.default_rng(11)
+    H, n, nq, G = 2, 1500, 5, 2
+    R = G * nq
+    k = rng.standard_normal((G, H, n, 64)) * 0.35 * np.exp2(rng.uniform(-5, 3, size=(G, H, n, 1)))
+    v = rng.standard_normal((G, H, n, 64)) * np.exp2(rng.uniform(-22, -14, size=(G, H, n, 1)))
+    k8, ks, kd = _mx_rows(k)
+    v8, vs, vd = _mx_rows(v)
+    vd16 = vd.astype(np.float16).astype(np.float64)
+    assert (np.abs(vd) < 2.0 ** -14).mean() > 0.5  # mostly f16 subnormals
+    q = (rng.standard_normal((R, H * 64)) * 0.5).astype(np.float32)
+    qh = q.astype(np.float16).astype(np.float64)
+    scale = 64.0 ** -0.25
+    ref, ref_exact = np.empty((R, H * 64)), np.empty((R, H * 64))
+    for r in range(R):
+        g = r // nq
+        for h in range(H):
+            sc = kd[g, h] @ qh[r, h * 64:(h + 1) * 64] * scale
+            p = np.exp(sc - sc.max())
+            p /= p.sum()
+            ref[r, h * 64:(h + 1) * 64] = p @ vd16[g, h]
+            ref_exact[r, h * 64:(h + 1) * 64] = p @ vd[g, h]
+    errs, exact = {}, {}
+    prev = mwx.set_xattn_mfs(True)
+    try:
+        for mfs in (True, False):
+            mwx.set_xattn_mfs(mfs)
+            o = ctx.test_xattn_mx(q, k8, ks, v8, vs, nq)
+            scale_r = np.abs(ref).max(axis=1, keepdims=True)
+            errs[mfs] = float((np.abs(o - ref) / scale_r).max())
+            exact[mfs] = float((np.abs(o - ref_exact) / scale_r).max())
+    finally:
+        mwx.set_xattn_mfs(None if prev < 0 else bool(prev))
+    print(f"MX cross-attention, V in f16's subnormal range: vs f16-rounded values MFMA "
+          f"{errs[True]:.2e} / v_dot2 {errs[False]:.2e}; vs unrounded MFMA {exact[True]:.2e} / "
+          f"v_dot2 {exact[False]:.2e} (of max |o| per row)")
+    assert errs[True] <= 3e-3 and errs[False] <= 3e-3, (errs, exact)
+
+
 @pytest.mark.parametrize("M,N,K", [(300, 512, 64), (300, 512, 128), (513, 256, 192),
                                    (256, 768, 1280), (1500, 1280, 5120)])
-def test_gemm_8phase_equals_2stage(micro, M, N, K, monkeypatch):
-    """The encoder GEMM's 8-phase main loop (MWX_GEMM_8PH=1) against the
+def test_gemm_8phase_equals_2stage(micro, M, N, K):
+    """The encoder GEMM's 8-phase main loop (mwx_test_set_gemm_8ph) against the
     2-stage loop (the default) on the same operands: bit-identical outputs
     (every output fragment accumulates its K in the same order), for f16 and
     bf16, K of 1 / 2 / 3 / 20 / 80 tiles (the prologue and the drained tail of
@@ -943,24 +993,30 @@ def test_gemm_8phase_equals_2stage(micro, M, N, K, monkeypatch):
     w = (rng.standard_normal((N, K)) / np.sqrt(K)).astype(np.float32)
     bias = rng.uniform(-2, 2, N).astype(np.float32)
     for bf16 in (False, True):
-        monkeypatch.delenv("MWX_GEMM_8PH", raising=False)
-        ref = ctx.test_gemm_gelu(a, w, bias, bf16, True)
-        monkeypatch.setenv("MWX_GEMM_8PH", "1")
-        out = ctx.test_gemm_gelu(a, w, bias, bf16, True)
+        try:
+            mwx.set_gemm_8ph(False)
+            ref = ctx.test_gemm_gelu(a, w, bias, bf16, True)
+            mwx.set_gemm_8ph(True)
+            out = ctx.test_gemm_gelu(a, w, bias, bf16, True)
+        finally:
+            mwx.set_gemm_8ph(None)
         assert np.array_equal(ref.view(np.uint32), out.view(np.uint32)), (bf16, np.abs(ref - out).max())
 
 
 @pytest.mark.parametrize("arch,wt", [("micro", mwx.GGML_F16), ("large-v3-l2", mwx.GGML_BF16),
                                      ("base", mwx.GGML_F16)])
-def test_encoder_8phase_gemm_bit_identical(make_model, arch, wt, monkeypatch):
+def test_encoder_8phase_gemm_bit_identical(make_model, arch, wt):
     """Whole encoder (conv stem, every layer's QKV / out / FFN GEMMs with their
     epilogues) and the all-layer cross-K/V GEMM: 8-phase == 2-stage, bit for bit."""
     path = make_model(arch, wt)
     pcm = pcm_clip(4, 30.0)
     with mwx.Context.open(path) as ctx:
-        monkeypatch.delenv("MWX_GEMM_8PH", raising=False)
-        e0, k0, v0 = ctx.test_encode(pcm, state_index=0)
-        monkeypatch.setenv("MWX_GEMM_8PH", "1")
-        e1, k1, v1 = ctx.test_encode(pcm, state_index=1)
+        try:
+            mwx.set_gemm_8ph(False)
+            e0, k0, v0 = ctx.test_encode(pcm, state_index=0)
+            mwx.set_gemm_8ph(True)
+            e1, k1, v1 = ctx.test_encode(pcm, state_index=1)
+        finally:
+            mwx.set_gemm_8ph(None)
     for x, y in ((e0, e1), (k0, k1), (v0, v1)):
         assert np.array_equal(x.view(np.uint32), y.view(np.uint32)), float(np.abs(x - y).max())

@@ -91,3 +91,68 @@ def test_first_divergence():
     assert orc.first_divergence(a, [ev("draw", 1), ev("draw", 5), ev("assign", 3)]) == 1
     assert orc.first_divergence(a, a[:2]) == 2
     assert np.isfinite(a[0].margin)
+
+
+def perturbed_guide(o, pcm, opt, amp):
+    """The oracle's loop replayed on its own logits plus seeded noise of
+    amplitude `amp` per prefix (a stand-in for the device's rounding): its
+    trace and the rows it decoded."""
+    mel, _ = o.mel(pcm)
+    cur = {}
+    rows = {}
+
+    def enc(seek):
+        cur["seek"] = seek
+        cur["kv"] = o.cross(o.encode(mel, seek=seek))
+
+    def logits(toks):
+        lg = o.decode_seq(*cur["kv"], toks)[-1]
+        rng = np.random.default_rng(abs(hash((cur["seek"],) + tuple(toks))) % 2 ** 32)
+        lg = lg + rng.uniform(-amp, amp, lg.shape).astype(np.float32)
+        rows[(cur["seek"], tuple(toks))] = lg
+        return lg
+
+    (_, segs, _, _), tb = o.traced(o.full_external, pcm, opt, enc, logits)
+    return segs, tb, rows
+
+
+@pytest.mark.parametrize("temperature_inc", [0.0, 0.2])
+def test_follow_mode_checks_every_decision(rich, temperature_inc):
+    """Follow mode (the whole-window beam comparison of
+    test_gpu_beam_oracle.py) on CPU: the guide is the oracle's loop on its own
+    logits perturbed by seeded noise, so near-tie draws flip as they do on the
+    device. The oracle on its own logits, following the guide, takes every
+    decision the guide took (forced where its own arithmetic differs, each
+    within the bound of the measured noise) and ends on the guide's tokens."""
+    from beam_follow import follow_compare
+
+    o = rich
+    opt = beam_opt()
+    opt.temperature_inc = temperature_inc
+    n_forced = 0
+    for k in range(2):
+        pcm = mwx.pcm16_to_f32(mwx.synth_pcm16(50 + k, (10 + 4 * k) * 16000))
+        gsegs, tb, rows = perturbed_guide(o, pcm, opt, 0.03)
+        r = follow_compare(o, pcm, opt, tb, rows)
+        assert r.tokens == [t.id for s in gsegs for t in s.tokens]
+        assert 0.0 < r.eps_max <= 0.03 + 1e-6
+        n_forced += len(r.forced)
+        print(r.summary(f"clip {k}"))
+    assert n_forced > 0  # the noise did flip near-tie decisions, and they were followed
+
+
+def test_follow_mode_stops_at_a_structural_difference(rich):
+    """A guide whose decoder status differs from the oracle's (a changed rule,
+    not a near-tie) is not followed past that event."""
+    o = rich
+    pcm = mwx.pcm16_to_f32(mwx.synth_pcm16(50, 6 * 16000))
+    _, tr = o.traced(o.full, pcm, beam_opt())
+    i = next(i for i, e in enumerate(tr) if e.kind == "status")
+    bad = list(tr)
+    e = bad[i]
+    bad[i] = orc.TraceEv(e.kind, e.seek, e.it, e.step, e.dec, e.a ^ 2, e.b, e.margin, e.v)
+    _, _, brk = o.traced_follow(bad, pcm, beam_opt())
+    assert brk == i
+    _, tr2, brk2 = o.traced_follow(tr, pcm, beam_opt())  # its own trace: followed to the end
+    assert brk2 is None and not [x for x in tr2 if x.forced]
+    assert [x.key() for x in tr2] == [x.key() for x in tr]
