@@ -591,6 +591,11 @@ def main():
     ap.add_argument("--prompt-leg", action="store_true",
                     help="long-form leg with real previous-window text in every prompt: "
                          "--rich --decode-steps 0 --clip-seconds 600")
+    ap.add_argument("--service-defaults", action="store_true",
+                    help="what a default request of the service costs (src/config.h:47,52, "
+                         "src/stt_engine.cpp:204-243): language auto (window-0 detect), beam 5, "
+                         "the temperature-fallback ladder (temperature_inc 0.2), token "
+                         "timestamps, '-rich' weights decoded to the model's stop")
     ap.add_argument("--beam", type=int, default=0,
                     help="beam size (0: greedy; the service default is 5)")
     ap.add_argument("--clip-seconds", type=float, default=30.0,
@@ -623,6 +628,9 @@ def main():
     args = ap.parse_args()
     if args.prompt_leg:
         args.rich, args.decode_steps, args.clip_seconds = True, 0, 600.0
+    if args.service_defaults:
+        args.rich, args.decode_steps = True, 0
+        args.beam = args.beam or 5
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return launch_ranks(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -662,9 +670,9 @@ def main():
     p = ctx.default_params(mwx.SAMPLING_BEAM_SEARCH if args.beam > 1 else mwx.SAMPLING_GREEDY)
     if args.beam > 1:
         p.beam_search.beam_size = args.beam
-    p.language = b"en"
+    p.language = b"auto" if args.service_defaults else b"en"
     p.temperature = 0.0
-    p.temperature_inc = 0.0
+    p.temperature_inc = 0.2 if args.service_defaults else 0.0
     p.token_timestamps = not args.no_token_timestamps  # on, as the service sets it (src/stt_engine.cpp:225)
     p.suppress_nst = True
     p.bench_fixed_steps = args.decode_steps
@@ -743,6 +751,8 @@ def main():
         L.mwx_perf_enable(so, ",".join(classes).encode())
     for lane in range(lanes):
         ctx.decode_counters(lane * args.clips, reset=True)
+        ctx.window_counters(lane * args.clips, reset=True)
+        ctx.runahead_fallbacks(lane * args.clips, reset=True)
     del tok_count[:]
     barrier()
     torch.cuda.synchronize()
@@ -769,14 +779,25 @@ def main():
     timed = read_timed(owners)
     # decode work of the timed batches: steps launched (one per token position
     # of the longest row), prompt positions run by the batched prefill, tokens
-    dsteps = dpre = 0
+    # windows decoded and decode attempts (a temperature-fallback re-run is
+    # an attempt beyond the window's first), run-ahead attempts redone on the
+    # host loop (0 unless device and host disagree)
+    dsteps = dpre = nwin = natt = nra = 0
     for lane in range(lanes):
         a, b = ctx.decode_counters(lane * args.clips, reset=True)
-        dsteps, dpre = dsteps + a, dpre + b
+        w, at = ctx.window_counters(lane * args.clips, reset=True)
+        dsteps, dpre, nwin, natt = dsteps + a, dpre + b, nwin + w, natt + at
+        nra += ctx.runahead_fallbacks(lane * args.clips, reset=True)
+    n_batches = args.steps
+    win_per_clip = nwin / n_batches / args.clips
     decode_work = {"decode_steps_per_batch": round(dsteps / args.steps, 1),
                    "prefill_positions_per_batch": round(dpre / args.steps, 1),
                    "tokens_per_clip": round(sum(tok_count) / args.steps / args.clips, 1),
-                   "windows_per_clip": n_windows if args.decode_steps else None}
+                   "windows_per_clip": round(win_per_clip, 3),
+                   "fallback_reruns_per_clip": round((natt - nwin) / n_batches / args.clips, 3),
+                   "runahead_host_redos": nra}
+    if not args.decode_steps:
+        n_windows = win_per_clip  # (encoder work: every decoded window is encoded)
     timed_1lane, steps_1lane, elapsed_1lane = None, 0, None
     if lanes > 1 and not args.no_one_lane:
         # after the timed region (not part of `value`): the same batches on one
@@ -910,7 +931,8 @@ def main():
                 "workload": (f"whisper-{args.arch}{' (-rich weights)' if args.rich else ''} "
                              f"{'MX-fp8 compute (from the ' + args.wtype + ' file)' if args.fp8 else args.wtype}"
                              f": batches of {args.clips} x "
-                             f"{args.clip_seconds:g} s clips per GPU ({lanes} in flight), mel + "
+                             f"{args.clip_seconds:g} s clips per GPU ({lanes} in flight), "
+                             f"{'service defaults (language auto: window-0 detect; temperature ladder 0.0/0.2/../1.0), ' if args.service_defaults else ''}mel + "
                              f"encoder + cross-KV + {args.decode_steps or 'until-EOT'} "
                              f"{'beam-%d' % args.beam if args.beam > 1 else 'greedy'} KV-cached "
                              f"decode steps per 30-s window, token timestamps "

@@ -28,6 +28,15 @@ int mwx_test_encode(struct mwx_context* ctx, struct mwx_state* state, const floa
 
 /* Teacher-forced decoder run against the cross K/V left by mwx_test_encode:
  * token i at position i, logits_out [n][n_vocab] (raw logits). */
+/* The encoder of one clip window with its intermediates copied out: x_out
+ * [n_audio_layer + 1][n_audio_ctx][n_audio_state] f32 = the residual stream
+ * after the conv stem and after each layer; a_out[0..3] = per layer the four
+ * GEMM A operands as the model's 16-bit type (raw bits), before any MX-fp8
+ * quantization: attention LayerNorm out, attention out, MLP LayerNorm out
+ * ([L][n_ctx][d] each) and GELU out ([L][n_ctx][4 d]). */
+int mwx_test_encode_dump(struct mwx_context* ctx, struct mwx_state* state, const float* pcm,
+                         int n, int seek, float* x_out, uint16_t* const* a_out);
+
 int mwx_test_decode(struct mwx_context* ctx, struct mwx_state* state, const int* tokens, int n,
                     float* logits_out);
 

@@ -731,9 +731,70 @@ struct ResultCache {
 };
 static ResultCache<std::vector<float>> g_enc_cache{8, {}};
 
+// the conv stem: mel window x [n_mels][2 n_ctx] -> residual stream inp [n_ctx][D]
+static void encode_stem(const Model& m, const std::vector<float>& x, std::vector<float>& inp) {
+  const int n_ctx = m.n_audio_ctx, D = m.n_audio_state;
+  const int T = 2 * n_ctx;
+  std::vector<float> h1((size_t)T * D), h2((size_t)n_ctx * D);
+  conv1d(m, m.w("encoder.conv1.weight"), m.w("encoder.conv1.bias"), x.data(), m.n_mels, T, D, 1, h1.data());
+  for (auto& v : h1) v = gelu(m, v);
+  // conv2 consumes channel-major input
+  std::vector<float> h1c((size_t)D * T);
+  for (int t = 0; t < T; ++t)
+    for (int d = 0; d < D; ++d) h1c[(size_t)d * T + t] = h1[(size_t)t * D + d];
+  conv1d(m, m.w("encoder.conv2.weight"), m.w("encoder.conv2.bias"), h1c.data(), D, T, D, 2, h2.data());
+  const float* pe = m.w("encoder.positional_embedding");
+  inp.resize((size_t)n_ctx * D);
+  for (size_t i = 0; i < inp.size(); ++i) inp[i] = pe[i] + gelu(m, h2[i]);
+}
+
+// Test hook of one encoder layer (orc_encode_layer): ext[g] non-null takes
+// GEMM g's A operand (0: attn LN output, 1: attention output, 2: mlp LN
+// output, 3: GELU output) from the caller instead of computing it; out[g]
+// non-null receives the A operand used.
+struct EncLayerIO {
+  const float* ext[4];
+  float* out[4];
+};
+
+// one encoder layer on the residual stream inp [n_ctx][D], in place
+static void encode_layer(const Model& m, int il, std::vector<float>& inp, const EncLayerIO* io) {
+  const int M = m.n_audio_ctx, D = m.n_audio_state, H = m.n_audio_head;
+  std::vector<float> cur((size_t)M * D), q((size_t)M * D), k((size_t)M * D),
+      v((size_t)M * D), o((size_t)M * D), ff((size_t)M * 4 * D);
+  const float KQscale = 1.0f / sqrtf((float)(D / H));
+  const bool mx = (m.flags & ORC_MXFP8) != 0;
+  auto operand = [&](int g, std::vector<float>& a) {
+    if (io && io->ext[g]) std::copy(io->ext[g], io->ext[g] + a.size(), a.begin());
+    if (io && io->out[g]) std::copy(a.begin(), a.end(), io->out[g]);
+  };
+  const std::string p = "encoder.blocks." + std::to_string(il);
+  layer_norm(inp.data(), m.w(p + ".attn_ln.weight"), m.w(p + ".attn_ln.bias"), M, D, cur.data());
+  operand(0, cur);
+  matmul(m, m.w(p + ".attn.query.weight"), cur.data(), M, D, D, q.data(), mx);
+  add_bias(q.data(), m.w(p + ".attn.query.bias"), M, D);
+  matmul(m, m.w(p + ".attn.key.weight"), cur.data(), M, D, D, k.data(), mx);
+  matmul(m, m.w(p + ".attn.value.weight"), cur.data(), M, D, D, v.data(), mx);
+  add_bias(v.data(), m.w(p + ".attn.value.bias"), M, D);
+  attention(m, q.data(), k.data(), v.data(), M, M, D, H, KQscale, -1, o.data());
+  operand(1, o);
+  matmul(m, m.w(p + ".attn.out.weight"), o.data(), M, D, D, cur.data(), mx);
+  add_bias(cur.data(), m.w(p + ".attn.out.bias"), M, D);
+  for (size_t i = 0; i < inp.size(); ++i) inp[i] = cur[i] + inp[i];
+  layer_norm(inp.data(), m.w(p + ".mlp_ln.weight"), m.w(p + ".mlp_ln.bias"), M, D, cur.data());
+  operand(2, cur);
+  matmul(m, m.w(p + ".mlp.0.weight"), cur.data(), M, 4 * D, D, ff.data(), mx);
+  add_bias(ff.data(), m.w(p + ".mlp.0.bias"), M, 4 * D);
+  for (auto& e : ff) e = gelu(m, e);
+  operand(3, ff);
+  matmul(m, m.w(p + ".mlp.2.weight"), ff.data(), M, D, 4 * D, cur.data(), mx);
+  add_bias(cur.data(), m.w(p + ".mlp.2.bias"), M, D);
+  for (size_t i = 0; i < inp.size(); ++i) inp[i] = cur[i] + inp[i];
+}
+
 // Encodes the 2*n_ctx mel frames starting at `seek`; out = embd_enc [n_ctx][D].
 static void encode(const Model& m, const Mel& mel, int seek, std::vector<float>& out) {
-  const int n_ctx = m.n_audio_ctx, D = m.n_audio_state, H = m.n_audio_head;
+  const int n_ctx = m.n_audio_ctx, D = m.n_audio_state;
   const int T = 2 * n_ctx;
   std::vector<float> x((size_t)m.n_mels * T, 0.0f);
   const int i0 = std::min(seek, mel.n_len), i1 = std::min(seek + T, mel.n_len);
@@ -745,45 +806,12 @@ static void encode(const Model& m, const Mel& mel, int seek, std::vector<float>&
     out = *hit;
     return;
   }
-  std::vector<float> h1((size_t)T * D), h2((size_t)n_ctx * D);
-  conv1d(m, m.w("encoder.conv1.weight"), m.w("encoder.conv1.bias"), x.data(), m.n_mels, T, D, 1, h1.data());
-  for (auto& v : h1) v = gelu(m, v);
-  // conv2 consumes channel-major input
-  std::vector<float> h1c((size_t)D * T);
-  for (int t = 0; t < T; ++t)
-    for (int d = 0; d < D; ++d) h1c[(size_t)d * T + t] = h1[(size_t)t * D + d];
-  conv1d(m, m.w("encoder.conv2.weight"), m.w("encoder.conv2.bias"), h1c.data(), D, T, D, 2, h2.data());
-  const float* pe = m.w("encoder.positional_embedding");
-  std::vector<float> inp((size_t)n_ctx * D);
-  for (size_t i = 0; i < inp.size(); ++i) inp[i] = pe[i] + gelu(m, h2[i]);
-
+  std::vector<float> inp;
+  encode_stem(m, x, inp);
   const int M = n_ctx;
-  std::vector<float> cur((size_t)M * D), q((size_t)M * D), k((size_t)M * D),
-      v((size_t)M * D), o((size_t)M * D), ff((size_t)M * 4 * D);
-  const float KQscale = 1.0f / sqrtf((float)(D / H));
   const int n_layers = g_enc_layer_limit >= 0 ? std::min(g_enc_layer_limit, m.n_audio_layer)
                                              : m.n_audio_layer;
-  const bool mx = (m.flags & ORC_MXFP8) != 0;
-  for (int il = 0; il < n_layers; ++il) {
-    const std::string p = "encoder.blocks." + std::to_string(il);
-    layer_norm(inp.data(), m.w(p + ".attn_ln.weight"), m.w(p + ".attn_ln.bias"), M, D, cur.data());
-    matmul(m, m.w(p + ".attn.query.weight"), cur.data(), M, D, D, q.data(), mx);
-    add_bias(q.data(), m.w(p + ".attn.query.bias"), M, D);
-    matmul(m, m.w(p + ".attn.key.weight"), cur.data(), M, D, D, k.data(), mx);
-    matmul(m, m.w(p + ".attn.value.weight"), cur.data(), M, D, D, v.data(), mx);
-    add_bias(v.data(), m.w(p + ".attn.value.bias"), M, D);
-    attention(m, q.data(), k.data(), v.data(), M, M, D, H, KQscale, -1, o.data());
-    matmul(m, m.w(p + ".attn.out.weight"), o.data(), M, D, D, cur.data(), mx);
-    add_bias(cur.data(), m.w(p + ".attn.out.bias"), M, D);
-    for (size_t i = 0; i < inp.size(); ++i) inp[i] = cur[i] + inp[i];
-    layer_norm(inp.data(), m.w(p + ".mlp_ln.weight"), m.w(p + ".mlp_ln.bias"), M, D, cur.data());
-    matmul(m, m.w(p + ".mlp.0.weight"), cur.data(), M, 4 * D, D, ff.data(), mx);
-    add_bias(ff.data(), m.w(p + ".mlp.0.bias"), M, 4 * D);
-    for (auto& e : ff) e = gelu(m, e);
-    matmul(m, m.w(p + ".mlp.2.weight"), ff.data(), M, D, 4 * D, cur.data(), mx);
-    add_bias(cur.data(), m.w(p + ".mlp.2.bias"), M, D);
-    for (size_t i = 0; i < inp.size(); ++i) inp[i] = cur[i] + inp[i];
-  }
+  for (int il = 0; il < n_layers; ++il) encode_layer(m, il, inp, nullptr);
   out.resize((size_t)M * D);
   layer_norm(inp.data(), m.w("encoder.ln_post.weight"), m.w("encoder.ln_post.bias"), M, D, out.data());
   if (!m.key.empty()) g_enc_cache.put(ckey, out);
@@ -2138,6 +2166,34 @@ int orc_mel(void* h, const float* pcm, int n, float* out, int out_cap, int* n_le
 }
 
 // encoder on a mel [n_mels][n_len]; out = [n_audio_ctx][n_audio_state]
+// test hooks of the encoder's parts (tests/test_gpu_c5.py per-layer check):
+// the conv stem's residual stream for the window at `seek`, and one layer on
+// a given residual stream x_in [n_ctx][D] -> x_out, with optional external /
+// returned GEMM A operands (EncLayerIO: attn LN out, attention out, mlp LN
+// out [n_ctx][D]; GELU out [n_ctx][4D])
+void orc_encode_stem(void* h, const float* mel_data, int n_len, int seek, float* x_out) {
+  const Model& m = *(const Model*)h;
+  const int T = 2 * m.n_audio_ctx;
+  std::vector<float> x((size_t)m.n_mels * T, 0.0f);
+  const int i0 = std::min(seek, n_len), i1 = std::min(seek + T, n_len);
+  for (int j = 0; j < m.n_mels; ++j)
+    for (int i = i0; i < i1; ++i) x[(size_t)j * T + (i - i0)] = mel_data[(size_t)j * n_len + i];
+  std::vector<float> inp;
+  encode_stem(m, x, inp);
+  std::copy(inp.begin(), inp.end(), x_out);
+}
+void orc_encode_layer(void* h, int il, const float* x_in, const float* const* ext, float* const* outs,
+                      float* x_out) {
+  const Model& m = *(const Model*)h;
+  std::vector<float> inp(x_in, x_in + (size_t)m.n_audio_ctx * m.n_audio_state);
+  EncLayerIO io{};
+  for (int g = 0; g < 4; ++g) {
+    io.ext[g] = ext ? ext[g] : nullptr;
+    io.out[g] = outs ? outs[g] : nullptr;
+  }
+  encode_layer(m, il, inp, &io);
+  std::copy(inp.begin(), inp.end(), x_out);
+}
 void orc_encode(void* h, const float* mel_data, int n_len, int seek, float* out) {
   auto* m = (Model*)h;
   Mel mel;

@@ -61,6 +61,8 @@ def lib() -> C.CDLL:
     L.orc_mel.argtypes = [P, fp, C.c_int, fp, C.c_int, C.POINTER(C.c_int)]
     L.orc_encode.argtypes = [P, fp, C.c_int, C.c_int, fp]
     L.orc_cross.argtypes = [P, fp, fp, fp]
+    L.orc_encode_stem.argtypes = [P, fp, C.c_int, C.c_int, fp]
+    L.orc_encode_layer.argtypes = [P, C.c_int, fp, C.POINTER(fp), C.POINTER(fp), fp]
     L.orc_decode_seq.argtypes = [P, fp, fp, C.POINTER(C.c_int), C.c_int, fp]
     L.orc_full.restype = P
     L.orc_full.argtypes = [P, C.POINTER(C.c_int), fp, C.c_char_p, C.c_char_p, fp, C.c_int,
@@ -304,6 +306,31 @@ class Oracle:
         out = np.empty((self.hp[1], self.d), dtype=np.float32)
         lib().orc_encode(self.h, _fp(mel), mel.shape[1], seek, _fp(out))
         return out
+
+    def encode_stem(self, mel: np.ndarray, seek: int = 0) -> np.ndarray:
+        """The conv stem's residual stream [n_ctx][d] (input of encoder layer 0)."""
+        mel = np.ascontiguousarray(mel, dtype=np.float32)
+        out = np.empty((self.hp[1], self.d), dtype=np.float32)
+        lib().orc_encode_stem(self.h, _fp(mel), mel.shape[1], seek, out.ctypes.data_as(C.POINTER(C.c_float)))
+        return out
+
+    def encode_layer(self, il: int, x: np.ndarray, ext=None, want_operands: bool = False):
+        """Encoder layer il on the residual stream x [n_ctx][d]: returns the
+        next residual stream, and with want_operands the four GEMM A operands
+        it used (attn LN out, attention out, mlp LN out, GELU out). ext: up to
+        four arrays (None entries: computed) that replace those operands."""
+        n, d = self.hp[1], self.d
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        shapes = [(n, d), (n, d), (n, d), (n, 4 * d)]
+        ext_arr = [None if ext is None or ext[g] is None else
+                   np.ascontiguousarray(ext[g], dtype=np.float32).reshape(shapes[g]) for g in range(4)]
+        outs = [np.empty(sh, np.float32) for sh in shapes] if want_operands else [None] * 4
+        FP = C.POINTER(C.c_float)
+        ext_p = (FP * 4)(*[FP() if a is None else _fp(a) for a in ext_arr])
+        out_p = (FP * 4)(*[FP() if a is None else _fp(a) for a in outs])
+        y = np.empty((n, d), np.float32)
+        lib().orc_encode_layer(self.h, il, _fp(x), ext_p, out_p, _fp(y))
+        return (y, outs) if want_operands else y
 
     def cross(self, enc: np.ndarray):
         enc = np.ascontiguousarray(enc, dtype=np.float32)

@@ -76,7 +76,13 @@ for s in "$@"; do
     ab*)  # A/B of builds on one box: ablib/libmwx_<build>.so, 2 lanes
       v=${s#ab}; [ "$v" = h ] && v=head
       run "${s}_$(date +%s)" 400 env MWX_LIB=$GRAFT_REPO_ROOT/ablib/libmwx_$v.so python -u bench.py --steps 12 --warmup 3 --no-cpu-baseline --no-one-lane ;;
-    tests) run tests 1150 python -u -m pytest tests -m gpu -v -s -rf --timeout 600 --timeout-method thread ;;
+    svc) run svc 700 python -u bench.py --service-defaults --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    svc2) run svc2 900 python -u bench.py --service-defaults --steps 4 --warmup 1 --no-cpu-baseline --no-one-lane ;;
+    fdl) run fdl 600 python -u -m pytest tests/test_gpu_fulldepth.py -k "language_auto" -m gpu -v -s -rf --timeout 500 --timeout-method thread ;;
+    beamorcr) run beamorcr 600 python -u -m pytest tests/test_gpu_beam_oracle.py -k "not full_depth" -m gpu -v -s -rf --timeout 500 --timeout-method thread ;;
+    beamorcf) run beamorcf 1000 python -u -m pytest tests/test_gpu_beam_oracle.py -k "full_depth" -m gpu -v -s -rf --durations=0 --timeout 900 --timeout-method thread ;;
+    newtests) run newtests 600 python -u -m pytest tests/test_gpu_parity.py -k "extreme_scales or 8phase or runahead_mismatch" -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
+    tests) run tests 1150 python -u -m pytest tests -m gpu -v -s -rf --durations=0 --timeout 600 --timeout-method thread ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python -u bench.py --steps 20 --warmup 5 ;;
     benchq) run benchq 400 python -u bench.py --steps 8 --warmup 2 --no-cpu-baseline ;;

@@ -794,6 +794,19 @@ struct Driver {
   // rows per clip in the current decode run (beam_size / best_of decoders are
   // consecutive rows of one clip); decode groups never split such a run
   int xgroup = 1;
+  // test hook (mwx_test_encode_dump, one clip): host copies of the residual
+  // stream after the stem and after every layer, and every layer's four GEMM
+  // A operands before any MX quantization (attn LN out, attention out, mlp LN
+  // out, GELU out; 16-bit bits)
+  struct EncDump {
+    float* x;        // [L_enc + 1][n_ctx][d]
+    uint16_t* a[4];  // [L_enc][n_ctx][d] (a[3]: [L_enc][n_ctx][4d])
+  };
+  const EncDump* dump = nullptr;
+  void dump_copy(void* dst, const void* src, size_t bytes) {
+    HIPC(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+  }
 
   Driver(Context& c, State& s, const mwx_full_params& p)
       : C(c), S(s), st(s.stream), P(p), hp(c.hp) {
@@ -902,6 +915,8 @@ struct Driver {
       e.span = span_slot(S, "enc_gemm", st);
     gemm<_Float16>(EPI_CONV2, false, h1p, 2 * d, (long)(T2 + 2) * d, C.conv2_w, 3 * d, Lc, d,
                    3 * d, nb, e, st); }
+    const size_t md = (size_t)Lc * d;  // (dump: one clip)
+    if (dump) dump_copy(dump->x, x, md * 4);
     const float kq_scale = 1.0f / sqrtf(64.0f);
     // fp8 compute: the A operand of every encoder / cross GEMM is the 16-bit
     // activation quantized to MX-fp8 (as the oracle's ORC_MXFP8 mode)
@@ -933,8 +948,10 @@ struct Driver {
       { PerfScope ps(S, "enc_gemm", st);
       e.span = span_slot(S, "enc_gemm", st);
       mgemm(EPI_ENC_QKV, h, d, W.qkv_x, W.qkv_w, 3 * d, e); }
+      if (dump) dump_copy(dump->a[0] + l * md, h, md * 2);
       { PerfScope ps(S, "enc_attn", st);
       enc_attention<T>(q, k, vt, o, nb, H, Lc, kq_scale, st); }
+      if (dump) dump_copy(dump->a[1] + l * md, o, md * 2);
       e = EpiParams();
       e.bias = W.o_b;
       e.c32 = x;
@@ -952,6 +969,10 @@ struct Driver {
       { PerfScope ps(S, "enc_gemm", st);
       e.span = span_slot(S, "enc_gemm", st);
       mgemm(EPI_GELU, h, d, W.fc1_x, W.fc1_w, 4 * d, e); }
+      if (dump) {
+        dump_copy(dump->a[2] + l * md, h, md * 2);
+        dump_copy(dump->a[3] + l * 4 * md, ff, 4 * md * 2);
+      }
       e = EpiParams();
       e.bias = W.fc2_b;
       e.c32 = x;
@@ -960,6 +981,7 @@ struct Driver {
       { PerfScope ps(S, "enc_gemm", st);
       e.span = span_slot(S, "enc_gemm", st);
       mgemm(EPI_RES, ff, 4 * d, W.fc2_x, W.fc2_w, d, e); }
+      if (dump) dump_copy(dump->x + (l + 1) * md, x, md * 4);
     }
     layer_norm<T>(x, C.enc_ln_w, C.enc_ln_b, enc, M, d, nullptr, st);
     // cross K/V of every decoder layer in one GEMM

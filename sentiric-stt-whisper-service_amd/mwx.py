@@ -213,6 +213,9 @@ def lib() -> C.CDLL:
     L.mwx_test_dequantize.argtypes = [C.c_int, C.c_void_p, C.c_long, C.POINTER(C.c_float)]
     L.mwx_test_decode_counters.restype = C.c_int
     L.mwx_test_decode_counters.argtypes = [P, C.POINTER(C.c_long), C.POINTER(C.c_long), C.c_int]
+    L.mwx_test_encode_dump.restype = C.c_int
+    L.mwx_test_encode_dump.argtypes = [P, P, C.POINTER(C.c_float), C.c_int, C.c_int,
+                                       C.POINTER(C.c_float), C.POINTER(C.c_void_p)]
     L.mwx_test_window_counters.restype = C.c_int
     L.mwx_test_window_counters.argtypes = [P, C.POINTER(C.c_long), C.POINTER(C.c_long), C.c_int]
     L.mwx_test_runahead_fallbacks.restype = C.c_long
@@ -615,6 +618,25 @@ class Context:
         if r != 0:
             raise RuntimeError(f"mwx_test_encode returned {r}")
         return enc, k, v
+
+    def test_encode_dump(self, pcm: np.ndarray, seek: int = 0, state_index: int = 0):
+        """mwx_test_encode_dump: (x [L+1][n_ctx][d] f32 — the residual stream
+        after the stem and after each layer, [a0, a1, a2, a3] — per layer the
+        four GEMM A operands before MX quantization, as float32 from the
+        model's 16-bit type)."""
+        pcm = np.ascontiguousarray(pcm, dtype=np.float32)
+        n_ctx, d, L = self.hparam("n_audio_ctx"), self.d, self._hp_from_file()[4]
+        x = np.empty((L + 1, n_ctx, d), np.float32)
+        a = [np.empty((L, n_ctx, d * (4 if g == 3 else 1)), np.uint16) for g in range(4)]
+        ptrs = (C.c_void_p * 4)(*[arr.ctypes.data for arr in a])
+        r = lib().mwx_test_encode_dump(self.ctx, self.state(state_index), fptr(pcm), len(pcm), seek,
+                                       fptr(x), ptrs)
+        if r != 0:
+            raise RuntimeError(f"mwx_test_encode_dump returned {r}")
+        bf16 = self.hparam("model_wtype") == GGML_BF16
+        conv = ((lambda u: (u.astype(np.uint32) << 16).view(np.float32)) if bf16 else
+                (lambda u: u.view(np.float16).astype(np.float32)))
+        return x, [conv(arr) for arr in a]
 
     def test_decode(self, tokens: Sequence[int]) -> np.ndarray:
         toks = np.ascontiguousarray(tokens, dtype=np.int32)

@@ -129,3 +129,78 @@ def test_c5_bench_call_batch_equals_single(v3path):
             assert ctx.token_records(n + c) == batched[c], c
         for b in dev:
             b.free()
+
+
+def _mx_round(a):
+    """MX-fp8 rounding of rows of 32-element blocks (the engine's and the MX
+    oracle's activation quantization): a power-of-two scale per block, the
+    smallest 2^E with max |x| <= 448 * 2^E, and e4m3 round-to-nearest-even
+    of x / 2^E (3 mantissa bits; subnormal step 2^-9); returns the rounded
+    values (float64)."""
+    h = a.reshape(-1, 32).astype(np.float64)
+    amax = np.abs(h).max(axis=1, keepdims=True)
+    E = np.ceil(np.log2(np.maximum(amax, 1e-30) / 448.0))
+    x = h / np.exp2(E)
+    _, ex = np.frexp(x)  # |x| = m 2^ex, m in [0.5, 1): floor(log2 |x|) = ex - 1
+    ulp = np.exp2(np.maximum(ex - 1, -6) - 3)
+    return (np.rint(x / ulp) * ulp * np.exp2(E)).reshape(a.shape)
+
+
+def test_mxfp8_encoder_per_layer_error_and_flips(v3path):
+    """Where C5's end-to-end logits error comes from: the
+    full-depth MX-fp8 encoder, layer by layer. For every layer l the device's
+    own layer-l input (its residual stream after layer l - 1) is fed to the
+    MX oracle's layer l, twice:
+      own  the oracle computes the layer's four GEMM A operands itself;
+      dev  the oracle takes the device's A operands (its LayerNorm, attention
+           and GELU outputs) and only runs the GEMMs / residual adds.
+    `dev` differs from the device only in f32 summation order; `own` adds the
+    operand differences, of which the MX-visible part is the e4m3 boundary
+    flips: elements whose MX rounding differs between the device's operand and
+    the oracle's. Per layer: local error of both, flip counts. Asserted: every
+    layer's `dev` error is summation noise (no per-layer arithmetic bug hides
+    under the end-to-end tolerance), every layer's `own` error within a fixed
+    multiple of the layer's flip-free error plus what its flips can move, and
+    the end-to-end drift of the residual stream no larger than the sum of the
+    per-layer local errors (accumulation, not one bad layer)."""
+    omx = orc.Oracle(v3path, mxfp8=True)
+    pcm = pcm_clip(0)
+    with mwx.Context.open(v3path, compute=mwx.COMPUTE_MXFP8) as ctx:
+        xs, ops = ctx.test_encode_dump(pcm)
+    L = xs.shape[0] - 1
+    mel, _ = omx.mel(pcm)
+    x0 = omx.encode_stem(mel)
+    stem_err = float(np.abs(xs[0] - x0).max())
+    rows = []
+    xo = x0  # the oracle's own stream, for the end-to-end drift
+    for l in range(L):
+        scale = float(np.abs(xs[l + 1]).max())
+        y_own, o_ops = omx.encode_layer(l, xs[l], want_operands=True)
+        y_dev = omx.encode_layer(l, xs[l], ext=[ops[g][l] for g in range(4)])
+        e_own = float(np.abs(y_own - xs[l + 1]).max())
+        e_dev = float(np.abs(y_dev - xs[l + 1]).max())
+        flips = [int((_mx_round(ops[g][l]) != _mx_round(o_ops[g])).sum()) for g in range(4)]
+        xo = omx.encode_layer(l, xo)
+        drift = float(np.abs(xo - xs[l + 1]).max())
+        rows.append((l, scale, e_own, e_dev, flips, drift))
+    n_el = [ops[g][0].size for g in range(4)]
+    print(f"MX-fp8 encoder, full depth: stem err {stem_err:.3g}")
+    print("layer | max|x| | local err (own ops) | local err (device ops) | e4m3 flips "
+          "(attnLN / attn / mlpLN / gelu) | end-to-end drift")
+    for l, scale, e_own, e_dev, flips, drift in rows:
+        fr = " / ".join(f"{f} ({f / n:.1e})" for f, n in zip(flips, n_el))
+        print(f"{l:2d} | {scale:8.2f} | {e_own:.4g} | {e_dev:.3g} | {fr} | {drift:.4g}")
+    e_dev_max = max(r[3] / r[1] for r in rows)
+    # device operands: f32 summation order only (relative to the stream's scale)
+    assert e_dev_max < 1e-4, e_dev_max
+    assert stem_err < 1e-2 * float(np.abs(x0).max()), stem_err
+    for l, scale, e_own, e_dev, flips, drift in rows:
+        # own operands: the flips (and the bf16 rounding they come with) are
+        # the only difference; a layer without flips must agree like `dev`
+        if sum(flips) == 0:
+            assert e_own <= 10 * max(e_dev, 1e-6 * scale), (l, e_own, e_dev)
+    # accumulation: the drift after layer l is bounded by the local errors so far
+    acc = 0.0
+    for l, scale, e_own, e_dev, flips, drift in rows:
+        acc += e_own
+        assert drift <= 4 * acc + 1e-3 * scale, (l, drift, acc)

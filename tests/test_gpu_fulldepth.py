@@ -194,3 +194,53 @@ def test_v3_geometry_plain_weights_greedy_matches_oracle(make_model):
             # behind the diagnostic `tid` field is a tie within bf16 noise —
             # seen: pt 0.3441 / 0.3416 on the same text token, equal t0 / t1)
             assert_same(segs, osegs, p_tol=3e-2, tid_tie_tol=1e-2)
+
+
+def test_full_depth_large_v3_language_auto_matches_oracle(v3full):
+    """The service's default language = "auto" (/root/reference/src/config.h:47)
+    on the benched model at full depth: the window-0 detect (encode, one
+    decode of <|startoftranscript|>, argmax over the language tokens) and the
+    greedy window that follows (STEPS fixed steps) against the oracle. The
+    detected language must equal the oracle's wherever the oracle's top-1 /
+    top-2 language-logit margin exceeds 2 x the measured logits error, and the
+    token ids must equal the oracle's up to the first step inside that noise."""
+    ctx, path = v3full
+    pcm = pcm_clip(0)
+    idx = len(ctx.states)
+    p = service_params(ctx, temperature_inc=0.0, language=b"auto")
+    p.bench_fixed_steps = STEPS
+    assert ctx.full(pcm, p, state_index=idx) == 0
+    ids = [t.id for s in ctx.segments(idx) for t in s.tokens]
+    o = orc.Oracle(path)
+    opt = greedy_opt(STEPS)
+    opt.language = "auto"
+    _, osegs, lang, _ = o.full(pcm, opt)
+    oids = [t.id for s in osegs for t in s.tokens]
+    n_lang = o.translate - o.sot - 1
+    mel, _ = o.mel(pcm)
+    k, v = o.cross(o.encode(mel))
+    lg_o = o.decode_seq(k, v, [o.sot])[0, o.sot + 1:o.sot + 1 + n_lang]
+    ctx.test_encode(pcm, cross=False)  # (mwx_test_decode runs on state 0)
+    lg_d = ctx.test_decode([o.sot])[0, o.sot + 1:o.sot + 1 + n_lang]
+    lerr = float(np.abs(lg_d - lg_o).max())
+    s = np.sort(lg_o)
+    lmargin = float(s[-1] - s[-2])
+    dlang = ctx.lang_id(idx)
+    print(f"full-depth large-v3 language auto: oracle language {lang}, device {dlang}; "
+          f"language-logit margin {lmargin:.4f}, err {lerr:.4f}")
+    assert lerr < 0.25, lerr
+    if lmargin > 2 * lerr:
+        assert dlang == lang, (dlang, lang, lmargin, lerr)
+    if dlang != lang:
+        return  # a near-tie language pick: the windows decode different prompts
+    prompt = [o.sot, o.sot + 1 + lang, o.transcribe]
+    m = text_margins(o, pcm, prompt, oids, o.eot)
+    lg_t = ctx.test_decode(prompt + oids[:-1])[len(prompt) - 1:, :o.eot]
+    ref = o.decode_seq(k, v, prompt + oids[:-1])[len(prompt) - 1:, :o.eot]
+    err = float(np.abs(lg_t - ref).max())
+    first = next((i for i, (a, b) in enumerate(zip(ids, oids)) if a != b), None)
+    print(f"  window 0 ({STEPS} steps): logits err {err:.4f}, oracle top-1 margin min "
+          f"{m.min():.4f}; ids equal up to step {STEPS if first is None else first}")
+    assert len(ids) == len(oids) == STEPS
+    if first is not None:
+        assert m[first] <= 2 * err, (first, float(m[first]), err)

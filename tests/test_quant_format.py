@@ -396,3 +396,19 @@ def test_model_quantize_tool_k(make_model, tmp_path, tt):
     assert np.corrcoef(x, y)[0, 1] > (0.8 if tt == mwx.GGML_Q2_K else 0.97)
     with pytest.raises(RuntimeError):
         mwx.quantize_model(make_model("tiny", mwx.GGML_F16), str(tmp_path / "bad.bin"), tt)
+
+
+def test_mx_round_helper_matches_e4m3_codes():
+    """tests/test_gpu_c5.py's vectorised MX rounding (used to count e4m3
+    boundary flips) equals the code-level e4m3 encode / decode of
+    test_gpu_parity.py on random blocks spanning many scales."""
+    import numpy as np
+    from test_gpu_c5 import _mx_round
+    from test_gpu_parity import _e4m3_decode, _e4m3_encode
+    rng = np.random.default_rng(5)
+    a = (rng.standard_normal((64, 256)) * np.exp2(rng.uniform(-20, 12, (64, 1)))).astype(np.float32)
+    a[3, :40] = 0.0
+    h = a.reshape(-1, 32).astype(np.float64)
+    E = np.ceil(np.log2(np.maximum(np.abs(h).max(axis=1, keepdims=True), 1e-30) / 448.0))
+    ref = _e4m3_decode(_e4m3_encode(h / np.exp2(E))) * np.exp2(E)
+    assert np.array_equal(_mx_round(a), ref.reshape(a.shape))
