@@ -116,6 +116,12 @@ int mwx_test_set_dec_shared(int on);
  * Returns the previous mode. */
 int mwx_test_set_gemm_8ph(int on);
 
+/* The decoder self-attention of beam / best-of groups as one workgroup per
+ * (group, head) with the shared history loaded once (1, the default) or one
+ * workgroup per (row, head) (0); -1: back to the MWX_SELF_GROUP environment
+ * default. Returns the previous mode. */
+int mwx_test_set_self_group(int on);
+
 /* Fault injection of the run-ahead safety net: run-ahead step `step` of every
  * later attempt is treated as a device/host disagreement (-1: none; -2: back
  * to the MWX_TEST_RA_MISMATCH environment default). Returns the previous

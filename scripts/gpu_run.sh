@@ -82,6 +82,13 @@ for s in "$@"; do
     beamorcr) run beamorcr 600 python -u -m pytest tests/test_gpu_beam_oracle.py -k "not full_depth" -m gpu -v -s -rf --timeout 500 --timeout-method thread ;;
     beamorcf) run beamorcf 1000 python -u -m pytest tests/test_gpu_beam_oracle.py -k "full_depth" -m gpu -v -s -rf --durations=0 --timeout 900 --timeout-method thread ;;
     newtests) run newtests 600 python -u -m pytest tests/test_gpu_parity.py -k "extreme_scales or 8phase or runahead_mismatch" -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
+    pmcbs)  # beam 5 bf16 at the benched 220 steps: FETCH and LDS / MFMA passes (the self-attention's history reads)
+      for x in "fetch:FETCH_SIZE" "lds:SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE"; do
+        n=${x%%:*}; c=${x#*:}
+        (cd /tmp && run pmcbs_$n 400 rocprofv3 --pmc $c --output-format csv -d "$O/${TAG}_pmcbs_$n" -o pmc -- $B --beam 5 --lanes 1 --steps 1 --warmup 0 --no-cpu-baseline) || exit 5
+        python3 scripts/pmc_mix.py "$O/${TAG}_pmcbs_$n" 14 > "$O/${TAG}_pmcbs_$n.md" || exit 5
+      done ;;
+    barprobe) run barprobe 120 ./scripts/probe/xcd_barrier_probe 4000 ;;
     tests) run tests 1150 python -u -m pytest tests -m gpu -v -s -rf --durations=0 --timeout 600 --timeout-method thread ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python -u bench.py --steps 20 --warmup 5 ;;
@@ -117,7 +124,7 @@ for s in "$@"; do
     streamr) run streamr 300 python -u bench.py --stream --rich --arch base --wtype f16 --steps 3 --warmup 1 ;;
     streamv3r) run streamv3r 500 python -u bench.py --stream --rich --arch large-v3 --wtype bf16 --steps 1 --warmup 1 ;;
     streamv3) run streamv3 400 python -u bench.py --stream --arch large-v3 --wtype bf16 --steps 2 --warmup 1 ;;
-    g8tests) run g8tests 300 python -u -m pytest tests/test_gpu_parity.py -k "8phase or gemm_gelu or encoder_and_cross" -m gpu -v -s -rf --timeout 120 --timeout-method thread ;;
+    g8tests) run g8tests 300 python -u -m pytest tests/test_gpu_parity.py -k "8phase or gemm_gelu or encoder_and_cross or mx_gemm or mxfp8_encoder" -m gpu -v -s -rf --timeout 120 --timeout-method thread ;;
     bench1g8) run bench1g8 400 env MWX_GEMM_8PH=1 python -u bench.py --lanes 1 --steps 4 --warmup 1 --no-cpu-baseline ;;
     ptests) run ptests 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
     tr8) run tr8 120 ./scripts/probe/tr8_probe ;;

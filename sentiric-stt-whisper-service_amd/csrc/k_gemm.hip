@@ -513,6 +513,19 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
   if ((STAGED16 || STAGED32) && (N & 63) == 0 && !P.pack_out) {
     // Epilogue through LDS: the ring is idle now; each wave stages its 128x64
     // tile (16 KB) so every global store is a 16-B (8-B for V^T) vector.
+    // Staging swizzles (bit-identical: layout only). A fragment store writes
+    // rows 4g + r (lane group g = lane >> 4) of 16 columns, so without a
+    // swizzle the four groups' rows (512 B apart) land on the same banks
+    // (4-way), and the V^T image's 16 e-rows of one t (256 B apart) on one
+    // bank (16-way; PMC r05: 0.39 of the QKV launch's LDS cycles conflicted).
+    //   16-bit row-major [row][64]: 16-B chunk ^ sw16(row) = ((row >> 2) & 3) << 1
+    //   f32 row-major [row][64]:    16-B chunk ^ sw32(row) = ((row >> 2) & 3) << 2
+    //   V^T [e][128 t], 8-B (4-t) stores: 8-B chunk ^ swv(e) = (e & 15) << 1
+    // so every store instruction covers distinct banks and the 16-B / 8-B
+    // read-outs stay row-contiguous permutations (conflict-free).
+    auto sw16 = [](int row) { return ((row >> 2) & 3) << 1; };
+    auto sw32 = [](int row) { return ((row >> 2) & 3) << 2; };
+    auto swv = [](int e) { return (e & 15) << 1; };
     __builtin_amdgcn_s_barrier();  // all waves are past their last ring read
     uint16_t* gtl = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(lds_raw) + GT_OFF);
     if constexpr (EPI == EPI_GELU) {
@@ -550,7 +563,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
               } else {
                 bits = __builtin_bit_cast(uint16_t, to_t<T>(g));
               }
-              wg[lr * 64 + lc] = bits;
+              wg[lr * 64 + (((lc >> 3) ^ sw16(lr)) << 3) + (lc & 7)] = bits;
             }
           }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -560,7 +573,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
           const int row = it * 8 + (lane >> 3), ch = lane & 7;
           const int m = wr0 + hh * 64 + row;
           if (m >= M) continue;
-          const uint4 v = *reinterpret_cast<const uint4*>(&wg[row * 64 + ch * 8]);
+          const uint4 v = *reinterpret_cast<const uint4*>(&wg[row * 64 + ((ch ^ sw16(row)) << 3)]);
           _Float16* dst = reinterpret_cast<_Float16*>(P.c16) + (long)bz * P.c_bstride +
                           (long)m * P.ldc + wc0 + ch * 8;
           *reinterpret_cast<uint4*>(dst) = v;
@@ -594,19 +607,27 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
         for (int j = 0; j < GFN; ++j) {
           const int lc = j * 16 + (lane & 15);
           const int n = wc0 + lc;
+          uint16_t bits[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int lr = i * 16 + (lane >> 4) * 4 + r;
             const float a = acc[i][j][r];
-            uint16_t bits;
             if constexpr (EPI == EPI_ENC_QKV) {
               const _Float16 hv = f16r(a + P.bias[n]);
-              bits = __builtin_bit_cast(uint16_t, hv);
+              bits[r] = __builtin_bit_cast(uint16_t, hv);
             } else {  // cross K: f16(acc * kscale); V: f16(acc + b)
               const _Float16 hv = part ? f16r(a + P.bias[n]) : f16r(a * P.kscale);
-              bits = __builtin_bit_cast(uint16_t, hv);
+              bits[r] = __builtin_bit_cast(uint16_t, hv);
             }
-            wl[transposed ? lc * 128 + lr : lr * 64 + lc] = bits;
+          }
+          const int lr0 = i * 16 + (lane >> 4) * 4;
+          if (transposed) {  // the lane's 4 consecutive t of column e = lc: one 8-B store
+            *reinterpret_cast<uint2*>(&wl[lc * 128 + (((lr0 >> 2) ^ swv(lc)) << 2)]) =
+                uint2{(uint32_t)bits[0] | ((uint32_t)bits[1] << 16),
+                      (uint32_t)bits[2] | ((uint32_t)bits[3] << 16)};
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              wl[(lr0 + r) * 64 + (((lc >> 3) ^ sw16(lr0 + r)) << 3) + (lc & 7)] = bits[r];
           }
         }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -618,7 +639,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
           const int row = it * 8 + (lane >> 3), ch = lane & 7;
           const int m = wr0 + row;
           if (m >= M) continue;
-          const uint4 v = *reinterpret_cast<const uint4*>(&wl[row * 64 + ch * 8]);
+          const uint4 v = *reinterpret_cast<const uint4*>(&wl[row * 64 + ((ch ^ sw16(row)) << 3)]);
           if constexpr (EPI == EPI_CROSS_KV) {
             if (P.ks8) {
               // MX-fp8 cross K/V cache: each (time, head) row of 64 f16
@@ -672,7 +693,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
           const int e = it * 2 + (lane >> 5), tg = lane & 31;
           const int m = wr0 + tg * 4;
           if (m >= M) continue;
-          const uint2 v = *reinterpret_cast<const uint2*>(&wl[e * 128 + tg * 4]);
+          const uint2 v = *reinterpret_cast<const uint2*>(&wl[e * 128 + ((tg ^ swv(e)) << 2)]);
           const int b = m / P.L, t = m - b * P.L;
           *reinterpret_cast<uint2*>(P.v + (((long)b * P.H + h) * 64 + e) * P.ldv + t) = v;
         }
@@ -706,7 +727,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
             for (int r = 0; r < 4; ++r) {
               const int lr = (i - hh * (GFM / 2)) * 16 + (lane >> 4) * 4 + r;
               const float a = acc[i][j][r] + bv;
-              wlf[lr * 64 + lc] = EPI == EPI_CONV2 ? gelu_ggml(a) : a;
+              wlf[lr * 64 + (((lc >> 2) ^ sw32(lr)) << 2) + (lc & 3)] = EPI == EPI_CONV2 ? gelu_ggml(a) : a;
             }
           }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -716,7 +737,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
           const int row = it * 4 + (lane >> 4), ch = lane & 15;
           const int m = wr0 + hh * 64 + row;
           if (m >= M) continue;
-          const f32x4 v = *reinterpret_cast<const f32x4*>(&wlf[row * 64 + ch * 4]);
+          const f32x4 v = *reinterpret_cast<const f32x4*>(&wlf[row * 64 + ((ch ^ sw32(row)) << 2)]);
           const long idx = (long)bz * P.c_bstride + (long)m * P.ldc + wc0 + ch * 4;
           f32x4 o;
           if constexpr (EPI == EPI_RES)

@@ -225,6 +225,8 @@ def lib() -> C.CDLL:
     L.mwx_test_set_dec_shared.restype = C.c_int
     L.mwx_test_set_dec_shared.argtypes = [C.c_int]
     L.mwx_test_set_gemm_8ph.restype = C.c_int
+    L.mwx_test_set_self_group.restype = C.c_int
+    L.mwx_test_set_self_group.argtypes = [C.c_int]
     L.mwx_test_set_gemm_8ph.argtypes = [C.c_int]
     L.mwx_test_set_ra_mismatch.restype = C.c_long
     L.mwx_test_set_ra_mismatch.argtypes = [C.c_long]
@@ -298,6 +300,13 @@ def set_gemm_8ph(on: Optional[bool]) -> int:
     """mwx_test_set_gemm_8ph: the encoder GEMM's 8-phase main loop (True) or
     the 2-stage ring (False); None: the MWX_GEMM_8PH default."""
     return lib().mwx_test_set_gemm_8ph(-1 if on is None else int(bool(on)))
+
+
+def set_self_group(on: Optional[bool]) -> int:
+    """mwx_test_set_self_group: beam / best-of self-attention one workgroup per
+    (group, head) (True) or per (row, head) (False); None: the MWX_SELF_GROUP
+    default."""
+    return lib().mwx_test_set_self_group(-1 if on is None else int(bool(on)))
 
 
 def set_ra_mismatch(step: Optional[int]) -> int:
