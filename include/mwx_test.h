@@ -116,11 +116,12 @@ int mwx_test_set_dec_shared(int on);
  * Returns the previous mode. */
 int mwx_test_set_gemm_8ph(int on);
 
-/* The decoder self-attention of beam / best-of groups as one workgroup per
- * (group, head) with the shared history loaded once (1, the default) or one
- * workgroup per (row, head) (0); -1: back to the MWX_SELF_GROUP environment
- * default. Returns the previous mode. */
-int mwx_test_set_self_group(int on);
+
+/* The MX-fp8 cross K/V cache's widening of e4m3 codes to f16 as the
+ * cross-attention kernels run it: n8 groups of 8 codes (codes[8 n8]), each
+ * group with one E8M0 exponent (e8[n8]); out[8 n8] = f16 bits. */
+int mwx_test_mx_widen(struct mwx_context* ctx, const uint8_t* codes, const uint8_t* e8, int n8,
+                      uint16_t* out);
 
 /* Fault injection of the run-ahead safety net: run-ahead step `step` of every
  * later attempt is treated as a device/host disagreement (-1: none; -2: back

@@ -415,6 +415,45 @@ static inline float dotf(const float* a, const float* b, int n) {
   return s;
 }
 
+// dotf of 2 input rows against 4 weight rows at once (8 independent
+// accumulator vectors instead of one dependent chain): every output is summed
+// exactly as dotf sums it (lane j of the 8-wide accumulator = acc[j], the
+// same pairwise tree, then the tail), so results are bit-identical to dotf
+typedef float v8f __attribute__((vector_size(32)));
+static inline v8f ld8f(const float* p) {
+  v8f v;
+  memcpy(&v, p, 32);
+  return v;
+}
+static inline float hsum8(v8f a) {
+  return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+}
+static void dot_2x4(const float* x0, const float* x1, const float* w0, int K, int ldw, float* y0,
+                    float* y1) {
+  v8f acc[2][4];
+  for (int r = 0; r < 2; ++r)
+    for (int j = 0; j < 4; ++j) acc[r][j] = v8f{0, 0, 0, 0, 0, 0, 0, 0};
+  int i = 0;
+  for (; i + 8 <= K; i += 8) {
+    const v8f a0 = ld8f(x0 + i), a1 = ld8f(x1 + i);
+    for (int j = 0; j < 4; ++j) {
+      const v8f b = ld8f(w0 + (size_t)j * ldw + i);
+      acc[0][j] += a0 * b;
+      acc[1][j] += a1 * b;
+    }
+  }
+  for (int j = 0; j < 4; ++j) {
+    const float* wj = w0 + (size_t)j * ldw;
+    float s0 = hsum8(acc[0][j]), s1 = hsum8(acc[1][j]);
+    for (int t = i; t < K; ++t) {
+      s0 += x0[t] * wj[t];
+      s1 += x1[t] * wj[t];
+    }
+    y0[j] = s0;
+    y1[j] = s1;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // MX-fp8 (engine compute mode MWX_COMPUTE_MXFP8; not a whisper.cpp mode):
 // every 32 consecutive k of a row share a power-of-two scale 2^E, E the
@@ -449,19 +488,50 @@ static void mx_round_rows(float* x, size_t rows, int K) {
 
 // y[M][N] = round_w(x)[M][K] . W[N][K]^T  (ggml_mul_mat, src0 = W); mx: the
 // rounded input is further MX-fp8 quantized (W was quantized at load)
-static void matmul(const Model& m, const float* W, const float* x, int M, int N,
-                   int K, float* y, bool mx = false) {
-  std::vector<float> xr((size_t)M * K);
-  for (size_t i = 0; i < xr.size(); ++i) xr[i] = m.rw(x[i]);
-  if (mx) mx_round_rows(xr.data(), M, K);
-#pragma omp parallel for schedule(static)
-  for (int n = 0; n < N; ++n) {
-    const float* wr = W + (size_t)n * K;
-    for (int r = 0; r < M; ++r) y[(size_t)r * N + n] = dotf(xr.data() + (size_t)r * K, wr, K);
+// y[r][n] = dotf(x[r], W[n]) for x [M][K], W [N][K]: blocks of NB weight rows
+// (L2-resident) against every input row, so the inputs stream once per block
+// instead of once per weight row, 2 x 4 outputs per register block; each
+// output is still exactly one dotf (same summation order)
+static void dot_rows(const float* x, int M, int K, const float* W, int N, float* y) {
+  constexpr int NB = 16;
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int n0 = 0; n0 < N; n0 += NB) {
+    const int n1 = std::min(N, n0 + NB);
+    int r = 0;
+    for (; r + 2 <= M; r += 2) {
+      const float* x0 = x + (size_t)r * K;
+      int n = n0;
+      for (; n + 4 <= n1; n += 4) {
+        float o0[4], o1[4];
+        dot_2x4(x0, x0 + K, W + (size_t)n * K, K, K, o0, o1);
+        for (int j = 0; j < 4; ++j) {
+          y[(size_t)r * N + n + j] = o0[j];
+          y[(size_t)(r + 1) * N + n + j] = o1[j];
+        }
+      }
+      for (; n < n1; ++n) {
+        y[(size_t)r * N + n] = dotf(x0, W + (size_t)n * K, K);
+        y[(size_t)(r + 1) * N + n] = dotf(x0 + K, W + (size_t)n * K, K);
+      }
+    }
+    for (; r < M; ++r) {
+      const float* x_r = x + (size_t)r * K;
+      for (int n = n0; n < n1; ++n) y[(size_t)r * N + n] = dotf(x_r, W + (size_t)n * K, K);
+    }
   }
 }
 
+static void matmul(const Model& m, const float* W, const float* x, int M, int N,
+                   int K, float* y, bool mx = false) {
+  std::vector<float> xr((size_t)M * K);
+#pragma omp parallel for schedule(static)
+  for (long i = 0; i < (long)xr.size(); ++i) xr[i] = m.rw(x[i]);
+  if (mx) mx_round_rows(xr.data(), M, K);
+  dot_rows(xr.data(), M, K, W, N, y);
+}
+
 static void add_bias(float* y, const float* b, int M, int N) {
+#pragma omp parallel for schedule(static)
   for (int r = 0; r < M; ++r)
     for (int n = 0; n < N; ++n) y[(size_t)r * N + n] += b[n];
 }
@@ -657,43 +727,50 @@ static void conv1d(const Model& m, const float* W /*[D][C][3]*/, const float* b,
         const float v = (ti >= 0 && ti < T) ? x[(size_t)c * T + ti] : 0.0f;
         col[((size_t)t * C + c) * 3 + k] = m.rw(v);
       }
+  dot_rows(col.data(), T_out, C * 3, W, D, y);
 #pragma omp parallel for schedule(static)
-  for (int d = 0; d < D; ++d) {
-    const float* wr = W + (size_t)d * C * 3;
-    for (int t = 0; t < T_out; ++t)
-      y[(size_t)t * D + d] = dotf(col.data() + (size_t)t * C * 3, wr, C * 3) + b[d];
-  }
+  for (int t = 0; t < T_out; ++t)
+    for (int d = 0; d < D; ++d) y[(size_t)t * D + d] += b[d];
 }
 
 // multi-head attention, one query block; Q[Lq][D], K[Lk][D], V[Lk][D] (f32);
 // scores scaled by `scale` inside softmax; causal: mask keys > q_pos0 + i.
+// khp / vtp (optional): K and V of every head already laid out as the loop
+// below builds them ([H][Lk][dh] and [H][dh][Lk], r16-rounded): the cross
+// K/V of a window, prepared once (cross_heads) instead of on every decode
 static void attention(const Model& m, const float* Q, const float* K, const float* V,
                       int Lq, int Lk, int D, int H, float scale, int causal_pos0,
-                      float* O) {
+                      float* O, const float* khp = nullptr, const float* vtp = nullptr) {
   const int dh = D / H;
 #pragma omp parallel
   {
-    std::vector<float> q(dh), w(Lk), kh((size_t)Lk * dh), vh((size_t)Lk * dh);
+    // vt: V of the head transposed [e][j] (the P.V sums read it contiguously,
+    // in the same order as before)
+    std::vector<float> q(dh), w(Lk), khb(khp ? 0 : (size_t)Lk * dh), vtb(vtp ? 0 : (size_t)dh * Lk);
 #pragma omp for schedule(static)
     for (int h = 0; h < H; ++h) {
-      for (int j = 0; j < Lk; ++j)
-        for (int e = 0; e < dh; ++e) {
-          kh[(size_t)j * dh + e] = m.r16(K[(size_t)j * D + h * dh + e]);
-          vh[(size_t)j * dh + e] = m.r16(V[(size_t)j * D + h * dh + e]);
-        }
+      const float* kh = khp ? khp + (size_t)h * Lk * dh : khb.data();
+      const float* vt = vtp ? vtp + (size_t)h * dh * Lk : vtb.data();
+      if (!khp)
+        for (int j = 0; j < Lk; ++j)
+          for (int e = 0; e < dh; ++e) khb[(size_t)j * dh + e] = m.r16(K[(size_t)j * D + h * dh + e]);
+      if (!vtp)
+        for (int j = 0; j < Lk; ++j)
+          for (int e = 0; e < dh; ++e) vtb[(size_t)e * Lk + j] = m.r16(V[(size_t)j * D + h * dh + e]);
       for (int i = 0; i < Lq; ++i) {
         for (int e = 0; e < dh; ++e) q[e] = m.r16(Q[(size_t)i * D + h * dh + e]);
         const int nk = causal_pos0 >= 0 ? std::min(Lk, causal_pos0 + i + 1) : Lk;
-        for (int j = 0; j < nk; ++j) w[j] = dotf(kh.data() + (size_t)j * dh, q.data(), dh);
+        for (int j = 0; j < nk; ++j) w[j] = dotf(kh + (size_t)j * dh, q.data(), dh);
         softmax(w.data(), nk, scale);
         for (int j = 0; j < nk; ++j) w[j] = m.r16(w[j]);
         for (int e = 0; e < dh; ++e) {
+          const float* ve = vt + (size_t)e * Lk;
           float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
           int j = 0;
           for (; j + 8 <= nk; j += 8)
-            for (int u = 0; u < 8; ++u) acc[u] += vh[(size_t)(j + u) * dh + e] * w[j + u];
+            for (int u = 0; u < 8; ++u) acc[u] += ve[j + u] * w[j + u];
           float s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
-          for (; j < nk; ++j) s += vh[(size_t)j * dh + e] * w[j];
+          for (; j < nk; ++j) s += ve[j] * w[j];
           O[(size_t)i * D + h * dh + e] = s;
         }
       }
@@ -737,7 +814,8 @@ static void encode_stem(const Model& m, const std::vector<float>& x, std::vector
   const int T = 2 * n_ctx;
   std::vector<float> h1((size_t)T * D), h2((size_t)n_ctx * D);
   conv1d(m, m.w("encoder.conv1.weight"), m.w("encoder.conv1.bias"), x.data(), m.n_mels, T, D, 1, h1.data());
-  for (auto& v : h1) v = gelu(m, v);
+#pragma omp parallel for schedule(static)
+  for (long i = 0; i < (long)h1.size(); ++i) h1[i] = gelu(m, h1[i]);
   // conv2 consumes channel-major input
   std::vector<float> h1c((size_t)D * T);
   for (int t = 0; t < T; ++t)
@@ -745,7 +823,8 @@ static void encode_stem(const Model& m, const std::vector<float>& x, std::vector
   conv1d(m, m.w("encoder.conv2.weight"), m.w("encoder.conv2.bias"), h1c.data(), D, T, D, 2, h2.data());
   const float* pe = m.w("encoder.positional_embedding");
   inp.resize((size_t)n_ctx * D);
-  for (size_t i = 0; i < inp.size(); ++i) inp[i] = pe[i] + gelu(m, h2[i]);
+#pragma omp parallel for schedule(static)
+  for (long i = 0; i < (long)inp.size(); ++i) inp[i] = pe[i] + gelu(m, h2[i]);
 }
 
 // Test hook of one encoder layer (orc_encode_layer): ext[g] non-null takes
@@ -785,7 +864,8 @@ static void encode_layer(const Model& m, int il, std::vector<float>& inp, const 
   operand(2, cur);
   matmul(m, m.w(p + ".mlp.0.weight"), cur.data(), M, 4 * D, D, ff.data(), mx);
   add_bias(ff.data(), m.w(p + ".mlp.0.bias"), M, 4 * D);
-  for (auto& e : ff) e = gelu(m, e);
+#pragma omp parallel for schedule(static)
+  for (long i = 0; i < (long)ff.size(); ++i) ff[i] = gelu(m, ff[i]);
   operand(3, ff);
   matmul(m, m.w(p + ".mlp.2.weight"), ff.data(), M, D, 4 * D, cur.data(), mx);
   add_bias(cur.data(), m.w(p + ".mlp.2.bias"), M, D);
@@ -820,7 +900,29 @@ static void encode(const Model& m, const Mel& mel, int seek, std::vector<float>&
 // kv_cross: per decoder layer K = f16(Kscale * Wk enc), V = f16(Wv enc + b)
 struct Cross {
   std::vector<float> k, v;  // [n_layer][n_ctx][D]
+  // per head, as attention() lays them out: kh [n_layer][H][n_ctx][dh],
+  // vt [n_layer][H][dh][n_ctx] (cross_heads)
+  std::vector<float> kh, vt;
 };
+static void cross_heads(const Model& m, Cross& c) {
+  const int M = m.n_audio_ctx, D = m.n_text_state, L = m.n_text_layer, H = m.n_text_head;
+  const int dh = D / H;
+  c.kh.resize(c.k.size());
+  c.vt.resize(c.v.size());
+#pragma omp parallel for schedule(static)
+  for (int lh = 0; lh < L * H; ++lh) {
+    const int il = lh / H, h = lh % H;
+    const float* K = c.k.data() + (size_t)il * M * D;
+    const float* V = c.v.data() + (size_t)il * M * D;
+    float* kh = c.kh.data() + (size_t)lh * M * dh;
+    float* vt = c.vt.data() + (size_t)lh * dh * M;
+    for (int j = 0; j < M; ++j)
+      for (int e = 0; e < dh; ++e) {
+        kh[(size_t)j * dh + e] = m.r16(K[(size_t)j * D + h * dh + e]);
+        vt[(size_t)e * M + j] = m.r16(V[(size_t)j * D + h * dh + e]);
+      }
+  }
+}
 static ResultCache<Cross> g_cross_cache{2, {}};
 static void cross(const Model& m, const std::vector<float>& enc, Cross& c) {
   const std::string ckey = m.key + "|cross|" + std::to_string(fnv1a(enc.data(), enc.size() * sizeof(float)));
@@ -857,14 +959,17 @@ static void cross(const Model& m, const std::vector<float>& enc, Cross& c) {
       mx_round_rows(c.v.data() + (size_t)il * M * D, M, D);
     }
   }
+  cross_heads(m, c);
 }
 
 // ---------------------------------------------------------------------------
 // decoder with KV cache (whisper_build_graph_decoder, non-flash path)
 // ---------------------------------------------------------------------------
 struct KV {
-  std::vector<float> k, v;  // [n_layer][n_text_ctx][D] (f16-rounded values)
-  int n = 0;                // tokens stored
+  // per layer [n][D] (f16-rounded values), grown as tokens are decoded (a
+  // beam hand-over copies what is stored, not n_text_ctx rows)
+  std::vector<std::vector<float>> k, v;
+  int n = 0;  // tokens stored
 };
 
 // Decodes `n_tok` tokens at positions n_past.. and returns logits of every
@@ -876,9 +981,10 @@ static void decode(const Model& m, const Cross& cr, KV& kv, const int* tokens, i
   const int dh = D / H;
   const float KQscale = powf((float)dh, -0.25f);
   if (kv.k.empty()) {
-    kv.k.assign((size_t)L * n_ctx * D, 0.0f);
-    kv.v.assign((size_t)L * n_ctx * D, 0.0f);
+    kv.k.resize(L);
+    kv.v.resize(L);
   }
+  (void)n_ctx;
   const int M = n_tok;
   const float* te = m.w("decoder.token_embedding.weight");
   const float* pe = m.w("decoder.positional_embedding");
@@ -897,8 +1003,10 @@ static void decode(const Model& m, const Cross& cr, KV& kv, const int* tokens, i
     for (auto& e : k) e *= KQscale;
     matmul(m, m.w(p + ".attn.value.weight"), cur.data(), M, D, D, v.data());
     add_bias(v.data(), m.w(p + ".attn.value.bias"), M, D);
-    float* kc = kv.k.data() + (size_t)il * n_ctx * D;
-    float* vc = kv.v.data() + (size_t)il * n_ctx * D;
+    kv.k[il].resize((size_t)(n_past + M) * D);
+    kv.v[il].resize((size_t)(n_past + M) * D);
+    float* kc = kv.k[il].data();
+    float* vc = kv.v[il].data();
     for (int i = 0; i < M; ++i)
       for (int d = 0; d < D; ++d) {
         kc[(size_t)(n_past + i) * D + d] = m.r16(k[(size_t)i * D + d]);
@@ -913,7 +1021,9 @@ static void decode(const Model& m, const Cross& cr, KV& kv, const int* tokens, i
     matmul(m, m.w(p + ".cross_attn.query.weight"), cur.data(), M, D, D, q.data());
     add_bias(q.data(), m.w(p + ".cross_attn.query.bias"), M, D);
     attention(m, q.data(), cr.k.data() + (size_t)il * n_actx * D, cr.v.data() + (size_t)il * n_actx * D,
-              M, n_actx, D, H, KQscale, -1, o.data());
+              M, n_actx, D, H, KQscale, -1, o.data(),
+              cr.kh.empty() ? nullptr : cr.kh.data() + (size_t)il * n_actx * D,
+              cr.vt.empty() ? nullptr : cr.vt.data() + (size_t)il * n_actx * D);
     matmul(m, m.w(p + ".cross_attn.out.weight"), o.data(), M, D, D, cur.data());
     add_bias(cur.data(), m.w(p + ".cross_attn.out.bias"), M, D);
     for (size_t i = 0; i < inp.size(); ++i) inp[i] = cur[i] + inp[i];
@@ -921,7 +1031,8 @@ static void decode(const Model& m, const Cross& cr, KV& kv, const int* tokens, i
     layer_norm(inp.data(), m.w(p + ".mlp_ln.weight"), m.w(p + ".mlp_ln.bias"), M, D, cur.data());
     matmul(m, m.w(p + ".mlp.0.weight"), cur.data(), M, 4 * D, D, ff.data());
     add_bias(ff.data(), m.w(p + ".mlp.0.bias"), M, 4 * D);
-    for (auto& e : ff) e = gelu(m, e);
+#pragma omp parallel for schedule(static)
+    for (long i = 0; i < (long)ff.size(); ++i) ff[i] = gelu(m, ff[i]);
     matmul(m, m.w(p + ".mlp.2.weight"), ff.data(), M, D, 4 * D, cur.data());
     add_bias(cur.data(), m.w(p + ".mlp.2.bias"), M, D);
     for (size_t i = 0; i < inp.size(); ++i) inp[i] = cur[i] + inp[i];
@@ -2224,6 +2335,7 @@ void orc_decode_seq(void* h, const float* k_cross, const float* v_cross, const i
   const size_t sz = (size_t)m->n_text_layer * m->n_audio_ctx * m->n_text_state;
   c.k.assign(k_cross, k_cross + sz);
   c.v.assign(v_cross, v_cross + sz);
+  cross_heads(*m, c);
   KV kv;
   std::vector<float> lg;
   for (int i = 0; i < n; ++i) {

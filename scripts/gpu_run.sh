@@ -81,7 +81,7 @@ for s in "$@"; do
     fdl) run fdl 600 python -u -m pytest tests/test_gpu_fulldepth.py -k "language_auto" -m gpu -v -s -rf --timeout 500 --timeout-method thread ;;
     beamorcr) run beamorcr 600 python -u -m pytest tests/test_gpu_beam_oracle.py -k "not full_depth" -m gpu -v -s -rf --timeout 500 --timeout-method thread ;;
     beamorcf) run beamorcf 1000 python -u -m pytest tests/test_gpu_beam_oracle.py -k "full_depth" -m gpu -v -s -rf --durations=0 --timeout 900 --timeout-method thread ;;
-    newtests) run newtests 600 python -u -m pytest tests/test_gpu_parity.py -k "extreme_scales or 8phase or runahead_mismatch" -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
+    newtests) run newtests 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shapes.py -k "extreme_scales or widening or runahead_mismatch or grouped_self or beam_search" -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
     pmcbs)  # beam 5 bf16 at the benched 220 steps: FETCH and LDS / MFMA passes (the self-attention's history reads)
       for x in "fetch:FETCH_SIZE" "lds:SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE"; do
         n=${x%%:*}; c=${x#*:}

@@ -662,229 +662,6 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(
   span_end(span);
 }
 
-// Self-attention of the NQ decoders of one clip (beam search / best-of
-// groups: rows g*NQ .. g*NQ+NQ-1) in one workgroup per (group, head). The
-// decoders' histories are mostly one history: beam hand-overs point their
-// position maps (kvmap) at the rows that wrote each position, so for every
-// position shared by the group's common ancestry all NQ rows resolve to the
-// SAME cache row. That row is loaded once (decoder 0's load) and scored
-// against every decoder's query; a decoder whose map resolves a position to
-// another row loads it itself (the divergent tail; exec-masked, skipped when
-// no lane needs it). Each decoder's arithmetic is exactly that of
-// dec_attn_kernel<T, true, 4> for its row (same key -> lane mapping, dot8 /
-// dpp_sum8 scores, LDS softmax with the same block reductions, P.V pair order
-// and cross-wave sum), so results do not depend on the grouping and equal a
-// row decoded alone (mwx_test_decode_last). Active decoders of a group are at
-// the same position (they step together); inactive ones are skipped.
-constexpr int SELF_MAX_KEYS = 448;  // n_text_ctx of every Whisper model
-template <typename T, int NQ>
-__global__ __launch_bounds__(256) void dec_sattn_group_kernel(
-    const float* __restrict__ P, int KS, int pcols, const float* __restrict__ bias, float qscale,
-    float kscale, _Float16* __restrict__ kbase, _Float16* __restrict__ vbase,
-    const int* __restrict__ kv_index, const int* __restrict__ pos, const int* __restrict__ active,
-    int cap, T* __restrict__ o, int H, float scale, const int* __restrict__ kvmap,
-    const int* __restrict__ own_from, int map_row0, int R, int write_new,
-    unsigned long long* span) {
-  constexpr int UB = 4, BR = 32 * UB;
-  __shared__ float sc[NQ][SELF_MAX_KEYS];
-  __shared__ float redf[4];
-  __shared__ double redd[4];
-  __shared__ float pv[4][64][9];
-  __shared__ float sq[NQ][64], snk[NQ][64], snv[NQ][64];
-  span_start(span);
-  const int g = blockIdx.x / H, h = blockIdx.x - (blockIdx.x / H) * H;
-  const int row0 = g * NQ;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int kg = lane >> 3, c = lane & 7;
-  // control words of the group's rows (one round trip)
-  int act[NQ], prow[NQ], slot[NQ], own0[NQ];
-#pragma unroll
-  for (int b = 0; b < NQ; ++b) {
-    const int row = row0 + b;
-    act[b] = active[row];
-    prow[b] = pos[row];
-    slot[b] = kv_index ? kv_index[row] : row;
-    own0[b] = own_from ? own_from[row] : 0;
-  }
-  int lead = -1;  // the first active decoder: the others' shared loads are its loads
-#pragma unroll
-  for (int b = NQ - 1; b >= 0; --b)
-    if (act[b]) lead = b;
-  if (lead < 0) {
-    span_end(span);
-    return;
-  }
-  const int n = prow[lead] + 1;
-  const int jnew = n - 1;
-  const int jmax = max(n - 2, 0);
-  const int D = H * 64;
-  const long rstride = (long)H * cap * 64;
-  _Float16* Kh = kbase + (long)h * cap * 64;  // row r's cache: Kh + r * rstride
-  _Float16* Vh = vbase + (long)h * cap * 64;
-  // the cache row holding position j for decoder b (j <= jmax)
-  auto src_row = [&](int b, int j) {
-    return (kvmap && j < own0[b]) ? kvmap[(long)(row0 + b) * cap + j] - map_row0 : slot[b];
-  };
-  // projections of this head for every decoder from the split-K slabs
-  const long pstride = (long)R * pcols;
-  const bool red = tid < 192;
-  const int part = tid >> 6, e = tid & 63;
-  const int col = part * D + h * 64 + e;
-  if (red) {
-    const float bcol = part != 1 ? bias[col] : 0.0f;
-#pragma unroll
-    for (int b = 0; b < NQ; ++b) {
-      if (!act[b]) continue;
-      const float* pp = P + (long)(row0 + b) * pcols + col;
-      float pk[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) pk[k] = pp[min(k, KS - 1) * pstride];
-      float acc = pk[0];
-#pragma unroll
-      for (int k = 1; k < 8; ++k) acc += k < KS ? pk[k] : 0.0f;
-      if (part == 0) {
-        sq[b][e] = (float)f16r((acc + bcol) * qscale);
-      } else if (part == 1) {
-        const _Float16 kv = f16r(acc * kscale);
-        snk[b][e] = (float)kv;
-        if (write_new) Kh[slot[b] * rstride + (long)prow[b] * 64 + e] = kv;
-      } else {
-        const _Float16 vv = f16r(acc + bcol);
-        snv[b][e] = (float)vv;
-        if (write_new) Vh[slot[b] * rstride + (long)prow[b] * 64 + e] = vv;
-      }
-    }
-  }
-  __syncthreads();
-  h2 qh[NQ][4];
-  f16x8 nkh[NQ], nvh[NQ];
-#pragma unroll
-  for (int b = 0; b < NQ; ++b) {
-#pragma unroll
-    for (int x = 0; x < 8; ++x) {
-      nkh[b][x] = (_Float16)snk[b][c * 8 + x];
-      nvh[b][x] = (_Float16)snv[b][c * 8 + x];
-    }
-#pragma unroll
-    for (int x = 0; x < 4; ++x)
-      qh[b][x] = h2{(_Float16)sq[b][c * 8 + 2 * x], (_Float16)sq[b][c * 8 + 2 * x + 1]};
-  }
-  const int nb = (n + BR - 1) / BR;
-  const bool wave_busy = wid * (8 * UB) < n;
-  // one batch of rows (this lane's UB positions) of K or V: the lead's rows,
-  // and per other decoder the rows its map resolves elsewhere
-  auto load_rows = [&](const _Float16* base, int bidx, f16x8 (&lb)[UB], int (&srow)[NQ][UB]) {
-#pragma unroll
-    for (int u = 0; u < UB; ++u) {
-      const int j = min(bidx * BR + wid * (8 * UB) + u * 8 + kg, jmax);
-#pragma unroll
-      for (int b = 0; b < NQ; ++b) srow[b][u] = src_row(b, j);
-      lb[u] = *reinterpret_cast<const f16x8*>(base + srow[lead][u] * rstride + (long)j * 64 + c * 8);
-    }
-  };
-  auto row_of = [&](const _Float16* base, int bidx, int b, int u, const f16x8& shared,
-                    int (&srow)[NQ][UB]) -> f16x8 {
-    f16x8 r = shared;
-    if (srow[b][u] != srow[lead][u]) {
-      const int j = min(bidx * BR + wid * (8 * UB) + u * 8 + kg, jmax);
-      r = *reinterpret_cast<const f16x8*>(base + srow[b][u] * rstride + (long)j * 64 + c * 8);
-    }
-    return r;
-  };
-  f16x8 kb[UB];
-  int srow[NQ][UB];
-  for (int bi = 0; wave_busy && bi < nb; ++bi) {
-    load_rows(Kh, bi, kb, srow);
-#pragma unroll
-    for (int b = 0; b < NQ; ++b) {
-      if (!act[b]) continue;
-#pragma unroll
-      for (int u = 0; u < UB; ++u) {
-        const int j = bi * BR + wid * (8 * UB) + u * 8 + kg;
-        const bool isnew = min(j, n - 1) == jnew;
-        const f16x8 kk = row_of(Kh, bi, b, u, kb[u], srow);
-        float d = dot8(qh[b], isnew ? nkh[b] : kk);
-        d = dpp_sum8(d);
-        if (c == 0 && j < n) sc[b][j] = d * scale;
-      }
-    }
-  }
-  // softmax per decoder (ggml order, as dec_attn_kernel's LDS path)
-#pragma unroll
-  for (int b = 0; b < NQ; ++b) {
-    if (!act[b]) continue;
-    __syncthreads();
-    float mx = -INFINITY;
-    for (int j = tid; j < n; j += 256) mx = fmaxf(mx, sc[b][j]);
-    mx = block_max_256(mx, redf);
-    double sum = 0.0;
-    for (int j = tid; j < n; j += 256) {
-      const float ex = expf(sc[b][j] - mx);
-      sc[b][j] = ex;
-      sum += (double)ex;
-    }
-    sum = block_sum_256d(sum, redd);
-    const float inv = (float)(1.0 / sum);
-    for (int j = tid; j < n; j += 256) sc[b][j] = (float)f16r(sc[b][j] * inv);
-  }
-  __syncthreads();
-  float acc[NQ][8];
-#pragma unroll
-  for (int b = 0; b < NQ; ++b)
-#pragma unroll
-    for (int x = 0; x < 8; ++x) acc[b][x] = 0.0f;
-  for (int bi = 0; wave_busy && bi < nb; ++bi) {
-    load_rows(Vh, bi, kb, srow);
-#pragma unroll
-    for (int b = 0; b < NQ; ++b) {
-      if (!act[b]) continue;
-#pragma unroll
-      for (int u = 0; u < UB; u += 2) {
-        const int j0 = bi * BR + wid * (8 * UB) + u * 8 + kg;
-        h2 ph;
-        f16x8 r[2];
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const int j = j0 + 8 * t;
-          float p = sc[b][min(j, n - 1)];
-          if (j >= n) p = 0.0f;
-          ph[t] = (_Float16)p;
-          const bool isnew = min(j, n - 1) == jnew;
-          const f16x8 vv = row_of(Vh, bi, b, u + t, kb[u + t], srow);
-          r[t] = isnew ? nvh[b] : vv;
-        }
-#pragma unroll
-        for (int x = 0; x < 8; ++x)
-          acc[b][x] = __builtin_amdgcn_fdot2(ph, h2{r[0][x], r[1][x]}, acc[b][x], false);
-      }
-    }
-  }
-#pragma unroll
-  for (int b = 0; b < NQ; ++b) {
-    if (!act[b]) continue;
-#pragma unroll
-    for (int x = 0; x < 8; ++x) {
-      float a = acc[b][x];
-      a = add_xor8(a);
-      a = add_xor16(a);
-      a = add_xor32(a);
-      acc[b][x] = a;
-    }
-    __syncthreads();
-    if (kg == 0) {
-#pragma unroll
-      for (int x = 0; x < 8; ++x) pv[wid][c][x] = acc[b][x];
-    }
-    __syncthreads();
-    if (tid < 64) {
-      const int cc = tid >> 3, x = tid & 7;
-      const float r = (pv[0][cc][x] + pv[1][cc][x]) + (pv[2][cc][x] + pv[3][cc][x]);
-      o[pack_index(row0 + b, h * 64 + cc * 8 + x, D)] = to_t<T>(r);
-    }
-  }
-  span_end(span);
-}
-
 // Cross-attention of NQ rows that share one clip's cross K/V (the decoders
 // of a beam search / best-of group: rows g*NQ .. g*NQ+NQ-1): one workgroup per
 // (group, head) streams the clip's K and V once for all NQ queries instead of
@@ -896,8 +673,9 @@ __global__ __launch_bounds__(256) void dec_sattn_group_kernel(
 // the bytes of the f16 cache. A lane's 8 codes lie in one half, so they are
 // widened to f16 with that half's scale (v_cvt_scalef32_pk_f16_fp8: exact
 // while code x scale is f16-representable — the cache's values are f16 values
-// MX-rounded, so they are; a block scale outside f16's range would saturate
-// or flush) and every score / P.V operation then runs
+// MX-rounded, so they are; measured: f16 RNE including subnormals, +-inf
+// past f16's range, test_mx_cache_widening_pinned) and every score / P.V
+// operation then runs
 // on f16 exactly as for the f16 cache. Each lane loads the scale pair of one
 // of its wave's 64 rows per batch; the pair a row needs is read from the lane
 // that loaded it (__shfl).
@@ -911,6 +689,17 @@ __device__ __forceinline__ f16x8 dequant_h8(uint2 raw, uint32_t e) {
   const h2 c = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(raw.y, sc, false);
   const h2 d = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(raw.y, sc, true);
   return f16x8{a[0], a[1], b[0], b[1], c[0], c[1], d[0], d[1]};
+}
+
+// test hook (mwx_test_mx_widen): dequant_h8 itself on 8 codes per thread
+__global__ void mx_widen_test_kernel(const uint2* __restrict__ codes, const uint8_t* __restrict__ e8,
+                                     int n8, f16x8* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n8) out[i] = dequant_h8(codes[i], e8[i]);
+}
+void mx_widen_test(const uint8_t* codes, const uint8_t* e8, int n8, uint16_t* out, hipStream_t st) {
+  mx_widen_test_kernel<<<(n8 + 255) / 256, 256, 0, st>>>(reinterpret_cast<const uint2*>(codes), e8,
+                                                         n8, reinterpret_cast<f16x8*>(out));
 }
 
 // MFS (MX-fp8 cache only, MWX_XATTN_MFS): scores and P.V on MFMA instead of
@@ -1538,22 +1327,6 @@ template void kv_append<_Float16>(const float*, int, int, const float*, float, _
 template void kv_append<__bf16>(const float*, int, int, const float*, float, _Float16*, _Float16*,
                                 const int*, const int*, const int*, int, int, int, hipStream_t);
 
-// the grouped self-attention on / off (MWX_SELF_GROUP=0 at start-up, or
-// self_group_set from a test)
-static std::atomic<int>& self_group_mode() {
-  static std::atomic<int> m{-1};
-  return m;
-}
-static bool self_group() {
-  int v = self_group_mode().load();
-  if (v < 0) {
-    v = (getenv("MWX_SELF_GROUP") && atoi(getenv("MWX_SELF_GROUP")) == 0) ? 0 : 1;
-    self_group_mode().store(v);
-  }
-  return v != 0;
-}
-int self_group_set(int on) { return self_group_mode().exchange(on < 0 ? -1 : (on ? 1 : 0)); }
-
 template <typename T>
 void dec_attention(const float* P, int KS, int pcols, const float* bias, float qscale,
                    float kscale, _Float16* kbase, _Float16* vbase, const int* kv_index,
@@ -1582,28 +1355,6 @@ void dec_attention(const float* P, int KS, int pcols, const float* bias, float q
   // MWX_XATTN_NBC=0: the runtime-batch-count cross kernel (A/B of the
   // constant-count load stream)
   static const bool xattn_nbc = !(getenv("MWX_XATTN_NBC") && atoi(getenv("MWX_XATTN_NBC")) == 0);
-  // beam / best-of groups (nq = 2..8 decoders per clip, not the prefill):
-  // one workgroup per (group, head) with the shared history loaded once
-  // (MWX_SELF_GROUP=0: the per-row kernel, for the A/B)
-  if (fixed_len == 0 && self_ub4 && self_group() && nq >= 2 && nq <= 8 && kv_len_cap <= SELF_MAX_KEYS) {
-    const dim3 gg((R / nq) * H);
-#define SGL(NQV)                                                                                  \
-  dec_sattn_group_kernel<T, NQV><<<gg, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale, kbase,   \
-                                                     vbase, kv_index, pos, active, kv_len_cap, o, \
-                                                     H, scale, kvmap, own_from, map_row0, R,      \
-                                                     write_new, span)
-    switch (nq) {
-      case 2: SGL(2); break;
-      case 3: SGL(3); break;
-      case 4: SGL(4); break;
-      case 5: SGL(5); break;
-      case 6: SGL(6); break;
-      case 7: SGL(7); break;
-      default: SGL(8); break;
-    }
-#undef SGL
-    return;
-  }
   if (fixed_len == 0 && self_ub4)
     dec_attn_kernel<T, true, 4><<<g, 256, 0, st>>>(P, KS, pcols, bias, qscale, kscale, kbase,
                                                    vbase, kv_index, pos, active, fixed_len,

@@ -235,8 +235,8 @@ int xattn_mfs_set(int on);
 int dec_shared_set(int on);
 // the encoder GEMM's 8-phase main loop on / off (-1: back to MWX_GEMM_8PH)
 int gemm_8ph_set(int on);
-// the grouped beam / best-of self-attention on / off (-1: back to MWX_SELF_GROUP)
-int self_group_set(int on);
+// test hook: the MX-fp8 cache's code widening (8 codes per E8M0 exponent) to f16 bits
+void mx_widen_test(const uint8_t* codes, const uint8_t* e8, int n8, uint16_t* out, hipStream_t st);
 template <typename T>
 bool dec_cross_attention_grouped(const float* P, int KS, int pcols, const float* bias,
                                  const void* kbase, const void* vbase, const int* kv_index,

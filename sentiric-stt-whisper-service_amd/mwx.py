@@ -225,8 +225,8 @@ def lib() -> C.CDLL:
     L.mwx_test_set_dec_shared.restype = C.c_int
     L.mwx_test_set_dec_shared.argtypes = [C.c_int]
     L.mwx_test_set_gemm_8ph.restype = C.c_int
-    L.mwx_test_set_self_group.restype = C.c_int
-    L.mwx_test_set_self_group.argtypes = [C.c_int]
+    L.mwx_test_mx_widen.restype = C.c_int
+    L.mwx_test_mx_widen.argtypes = [P, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
     L.mwx_test_set_gemm_8ph.argtypes = [C.c_int]
     L.mwx_test_set_ra_mismatch.restype = C.c_long
     L.mwx_test_set_ra_mismatch.argtypes = [C.c_long]
@@ -300,13 +300,6 @@ def set_gemm_8ph(on: Optional[bool]) -> int:
     """mwx_test_set_gemm_8ph: the encoder GEMM's 8-phase main loop (True) or
     the 2-stage ring (False); None: the MWX_GEMM_8PH default."""
     return lib().mwx_test_set_gemm_8ph(-1 if on is None else int(bool(on)))
-
-
-def set_self_group(on: Optional[bool]) -> int:
-    """mwx_test_set_self_group: beam / best-of self-attention one workgroup per
-    (group, head) (True) or per (row, head) (False); None: the MWX_SELF_GROUP
-    default."""
-    return lib().mwx_test_set_self_group(-1 if on is None else int(bool(on)))
 
 
 def set_ra_mismatch(step: Optional[int]) -> int:
@@ -676,6 +669,19 @@ class Context:
     def runahead_fallbacks(self, state_index: int = 0, reset: bool = True) -> int:
         """Run-ahead attempts redone on the host loop (mwx_test_runahead_fallbacks)."""
         return lib().mwx_test_runahead_fallbacks(self.state(state_index), 1 if reset else 0)
+
+    def test_mx_widen(self, codes: np.ndarray, e8: np.ndarray) -> np.ndarray:
+        """mwx_test_mx_widen: e4m3 codes (uint8, groups of 8) widened to f16
+        with one E8M0 exponent per group, as the cross-attention kernels do."""
+        codes = np.ascontiguousarray(codes, np.uint8)
+        e8 = np.ascontiguousarray(e8, np.uint8)
+        assert codes.size == 8 * e8.size
+        out = np.empty(codes.size, np.uint16)
+        r = lib().mwx_test_mx_widen(self.ctx, codes.ctypes.data, e8.ctypes.data, e8.size,
+                                    out.ctypes.data)
+        if r != 0:
+            raise RuntimeError(f"mwx_test_mx_widen returned {r}")
+        return out.view(np.float16)
 
     def test_xattn_mx(self, q: np.ndarray, k8: np.ndarray, ks: np.ndarray, v8: np.ndarray,
                       vs: np.ndarray, nq: int) -> np.ndarray:

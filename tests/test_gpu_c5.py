@@ -136,14 +136,15 @@ def _mx_round(a):
     oracle's activation quantization): a power-of-two scale per block, the
     smallest 2^E with max |x| <= 448 * 2^E, and e4m3 round-to-nearest-even
     of x / 2^E (3 mantissa bits; subnormal step 2^-9); returns the rounded
-    values (float64)."""
-    h = a.reshape(-1, 32).astype(np.float64)
+    values (float32: every step is exact there for activation magnitudes)."""
+    h = np.ascontiguousarray(a, dtype=np.float32).reshape(-1, 32)
     amax = np.abs(h).max(axis=1, keepdims=True)
-    E = np.ceil(np.log2(np.maximum(amax, 1e-30) / 448.0))
-    x = h / np.exp2(E)
+    E = np.ceil(np.log2(np.maximum(amax, np.float32(1e-30)) / np.float32(448.0)))
+    s = np.exp2(E).astype(np.float32)
+    x = h / s
     _, ex = np.frexp(x)  # |x| = m 2^ex, m in [0.5, 1): floor(log2 |x|) = ex - 1
-    ulp = np.exp2(np.maximum(ex - 1, -6) - 3)
-    return (np.rint(x / ulp) * ulp * np.exp2(E)).reshape(a.shape)
+    ulp = np.exp2(np.maximum(ex - 1, -6) - 3).astype(np.float32)
+    return (np.rint(x / ulp) * ulp * s).reshape(a.shape)
 
 
 def test_mxfp8_encoder_per_layer_error_and_flips(v3path):

@@ -932,14 +932,48 @@ def test_mx_cross_attention_kernel_vs_f64(micro, sharp):
 
 
 
+def test_mx_cache_widening_pinned(micro):
+    """The MX-fp8 cross K/V cache's widening to f16 (v_cvt_scalef32_pk_f16_fp8,
+    both cross-attention paths) for every finite e4m3 code under E8M0
+    exponents 2^-37 .. 2^13: equal to code x 2^E rounded to f16 with
+    round-to-nearest-even wherever that is within f16's range (normal or
+    subnormal, flushed nowhere: r06c measured 12630 values, 5678 of them
+    subnormal, 2942 rounding to 0), and +-inf beyond it (no saturation). Pins
+    what 'exact while code x scale is f16-representable' means."""
+    ctx, _, _ = micro
+    codes = np.array([c for c in range(256) if (c & 0x7F) != 0x7F], np.uint8)  # finite codes
+    vals = _e4m3_decode(codes.astype(np.int64))
+    exps = np.arange(127 - 37, 127 + 14)
+    n = len(codes)
+    pad = (-n) % 8
+    cg = np.concatenate([codes, np.zeros(pad, np.uint8)])
+    allc = np.tile(cg, len(exps))
+    alle = np.repeat(exps.astype(np.uint8), len(cg) // 8)
+    dev = ctx.test_mx_widen(allc, alle).astype(np.float64).reshape(len(exps), -1)[:, :n]
+    want = (vals[None, :] * np.exp2(exps[:, None] - 127.0))
+    rne = want.astype(np.float16).astype(np.float64)
+    ok = np.abs(want) <= 65504.0
+    assert np.array_equal(dev[ok], rne[ok]), np.argwhere((dev != rne) & ok)[:8]
+    sub = ok & (np.abs(want) < 2.0 ** -14) & (want != 0)
+    big = ~ok
+    assert np.all(np.isinf(dev[big])) and np.array_equal(np.sign(dev[big]), np.sign(want[big]))
+    print(f"MX widening: {int(ok.sum())} representable values equal to f16 RNE "
+          f"({int(sub.sum())} of them f16 subnormals, {int((sub & (rne == 0)).sum())} rounding to 0); "
+          f"beyond f16's range: {sorted(set(np.abs(dev[big]).tolist()))[:4]}")
+
+
 def test_mx_cross_attention_kernel_extreme_scales(micro):
     """Block scales at the edge of f16's range: V rows whose
-    code x scale values fall into f16's subnormal range (scales 2^-30 ..
-    2^-22). Both kernel paths widen the codes to f16 before the arithmetic,
-    so the pinned behaviour is attention over the f16-ROUNDED dequantized
-    values (subnormals kept, not flushed): within 3e-3 of max |o| per row of
-    float64 attention over np.float16(values), for the MFMA and the v_dot2
-    path alike; the distance to the unrounded values is printed."""
+    code x scale values fall into f16's subnormal range (row magnitudes
+    2^-22 .. 2^-14). Both kernel paths widen the codes to f16 before the
+    arithmetic, so the pinned behaviour is attention over the f16-ROUNDED
+    dequantized values with f16 subnormals kept (a flush to zero would lose
+    whole rows): for the MFMA and the v_dot2 path alike, max |o - o64| per row
+    within one f16 subnormal step (2^-24, the output is f16 here and lies in
+    that range itself) + 3e-3 x max |o64|, o64 = float64 attention over
+    np.float16(values); the distance to the unrounded values is printed.
+    (Measured first at a relative bound alone: 1.3e-2, the output's own f16
+    subnormal rounding.)"""
     ctx, _, _ = micro
     rng = np.random.default_rng(11)
     H, n, nq, G = 2, 1500, 5, 2
@@ -968,15 +1002,15 @@ def test_mx_cross_attention_kernel_extreme_scales(micro):
         for mfs in (True, False):
             mwx.set_xattn_mfs(mfs)
             o = ctx.test_xattn_mx(q, k8, ks, v8, vs, nq)
-            scale_r = np.abs(ref).max(axis=1, keepdims=True)
-            errs[mfs] = float((np.abs(o - ref) / scale_r).max())
-            exact[mfs] = float((np.abs(o - ref_exact) / scale_r).max())
+            bound = 2.0 ** -24 + 3e-3 * np.abs(ref).max(axis=1, keepdims=True)
+            errs[mfs] = float((np.abs(o - ref) / bound).max())
+            exact[mfs] = float((np.abs(o - ref_exact) / bound).max())
     finally:
         mwx.set_xattn_mfs(None if prev < 0 else bool(prev))
-    print(f"MX cross-attention, V in f16's subnormal range: vs f16-rounded values MFMA "
-          f"{errs[True]:.2e} / v_dot2 {errs[False]:.2e}; vs unrounded MFMA {exact[True]:.2e} / "
-          f"v_dot2 {exact[False]:.2e} (of max |o| per row)")
-    assert errs[True] <= 3e-3 and errs[False] <= 3e-3, (errs, exact)
+    print(f"MX cross-attention, V in f16's subnormal range: max |o - o64| / (2^-24 + 3e-3 max|o64|) "
+          f"vs f16-rounded values MFMA {errs[True]:.3f} / v_dot2 {errs[False]:.3f}; vs unrounded "
+          f"MFMA {exact[True]:.3f} / v_dot2 {exact[False]:.3f}")
+    assert errs[True] <= 1.0 and errs[False] <= 1.0, (errs, exact)
 
 
 @pytest.mark.parametrize("M,N,K", [(300, 512, 64), (300, 512, 128), (513, 256, 192),

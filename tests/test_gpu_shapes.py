@@ -140,33 +140,6 @@ def test_v3_geometry_beam_batch_equals_single(v3):
         assert mwx.token_ids(ctx.segments(j)) == batched[i], i
 
 
-@pytest.mark.parametrize("mx", [False, True])
-def test_v3_geometry_grouped_self_attention_bit_identical(make_model, mx):
-    """The beam / best-of self-attention as one workgroup per (group, head)
-    with the group's shared history loaded once (the default) against one
-    workgroup per (row, head): token records (id, t0, t1, p) bit for bit, beam
-    5 with the temperature ladder live (best-of 5 groups on fallback), 6 clips
-    of 12-30 s (window seeks, decoders finishing at different steps), bf16 and
-    MX-fp8 compute."""
-    path = make_model("large-v3-l2-rich", mwx.GGML_BF16)
-    with mwx.Context.open(path, compute=mwx.COMPUTE_MXFP8 if mx else mwx.COMPUTE_MODEL) as ctx:
-        p = service_params(ctx, beam=5, temperature_inc=0.2, language=b"en")
-        pcms = [pcm_clip(70 + k, 12.0 + 3.5 * k) for k in range(6)]
-        out = {}
-        try:
-            for grouped in (True, False):
-                mwx.set_self_group(grouped)
-                base = fresh(ctx)
-                for i in range(6):
-                    ctx.state(base + i)
-                assert ctx.full_batch_states(pcms, p, range(base, base + 6)) == 0
-                out[grouped] = [ctx.token_records(base + i) for i in range(6)]
-        finally:
-            mwx.set_self_group(None)
-    assert sum(len(r) for r in out[True]) > 50
-    assert out[True] == out[False]
-
-
 def test_v3_geometry_beam5_long_form_replay_exact(v3):
     """Beam 5 + 70-s long-form seek loop at large-v3 geometry: token for token
     identical to the oracle's whisper_full logic run on the device's logits."""
