@@ -405,14 +405,22 @@ def launch_ranks(n):
     return rc
 
 
+def one_device():
+    """MWX_BENCH_ONE_DEVICE=1: every rank on GPU 0 and the record gather over
+    gloo (RCCL needs one GPU per rank) -- the N-rank path exercised on a
+    1-GPU box (tests/test_multi_rank.py); never for a timed line."""
+    return os.environ.get("MWX_BENCH_ONE_DEVICE") == "1"
+
+
 def init_dist(world, local):
     """torch.distributed over RCCL (backend "nccl") when the rank has a GPU,
-    gloo otherwise (the CPU tests of the launcher / gather path)."""
+    gloo otherwise (the CPU tests of the launcher / gather path, and
+    MWX_BENCH_ONE_DEVICE)."""
     if world <= 1:
         return None
     import torch
     import torch.distributed as dist
-    if torch.cuda.is_available():
+    if torch.cuda.is_available() and not one_device():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     else:
@@ -621,6 +629,8 @@ def main():
                     help="PCM in host memory, uploaded inside each step (PCIe-inclusive rate)")
     ap.add_argument("--pcm16", action="store_true",
                     help="with --host-input: upload int16 PCM, converted on the device")
+    ap.add_argument("--dump-gather", default=None,
+                    help="rank 0 saves the last gathered record block (int32 .npy) here")
     ap.add_argument("--stream", action="store_true",
                     help="streaming partial-latency leg (SURVEY.md §8 f3) instead of transcription")
     ap.add_argument("--prosody", action="store_true",
@@ -647,6 +657,8 @@ def main():
         return stream_bench(args)
 
     import torch
+    if one_device():
+        local = 0
     dist = init_dist(world, local)
 
     def barrier():
@@ -715,9 +727,11 @@ def main():
 
     tok_count = []  # tokens generated per batch (list.append: thread-safe)
 
+    gdev = None if dist is not None and dist.get_backend() == "gloo" else "cuda"
+
     def gather(block):
         # RCCL over xGMI: every rank's token records (id, t0, t1, p) to rank 0
-        g = shard.gather_to_rank0(dist, block, device="cuda")
+        g = shard.gather_to_rank0(dist, block, device=gdev)
         if g is not None:
             gathered["tokens"] = g
 
@@ -814,8 +828,10 @@ def main():
         torch.cuda.synchronize()
         elapsed_1lane = time.perf_counter() - t1
         timed_1lane = read_timed(owners[:1])
+    if args.dump_gather and rank == 0 and gathered.get("tokens") is not None:
+        np.save(args.dump_gather, gathered["tokens"])
     if dist is not None:
-        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        e = torch.tensor([elapsed], dtype=torch.float64, device=gdev or "cpu")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     audio_s = world * args.clips * args.clip_seconds * args.steps

@@ -2293,6 +2293,11 @@ void orc_encode_stem(void* h, const float* mel_data, int n_len, int seek, float*
   encode_stem(m, x, inp);
   std::copy(inp.begin(), inp.end(), x_out);
 }
+void orc_encode_post(void* h, const float* x, float* out) {
+  const Model& m = *(const Model*)h;
+  layer_norm(x, m.w("encoder.ln_post.weight"), m.w("encoder.ln_post.bias"), m.n_audio_ctx,
+             m.n_audio_state, out);
+}
 void orc_encode_layer(void* h, int il, const float* x_in, const float* const* ext, float* const* outs,
                       float* x_out) {
   const Model& m = *(const Model*)h;

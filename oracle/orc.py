@@ -62,6 +62,7 @@ def lib() -> C.CDLL:
     L.orc_encode.argtypes = [P, fp, C.c_int, C.c_int, fp]
     L.orc_cross.argtypes = [P, fp, fp, fp]
     L.orc_encode_stem.argtypes = [P, fp, C.c_int, C.c_int, fp]
+    L.orc_encode_post.argtypes = [P, fp, fp]
     L.orc_encode_layer.argtypes = [P, C.c_int, fp, C.POINTER(fp), C.POINTER(fp), fp]
     L.orc_decode_seq.argtypes = [P, fp, fp, C.POINTER(C.c_int), C.c_int, fp]
     L.orc_full.restype = P
@@ -312,6 +313,13 @@ class Oracle:
         mel = np.ascontiguousarray(mel, dtype=np.float32)
         out = np.empty((self.hp[1], self.d), dtype=np.float32)
         lib().orc_encode_stem(self.h, _fp(mel), mel.shape[1], seek, out.ctypes.data_as(C.POINTER(C.c_float)))
+        return out
+
+    def encode_post(self, x: np.ndarray) -> np.ndarray:
+        """The encoder output (ln_post) of a residual stream after the last layer."""
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        out = np.empty_like(x)
+        lib().orc_encode_post(self.h, _fp(x), _fp(out))
         return out
 
     def encode_layer(self, il: int, x: np.ndarray, ext=None, want_operands: bool = False):

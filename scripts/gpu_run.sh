@@ -78,7 +78,7 @@ for s in "$@"; do
       run "${s}_$(date +%s)" 400 env MWX_LIB=$GRAFT_REPO_ROOT/ablib/libmwx_$v.so python -u bench.py --steps 12 --warmup 3 --no-cpu-baseline --no-one-lane ;;
     svc) run svc 700 python -u bench.py --service-defaults --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
     svc2) run svc2 900 python -u bench.py --service-defaults --steps 4 --warmup 1 --no-cpu-baseline --no-one-lane ;;
-    fdl) run fdl 600 python -u -m pytest tests/test_gpu_fulldepth.py -k "language_auto" -m gpu -v -s -rf --timeout 500 --timeout-method thread ;;
+    fdl) run fdl 600 python -u -m pytest tests/test_gpu_fulldepth.py -k "language_auto" -m gpu -v -s -rf --durations=0 --timeout 500 --timeout-method thread ;;
     beamorcr) run beamorcr 600 python -u -m pytest tests/test_gpu_beam_oracle.py -k "not full_depth" -m gpu -v -s -rf --timeout 500 --timeout-method thread ;;
     beamorcf) run beamorcf 1000 python -u -m pytest tests/test_gpu_beam_oracle.py -k "full_depth" -m gpu -v -s -rf --durations=0 --timeout 900 --timeout-method thread ;;
     newtests) run newtests 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shapes.py -k "extreme_scales or widening or runahead_mismatch or grouped_self or beam_search" -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
@@ -88,6 +88,7 @@ for s in "$@"; do
         (cd /tmp && run pmcbs_$n 400 rocprofv3 --pmc $c --output-format csv -d "$O/${TAG}_pmcbs_$n" -o pmc -- $B --beam 5 --lanes 1 --steps 1 --warmup 0 --no-cpu-baseline) || exit 5
         python3 scripts/pmc_mix.py "$O/${TAG}_pmcbs_$n" 14 > "$O/${TAG}_pmcbs_$n.md" || exit 5
       done ;;
+    c5layer) run c5layer 600 python -u -m pytest tests/test_gpu_c5.py -k "per_layer" -m gpu -v -s -rf --durations=0 --timeout 500 --timeout-method thread ;;
     barprobe) run barprobe 120 ./scripts/probe/xcd_barrier_probe 4000 ;;
     tests) run tests 1150 python -u -m pytest tests -m gpu -v -s -rf --durations=0 --timeout 600 --timeout-method thread ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;

@@ -63,6 +63,7 @@ def test_full_depth_mxfp8_teacher_forced_220_steps(v3path):
         assert ctx.full(pcm, p, state_index=0) == 0
         ids = [t.id for s in ctx.segments(0) for t in s.tokens]
         _, k_dev, v_dev = ctx.test_encode(pcm, state_index=1)
+        x_dev0 = ctx.test_encode_dump(pcm, state_index=2)[0][0].copy()  # the device's stem output
         lg_d = ctx.test_decode(toks)[len(prompt) - 1:]
     n_text = omx.eot
     err = float(np.abs(lg_d[:, :n_text] - lg_o[:, :n_text]).max())
@@ -89,12 +90,27 @@ def test_full_depth_mxfp8_teacher_forced_220_steps(v3path):
     # MX quantisation of the activations is a step function (e4m3: 3 mantissa
     # bits): where the device's and the oracle's f32 summation orders put an
     # activation on different sides of an e4m3 rounding boundary, that element
-    # moves by up to 1/16 of its magnitude. Over the 32 encoder layers such
-    # flips accumulate: end to end max |d logit| measured 1.10 (mean 0.20)
-    # against 0.142 in bf16 (test_gpu_fulldepth.py) and 0.09 at 2 + 2 layers;
-    # the decoder alone, on the same cross K/V, is bounded separately
-    assert err < 2.0, err
-    assert err_dec < 0.6, err_dec
+    # moves by up to 1/16 of its binade, and later layers amplify it
+    # (test_mxfp8_encoder_per_layer_error_and_flips: every layer's GEMMs agree
+    # to summation noise on identical operands; the encoder's drift equals the
+    # MX oracle's own drift under the device's stem difference). The bound is
+    # that noise floor carried to the logits: the MX oracle's decoder on its
+    # own cross K/V against its decoder on the cross K/V of its encoder run
+    # from a stem perturbed by the device's stem error (err_self), plus the
+    # decoder's own error on identical cross K/V (err_dec, bf16-level)
+    x0 = omx.encode_stem(mel)
+    stem_err = float(np.abs(x_dev0 - x0).max())
+    xp = x0 + np.random.default_rng(0).uniform(-stem_err, stem_err, x0.shape).astype(np.float32)
+    for l in range(omx.hp[4]):
+        xp = omx.encode_layer(l, xp)
+    kp, vp = omx.cross(omx.encode_post(xp))
+    lg_p = omx.decode_seq(kp, vp, toks)[len(prompt) - 1:]
+    err_self = float(np.abs(lg_p[:, :n_text] - lg_o[:, :n_text]).max())
+    print(f"  noise floor: MX oracle vs itself from a stem perturbed by the device's stem error "
+          f"{stem_err:.3g}: logits err {err_self:.4f}; bound err_dec + 1.5 err_self = "
+          f"{err_dec + 1.5 * err_self:.4f}")
+    assert err_dec < 0.25, err_dec  # bf16 full depth: 0.142 (test_gpu_fulldepth.py)
+    assert err <= err_dec + 1.5 * err_self, (err, err_dec, err_self)
     assert agree >= BENCH_STEPS // 2, agree
     if first is not None:
         assert m[first] <= 2 * err, (first, ids[first], oids[first], float(m[first]), err)
@@ -158,12 +174,18 @@ def test_mxfp8_encoder_per_layer_error_and_flips(v3path):
     `dev` differs from the device only in f32 summation order; `own` adds the
     operand differences, of which the MX-visible part is the e4m3 boundary
     flips: elements whose MX rounding differs between the device's operand and
-    the oracle's. Per layer: local error of both, flip counts. Asserted: every
-    layer's `dev` error is summation noise (no per-layer arithmetic bug hides
-    under the end-to-end tolerance), every layer's `own` error within a fixed
-    multiple of the layer's flip-free error plus what its flips can move, and
-    the end-to-end drift of the residual stream no larger than the sum of the
-    per-layer local errors (accumulation, not one bad layer)."""
+    the oracle's.
+    And the reference's own sensitivity: the MX oracle run twice from its own
+    stem output, once as is and once with uniform noise of the device's
+    measured stem error added (the size of the only difference the device has
+    going into layer 0). Its drift between the two runs is the noise floor of
+    MX-fp8 arithmetic itself (every flip moves an element by 1/16 of its
+    binade, and the next layers amplify it); the device's drift from the
+    oracle must stay within 1.5x of it at every layer.
+    Asserted: every layer's `dev` error is summation noise (a per-layer GEMM /
+    residual bug cannot hide); `own` errors and flip rates have no outlier
+    layer (an operand-producer bug would show as one); the device's drift is
+    the MX arithmetic's own."""
     omx = orc.Oracle(v3path, mxfp8=True)
     pcm = pcm_clip(0)
     with mwx.Context.open(v3path, compute=mwx.COMPUTE_MXFP8) as ctx:
@@ -172,36 +194,39 @@ def test_mxfp8_encoder_per_layer_error_and_flips(v3path):
     mel, _ = omx.mel(pcm)
     x0 = omx.encode_stem(mel)
     stem_err = float(np.abs(xs[0] - x0).max())
+    rng = np.random.default_rng(0)
+    xo = x0  # the oracle's own stream
+    xp = x0 + rng.uniform(-stem_err, stem_err, x0.shape).astype(np.float32)  # perturbed stem
     rows = []
-    xo = x0  # the oracle's own stream, for the end-to-end drift
     for l in range(L):
         scale = float(np.abs(xs[l + 1]).max())
         y_own, o_ops = omx.encode_layer(l, xs[l], want_operands=True)
         y_dev = omx.encode_layer(l, xs[l], ext=[ops[g][l] for g in range(4)])
         e_own = float(np.abs(y_own - xs[l + 1]).max())
         e_dev = float(np.abs(y_dev - xs[l + 1]).max())
-        flips = [int((_mx_round(ops[g][l]) != _mx_round(o_ops[g])).sum()) for g in range(4)]
+        flips = [float((_mx_round(ops[g][l]) != _mx_round(o_ops[g])).mean()) for g in range(4)]
         xo = omx.encode_layer(l, xo)
+        xp = omx.encode_layer(l, xp)
         drift = float(np.abs(xo - xs[l + 1]).max())
-        rows.append((l, scale, e_own, e_dev, flips, drift))
-    n_el = [ops[g][0].size for g in range(4)]
-    print(f"MX-fp8 encoder, full depth: stem err {stem_err:.3g}")
-    print("layer | max|x| | local err (own ops) | local err (device ops) | e4m3 flips "
-          "(attnLN / attn / mlpLN / gelu) | end-to-end drift")
-    for l, scale, e_own, e_dev, flips, drift in rows:
-        fr = " / ".join(f"{f} ({f / n:.1e})" for f, n in zip(flips, n_el))
-        print(f"{l:2d} | {scale:8.2f} | {e_own:.4g} | {e_dev:.3g} | {fr} | {drift:.4g}")
-    e_dev_max = max(r[3] / r[1] for r in rows)
-    # device operands: f32 summation order only (relative to the stream's scale)
-    assert e_dev_max < 1e-4, e_dev_max
+        self_drift = float(np.abs(xo - xp).max())
+        rows.append((l, scale, e_own, e_dev, flips, drift, self_drift))
+    print(f"MX-fp8 encoder, full depth: stem err {stem_err:.3g} (device vs oracle)")
+    print("layer | max|x| | local err (own ops) | local err (device ops) | e4m3 flip rate "
+          "(attnLN / attn / mlpLN / gelu) | drift device vs oracle | oracle vs oracle (stem noise)")
+    for l, scale, e_own, e_dev, flips, drift, sd in rows:
+        fr = " / ".join(f"{f:.3f}" for f in flips)
+        print(f"{l:2d} | {scale:6.2f} | {e_own:.4g} | {e_dev:.3g} | {fr} | {drift:.4g} | {sd:.4g}")
+    # device operands: the GEMMs and residual adds agree to f32 summation order
+    e_dev_rel = max(r[3] / r[1] for r in rows)
+    assert e_dev_rel < 1e-4, e_dev_rel  # measured 3e-5 (r06d)
     assert stem_err < 1e-2 * float(np.abs(x0).max()), stem_err
-    for l, scale, e_own, e_dev, flips, drift in rows:
-        # own operands: the flips (and the bf16 rounding they come with) are
-        # the only difference; a layer without flips must agree like `dev`
-        if sum(flips) == 0:
-            assert e_own <= 10 * max(e_dev, 1e-6 * scale), (l, e_own, e_dev)
-    # accumulation: the drift after layer l is bounded by the local errors so far
-    acc = 0.0
-    for l, scale, e_own, e_dev, flips, drift in rows:
-        acc += e_own
-        assert drift <= 4 * acc + 1e-3 * scale, (l, drift, acc)
+    # own operands: no outlier layer (measured 0.17-0.31, 0.2-2.9 % of max |x|;
+    # flip rates 3.1-4.5 % of the LayerNorm / attention outputs, 4-11 % of GELU)
+    med = float(np.median([r[2] for r in rows]))
+    for l, scale, e_own, e_dev, flips, drift, sd in rows:
+        assert e_own <= 2.0 * med and e_own <= 0.04 * scale, (l, e_own, med, scale)
+        assert max(flips[:3]) <= 0.06 and flips[3] <= 0.15, (l, flips)
+        # the device drifts no further from the oracle than the oracle drifts
+        # from itself under the device's stem difference (r06d / CPU: 0.48 /
+        # 0.45 after layer 0, 4.51 / 4.48 after layer 31)
+        assert drift <= 1.5 * sd + 0.05, (l, drift, sd)

@@ -150,3 +150,41 @@ def test_bench_gpus2_launches_two_ranks():
     assert len(lines) == 1, r.stdout  # rank 0 only
     line = lines[0]
     assert line["n_gpus"] == 2 and line["gathered_clips"] == 6 and line["gather_rank_order_ok"]
+
+
+@pytest.mark.gpu
+def test_two_engine_ranks_gather_equals_single(tmp_path):
+    """The data-parallel path with real engine ranks:
+    `bench.py --gpus 2` starts two rank processes, each transcribing its own
+    shard of clips with the engine, and gathers every rank's token records
+    to rank 0. On the one-GPU box both ranks share GPU 0 and the gather runs
+    over gloo (MWX_BENCH_ONE_DEVICE=1; RCCL needs a GPU per rank). Rank 0's
+    gathered block holds rank 0's clips then rank 1's, and every clip's
+    records (id, t0, t1, p) equal that clip decoded alone."""
+    out = tmp_path / "gathered.npy"
+    env = dict(os.environ, MWX_BENCH_ONE_DEVICE="1", TMPDIR=str(tmp_path))
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--arch", "micro",
+           "--wtype", "f16", "--clips", "3", "--steps", "1", "--warmup", "0", "--lanes", "1",
+           "--decode-steps", "24", "--no-cpu-baseline", "--no-one-lane", "--dump-gather", str(out)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["gathered"]["complete"], line["gathered"]
+    got = shard.unpack_records(np.load(out))
+    assert len(got) == 6
+    import mwx
+    path = str(tmp_path / "mwx_bench_micro_f16.bin")  # the model file the run wrote
+    with mwx.Context.open(path) as ctx:
+        p = ctx.default_params(mwx.SAMPLING_GREEDY)  # (bench.py main(), same fields)
+        p.language = b"en"
+        p.temperature = 0.0
+        p.temperature_inc = 0.0
+        p.token_timestamps = True
+        p.suppress_nst = True
+        p.bench_fixed_steps = 24
+        for c in range(6):  # global clip id c = rank * 3 + i (shard.clip_ids)
+            pcm = mwx.pcm16_to_f32(mwx.synth_pcm16(c, 30 * 16000))
+            assert ctx.full(pcm, p, state_index=c) == 0
+            assert ctx.token_records(c) == got[c], c
+    print(f"two engine ranks: {sum(len(g) for g in got)} tokens of 6 clips gathered to rank 0, "
+          f"each clip equal to its single-engine run")
