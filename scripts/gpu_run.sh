@@ -89,6 +89,9 @@ for s in "$@"; do
         python3 scripts/pmc_mix.py "$O/${TAG}_pmcbs_$n" 14 > "$O/${TAG}_pmcbs_$n.md" || exit 5
       done ;;
     c5layer) run c5layer 600 python -u -m pytest tests/test_gpu_c5.py -k "per_layer" -m gpu -v -s -rf --durations=0 --timeout 500 --timeout-method thread ;;
+    pmcl)  # greedy one lane, short decode: LDS conflicts / MFMA busy of the encoder GEMMs and attention
+      (cd /tmp && run pmcl 400 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d "$O/${TAG}_pmcl" -o pmc -- $B --lanes 1 --steps 1 --warmup 0 --decode-steps 8 --no-cpu-baseline) || exit 5
+      python3 scripts/pmc_mix.py "$O/${TAG}_pmcl" 14 > "$O/${TAG}_pmcl.md" || exit 5 ;;
     barprobe) run barprobe 120 ./scripts/probe/xcd_barrier_probe 4000 ;;
     tests) run tests 1150 python -u -m pytest tests -m gpu -v -s -rf --durations=0 --timeout 600 --timeout-method thread ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
