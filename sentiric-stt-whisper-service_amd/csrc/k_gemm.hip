@@ -416,14 +416,25 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
 #pragma unroll
   for (int t = 0; t < NSTG - 1; ++t)
     if (t < nk) GLDS(t, t);
+  // MX: each tile's scales are requested one tile ahead, right after that
+  // tile's DMA, so the counted wait that lands the tile lands its scales too
+  // (requested at the top of their own tile they exposed an L2 round trip at
+  // every tile's wait)
+  int sa_n[MX ? GFM : 1], sw_n[MX ? GFN : 1];
+  if constexpr (MX) {
+#pragma unroll
+    for (int i = 0; i < GFM; ++i) sa_n[i] = sap[i][0];
+#pragma unroll
+    for (int j = 0; j < GFN; ++j) sw_n[j] = swp[j][0];
+  }
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt % NSTG;
     int sa_k[MX ? GFM : 1], sw_k[MX ? GFN : 1];
-    if constexpr (MX) {  // this tile's scales (issued before the wait: L2 hits)
+    if constexpr (MX) {
 #pragma unroll
-      for (int i = 0; i < GFM; ++i) sa_k[i] = sap[i][kt * 4];
+      for (int i = 0; i < GFM; ++i) sa_k[i] = sa_n[i];
 #pragma unroll
-      for (int j = 0; j < GFN; ++j) sw_k[j] = swp[j][kt * 4];
+      for (int j = 0; j < GFN; ++j) sw_k[j] = sw_n[j];
     }
     // tile kt has landed (this wave's DMA), then the barrier makes every
     // wave's part visible and orders all reads of the other stage (tile kt-1)
@@ -447,6 +458,12 @@ __global__ __launch_bounds__(512, 1) void gemm_big(const void* __restrict__ Av, 
     __builtin_amdgcn_sched_barrier(0);
     if (kt + NSTG - 1 < nk) GLDS(kt + NSTG - 1, (kt + NSTG - 1) % NSTG);
     if constexpr (MX) {
+      if (kt + 1 < nk) {
+#pragma unroll
+        for (int i = 0; i < GFM; ++i) sa_n[i] = sap[i][(kt + 1) * 4];
+#pragma unroll
+        for (int j = 0; j < GFN; ++j) sw_n[j] = swp[j][(kt + 1) * 4];
+      }
       typedef int v8i __attribute__((ext_vector_type(8)));
       v8i af[GFM], bf[GFN];
       const int g = lane >> 4;
