@@ -910,8 +910,8 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
   // f16-representable, as in the v_dot2 path; the B operand (8 keys of one
   // column) is two transposed 16-bit reads (ds_read_b64_tr_b16), and the A
   // operand the query's f16 P itself (no per-key scale arithmetic). The
-  // 32-B column blocks of a row are XOR-swizzled by (row >> 1) & 3, so a
-  // 16-lane group's four rows hit distinct banks.
+  // 32-B column blocks of a row are XOR-swizzled (vsw below) so that both
+  // the staging stores and the transposed reads are bank-conflict free.
   // (256-B aligned: the block swizzle assumes a tile row starts at bank 0)
   __shared__ __attribute__((aligned(256))) _Float16 vtile[MFS ? 4 : 1][MFS ? 32 * 64 : 8];
   const int nt32 = (n + 31) >> 5;
@@ -1068,18 +1068,27 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
     // this lane's transposed-read slot: row q = (lane >> 2) & 3 of the
     // group's 4-row block, columns 4 (lane & 3) .. + 3 of the 16-column block
     const int trq = (lane >> 2) & 3, trp = lane & 3;
+    // 32-B column-block swizzle of a V tile row: (row >> 1) & 3 spreads a
+    // read group's rows 4 apart over the banks; row bit 3 (lanes 16-31 of a
+    // transposed read: rows 8-15) flips the block pair too, so the two
+    // 16-lane halves of a ds_read_b64_tr_b16 no longer meet on the same banks
+    auto vsw = [](int row) { return ((row >> 1) & 3) ^ (((row >> 3) & 1) << 1); };
     auto pv_tile = [&](int t, int b) {
       {  // stage the tile as f16 (this wave's region only: in-order LDS, no barrier)
         const f16x8 d0 = dequant_h8(uint2{vr[b][0][0], vr[b][0][1]}, vse[b]);
         const f16x8 d1 = dequant_h8(uint2{vr[b][0][2], vr[b][0][3]}, vse[b]);
         const f16x8 d2 = dequant_h8(uint2{vr[b][1][0], vr[b][1][1]}, vse[b]);
         const f16x8 d3 = dequant_h8(uint2{vr[b][1][2], vr[b][1][3]}, vse[b]);
-        const int sw = (vrow >> 1) & 3, b0 = 2 * (lane & 1);  // the lane's two 16-column blocks
+        const int sw = vsw(vrow), b0 = 2 * (lane & 1);  // the lane's two 16-column blocks
         _Float16* rw = vw + vrow * 64;
-        *reinterpret_cast<f16x8*>(rw + ((b0 ^ sw) << 4)) = d0;
-        *reinterpret_cast<f16x8*>(rw + ((b0 ^ sw) << 4) + 8) = d1;
-        *reinterpret_cast<f16x8*>(rw + (((b0 + 1) ^ sw) << 4)) = d2;
-        *reinterpret_cast<f16x8*>(rw + (((b0 + 1) ^ sw) << 4) + 8) = d3;
+        // odd rows store their two 16-B halves in the other order, so each
+        // store instruction's 8-lane groups cover 8 distinct 16-B bank slots
+        // (same LDS image; in one order rows 2m and 2m + 1 collided)
+        const bool odd = vrow & 1;
+        *reinterpret_cast<f16x8*>(rw + ((b0 ^ sw) << 4) + (odd ? 8 : 0)) = odd ? d1 : d0;
+        *reinterpret_cast<f16x8*>(rw + ((b0 ^ sw) << 4) + (odd ? 0 : 8)) = odd ? d0 : d1;
+        *reinterpret_cast<f16x8*>(rw + (((b0 + 1) ^ sw) << 4) + (odd ? 8 : 0)) = odd ? d3 : d2;
+        *reinterpret_cast<f16x8*>(rw + (((b0 + 1) ^ sw) << 4) + (odd ? 0 : 8)) = odd ? d2 : d3;
       }
       if (t + 4 * VB < nt32) v_load(t + 4 * VB, b);
       // A operand: P of query mrow (rows >= NQ zero) at keys t*32 + 8 gq .. + 7
@@ -1096,7 +1105,7 @@ __global__ __launch_bounds__(256) void dec_xattn_kernel(
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int row = 8 * gq + 4 * h + trq;
-          const _Float16* src = vw + row * 64 + ((nt ^ ((row >> 1) & 3)) << 4) + 4 * trp;
+          const _Float16* src = vw + row * 64 + ((nt ^ vsw(row)) << 4) + 4 * trp;
           // (the whole 64-bit result reinterpreted at once: per-element
           // extraction of the v4i16 miscompiled here, only element 0 of each
           // read reached the operand)
