@@ -181,13 +181,10 @@ __global__ __launch_bounds__(64 * QW) void enc_attn_kernel(const _Float16* __res
       rs = add_xor32(rs);
       lrow[u] = lrow[u] * alpha + rs;
       mrow[u] = mnew;
-      // the O rescale only when some query's running max moved (alpha = 1
-      // multiplies exactly, so skipping it is bit-identical; after the first
-      // tiles the max rarely moves)
-      if (__any(alpha != 1.0f)) {
+      // (skipping this rescale when no query's running max moved -- alpha = 1
+      // is exact -- measured slower: 685 vs 638 us per layer, r06g)
 #pragma unroll
-        for (int te = 0; te < 4; ++te) oacc[te][u] *= alpha;
-      }
+      for (int te = 0; te < 4; ++te) oacc[te][u] *= alpha;
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         f16x8 v;
