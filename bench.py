@@ -796,11 +796,11 @@ def main():
     # windows decoded and decode attempts (a temperature-fallback re-run is
     # an attempt beyond the window's first), run-ahead attempts redone on the
     # host loop (0 unless device and host disagree)
-    dsteps = dpre = nwin = natt = nra = 0
+    dsteps = dpre = nwin = natt = nra = ncs = 0
     for lane in range(lanes):
         a, b = ctx.decode_counters(lane * args.clips, reset=True)
-        w, at = ctx.window_counters(lane * args.clips, reset=True)
-        dsteps, dpre, nwin, natt = dsteps + a, dpre + b, nwin + w, natt + at
+        w, at, cs = ctx.window_counters(lane * args.clips, reset=True)
+        dsteps, dpre, nwin, natt, ncs = dsteps + a, dpre + b, nwin + w, natt + at, ncs + cs
         nra += ctx.runahead_fallbacks(lane * args.clips, reset=True)
     n_batches = args.steps
     win_per_clip = nwin / n_batches / args.clips
@@ -809,7 +809,8 @@ def main():
                    "tokens_per_clip": round(sum(tok_count) / args.steps / args.clips, 1),
                    "windows_per_clip": round(win_per_clip, 3),
                    "fallback_reruns_per_clip": round((natt - nwin) / n_batches / args.clips, 3),
-                   "runahead_host_redos": nra}
+                   "runahead_host_redos": nra,
+                   "live_clips_per_step": round(ncs / max(1, dsteps), 2)}
     if not args.decode_steps:
         n_windows = win_per_clip  # (encoder work: every decoded window is encoded)
     timed_1lane, steps_1lane, elapsed_1lane = None, 0, None
@@ -854,8 +855,12 @@ def main():
         avg_s = avg_raw - ev_s if ev_s is not None and ev_s < 0.5 * avg_raw else avg_raw
         # the engine times every 8th decode step's launches (MWX_PERF_PERIOD),
         # all inside the timed region
-        rows = args.clips * max(1, args.beam)
-        clips_per_launch = args.clips
+        # clips whose cross K/V one launch reads: all of them at fixed steps;
+        # decoding to the model's stop, the timed steps' measured average of
+        # clips with a live row (clips finish their windows at different steps)
+        clips_per_launch = args.clips if args.decode_steps else max(
+            1e-9, decode_work["live_clips_per_step"])
+        rows = clips_per_launch * max(1, args.beam)
         bound, work, desc = kernel_model(args.arch, args.perf_class, clips_per_launch, rows,
                                          launches // max(1, nsteps), prompt_len,
                                          args.decode_steps, n_windows, kv8=args.fp8)

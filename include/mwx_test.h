@@ -62,10 +62,13 @@ int mwx_test_decode_counters(struct mwx_state* state, long* steps, long* prefill
                              int reset);
 
 /* Window counters of a state (the first state of a batch drives it): clip
- * windows decoded and decode attempts run (one per window and temperature
- * tried, so attempts - windows = temperature-fallback re-runs) since the
- * last reset. reset != 0 zeroes them after reading. */
-int mwx_test_window_counters(struct mwx_state* state, long* windows, long* attempts, int reset);
+ * windows decoded, decode attempts run (one per window and temperature
+ * tried, so attempts - windows = temperature-fallback re-runs) and decode
+ * steps summed over the clips live in each (each such clip-step reads the
+ * clip's cross K/V once per layer) since the last reset. reset != 0 zeroes
+ * them after reading. */
+int mwx_test_window_counters(struct mwx_state* state, long* windows, long* attempts,
+                             long* clip_steps, int reset);
 
 /* Run-ahead decode attempts a state redid on the host-driven token loop
  * because the device's advance and the host's replay disagreed (or

@@ -219,6 +219,10 @@ struct State {
   // (mwx_test_window_counters): clip windows decoded, decode attempts run
   // (one per window and temperature tried: attempts - windows = fallbacks)
   long n_windows = 0, n_attempts = 0;
+  // decode steps x clips with a live row in them (a clip's cross K/V is read
+  // once per step by the grouped / per-row cross-attention): the bench's
+  // bytes-per-launch model for legs whose clips finish at different steps
+  long n_clip_steps = 0;
   // run-ahead attempts redone on the host loop (mwx_test_runahead_fallbacks)
   long n_ra_fallback = 0;
   DBuf lpflt, lpparts, lpres;  // logits-processing scratch

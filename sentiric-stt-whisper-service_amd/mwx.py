@@ -217,7 +217,8 @@ def lib() -> C.CDLL:
     L.mwx_test_encode_dump.argtypes = [P, P, C.POINTER(C.c_float), C.c_int, C.c_int,
                                        C.POINTER(C.c_float), C.POINTER(C.c_void_p)]
     L.mwx_test_window_counters.restype = C.c_int
-    L.mwx_test_window_counters.argtypes = [P, C.POINTER(C.c_long), C.POINTER(C.c_long), C.c_int]
+    L.mwx_test_window_counters.argtypes = [P, C.POINTER(C.c_long), C.POINTER(C.c_long),
+                                           C.POINTER(C.c_long), C.c_int]
     L.mwx_test_runahead_fallbacks.restype = C.c_long
     L.mwx_test_runahead_fallbacks.argtypes = [P, C.c_int]
     L.mwx_test_set_xattn_mfs.restype = C.c_int
@@ -659,12 +660,13 @@ class Context:
         return st.value, pf.value
 
     def window_counters(self, state_index: int = 0, reset: bool = True):
-        """(clip windows decoded, decode attempts run) on a state since the last
-        reset (mwx_test_window_counters); attempts - windows = fallbacks."""
-        w, a = C.c_long(), C.c_long()
+        """(clip windows decoded, decode attempts run, clip-steps) on a state
+        since the last reset (mwx_test_window_counters); attempts - windows =
+        fallbacks; clip-steps = decode steps summed over the clips live in them."""
+        w, a, cs = C.c_long(), C.c_long(), C.c_long()
         lib().mwx_test_window_counters(self.state(state_index), C.byref(w), C.byref(a),
-                                       1 if reset else 0)
-        return w.value, a.value
+                                       C.byref(cs), 1 if reset else 0)
+        return w.value, a.value, cs.value
 
     def runahead_fallbacks(self, state_index: int = 0, reset: bool = True) -> int:
         """Run-ahead attempts redone on the host loop (mwx_test_runahead_fallbacks)."""
