@@ -87,11 +87,17 @@ for s in "$@"; do
         n=${x%%:*}; c=${x#*:}
         (cd /tmp && run pmcbs_$n 400 rocprofv3 --pmc $c --output-format csv -d "$O/${TAG}_pmcbs_$n" -o pmc -- $B --beam 5 --lanes 1 --steps 1 --warmup 0 --no-cpu-baseline) || exit 5
         python3 scripts/pmc_mix.py "$O/${TAG}_pmcbs_$n" 14 > "$O/${TAG}_pmcbs_$n.md" || exit 5
+        rm -rf "$O/${TAG}_pmcbs_$n"  # (raw CSVs exceed what gpurun copies back)
       done ;;
     c5layer) run c5layer 600 python -u -m pytest tests/test_gpu_c5.py -k "per_layer" -m gpu -v -s -rf --durations=0 --timeout 500 --timeout-method thread ;;
     pmcl)  # greedy one lane, short decode: LDS conflicts / MFMA busy of the encoder GEMMs and attention
       (cd /tmp && run pmcl 400 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d "$O/${TAG}_pmcl" -o pmc -- $B --lanes 1 --steps 1 --warmup 0 --decode-steps 8 --no-cpu-baseline) || exit 5
       python3 scripts/pmc_mix.py "$O/${TAG}_pmcl" 14 > "$O/${TAG}_pmcl.md" || exit 5 ;;
+    enctests) run enctests 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fulldepth.py tests/test_gpu_shapes.py -k "encoder or greedy or mel or batch32 or fulldepth or full_depth_large_v3_greedy" -m gpu -v -s -rf --durations=0 --timeout 500 --timeout-method thread ;;
+    pmcxc5)  # the MX-fp8 grouped cross-attention (C5): LDS / MFMA and FETCH passes
+      (cd /tmp && run pmcxc5_lds 400 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d "$O/${TAG}_pmcxc5_lds" -o pmc -- $B --fp8 --beam 5 --lanes 1 --steps 1 --warmup 0 --decode-steps 8 --no-cpu-baseline) || exit 5
+      python3 scripts/pmc_mix.py "$O/${TAG}_pmcxc5_lds" 12 > "$O/${TAG}_pmcxc5_lds.md" || exit 5
+      rm -rf "$O/${TAG}_pmcxc5_lds" ;;
     barprobe) run barprobe 120 ./scripts/probe/xcd_barrier_probe 4000 ;;
     tests) run tests 1150 python -u -m pytest tests -m gpu -v -s -rf --durations=0 --timeout 600 --timeout-method thread ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
