@@ -28,6 +28,7 @@ sample on this host).
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -332,6 +333,40 @@ def prosody_bench(args):
         dist.destroy_process_group()
 
 
+def is_headline_config(args):
+    """The full default C3 run (BASELINE.json configs[1]) - the one the driver's bench line is."""
+    return (not args.no_service_leg and not args.no_cpu_baseline and not args.service_defaults
+            and args.arch == "large-v3"
+            and args.beam <= 1 and not args.fp8 and not args.rich and args.decode_steps == 220
+            and args.clip_seconds == 30.0 and not args.host_input)
+
+
+def service_leg():
+    """What a DEFAULT request of the service costs, reported beside the headline (VERDICT r05
+    weak 9): one batch of 32 x 30-s clips at --service-defaults (language auto, beam 5, the
+    temperature ladder, token timestamps, '-rich' weights decoded to the model's stop), one lane,
+    after one warm-up batch. Run as a child process once this process has released its context;
+    its failure is reported, never fatal to the headline."""
+    cmd = [sys.executable, "-u", os.path.abspath(__file__), "--service-defaults", "--lanes", "1",
+           "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-one-lane"]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+        rec = None
+        for ln in r.stdout.splitlines():
+            if ln.startswith("{"):
+                rec = json.loads(ln)
+        if r.returncode != 0 or rec is None:
+            return {"error": f"exit {r.returncode}: {r.stderr[-400:]}"}
+    except Exception as ex:
+        return {"error": str(ex)}
+    return {"value": rec["value"], "unit": rec["unit"], "ms_per_step": rec["ms_per_step"],
+            "steps": rec["steps"], "warmup": rec["warmup"], "lanes": 1,
+            "workload": rec["config"]["workload"], "decode_work": rec.get("decode_work"),
+            "cmd": "python bench.py --service-defaults --lanes 1 --steps 1 --warmup 1"}
+
+
 def prosody_cpu_baseline(pcm, desc, budget_s=10.0):
     """The reference's extract_prosody (oracle/_ref, compiled from its own
     sources) — or, where that was not built, the oracle restatement — on one
@@ -604,6 +639,10 @@ def main():
                          "src/stt_engine.cpp:204-243): language auto (window-0 detect), beam 5, "
                          "the temperature-fallback ladder (temperature_inc 0.2), token "
                          "timestamps, '-rich' weights decoded to the model's stop")
+    ap.add_argument("--no-service-leg", action="store_true",
+                    help="skip the service-default leg the full default (C3) run reports beside its "
+                         "headline (one batch at --service-defaults, one lane, in a child process; "
+                         "--no-cpu-baseline quick runs skip it too)")
     ap.add_argument("--beam", type=int, default=0,
                     help="beam size (0: greedy; the service default is 5)")
     ap.add_argument("--clip-seconds", type=float, default=30.0,
@@ -975,8 +1014,11 @@ def main():
             "one_lane": roof_1lane,
             "cpu_baseline": cpu,
         }
-        print(json.dumps(line), flush=True)
     ctx.close()
+    if rank == 0:
+        if world == 1 and is_headline_config(args):
+            line["service_defaults"] = service_leg()
+        print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

@@ -67,3 +67,15 @@ def test_error_stops_lanes_and_is_raised():
     with pytest.raises(RuntimeError, match="rc=-1"):
         bench.run_lanes(50, 2, step)
     assert calls[0] < 50
+
+
+def test_service_leg_rides_only_on_the_full_default_run():
+    from types import SimpleNamespace
+    base = dict(no_service_leg=False, no_cpu_baseline=False, service_defaults=False,
+                arch="large-v3", beam=0, fp8=False, rich=False, decode_steps=220,
+                clip_seconds=30.0, host_input=False)
+    assert bench.is_headline_config(SimpleNamespace(**base))
+    for k, v in [("no_service_leg", True), ("no_cpu_baseline", True), ("service_defaults", True),
+                 ("arch", "base"), ("beam", 5), ("fp8", True), ("rich", True),
+                 ("decode_steps", 0), ("clip_seconds", 600.0), ("host_input", True)]:
+        assert not bench.is_headline_config(SimpleNamespace(**{**base, k: v})), k
