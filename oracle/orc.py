@@ -160,8 +160,11 @@ class FullOptions:
     @classmethod
     def service_defaults(cls, beam_size: int = 1) -> "FullOptions":
         """Parameters SttEngine::transcribe sets (src/stt_engine.cpp:204-243)
-        with the Settings defaults of src/config.h (greedy when beam_size=1)."""
-        return cls(strategy=0 if beam_size <= 1 else 1, best_of=5, beam_size=beam_size,
+        with the Settings defaults of src/config.h (greedy when beam_size=1).
+        best_of is set for greedy only (stt_engine.cpp:235-238); beam search
+        keeps whisper_full_default_params' -1, i.e. one decoder at t > 0."""
+        return cls(strategy=0 if beam_size <= 1 else 1, best_of=5 if beam_size <= 1 else -1,
+                   beam_size=beam_size,
                    token_timestamps=True, suppress_nst=True, no_speech_thold=0.85,
                    entropy_thold=2.40, logprob_thold=-0.7, temperature=0.0, language="auto")
 

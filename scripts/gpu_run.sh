@@ -28,6 +28,7 @@
 #   profc2     kernel trace of the C2 leg
 #   profb5     kernel trace of beam 5 (one lane)
 #   profc5     kernel trace of the C5 leg (one lane, one 600-s batch)
+#   profsvc    kernel trace of one service-default batch (one lane)
 #   pmcb5      instruction-mix / stall counters of a short beam-5 decode, bf16 and MX-fp8
 #   pmc        FETCH_SIZE / WRITE_SIZE / MFMA-busy passes (each its own run) on a short decode
 # Outputs go to gpurun_out/<TAG>_*; copy the summaries to be judged into profiles/.
@@ -81,6 +82,8 @@ for s in "$@"; do
     fdl) run fdl 600 python -u -m pytest tests/test_gpu_fulldepth.py -k "language_auto" -m gpu -v -s -rf --durations=0 --timeout 500 --timeout-method thread ;;
     beamorcr) run beamorcr 600 python -u -m pytest tests/test_gpu_beam_oracle.py -k "not full_depth" -m gpu -v -s -rf --timeout 500 --timeout-method thread ;;
     beamorcf) run beamorcf 1000 python -u -m pytest tests/test_gpu_beam_oracle.py -k "full_depth" -m gpu -v -s -rf --durations=0 --timeout 900 --timeout-method thread ;;
+    ratests) run ratests 700 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shapes.py -k "runahead or beam or fallback or temperature or service or group_of_7 or sampl" -m gpu -v -s -rf --durations=0 --timeout 300 --timeout-method thread ;;
+    ladderdiag) run ladderdiag 400 python -u scripts/probe/ladder_diag.py ;;
     newtests) run newtests 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shapes.py -k "extreme_scales or widening or runahead_mismatch or grouped_self or beam_search" -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
     pmcbs)  # beam 5 bf16 at the benched 220 steps: FETCH and LDS / MFMA passes (the self-attention's history reads)
       for x in "fetch:FETCH_SIZE" "lds:SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE"; do
@@ -160,6 +163,7 @@ for s in "$@"; do
     prof1) (cd /tmp && run prof1 600 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_prof1" -o prof -- $B --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline) || exit 4; python3 scripts/prof_box.py "$O/${TAG}_prof1" || exit 4 ;;
     profc2) (cd /tmp && run profc2 400 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_profc2" -o prof -- $B --arch base --wtype f16 --clips 1 --lanes 1 --steps 5 --warmup 2 --no-cpu-baseline) || exit 4; python3 scripts/prof_box.py "$O/${TAG}_profc2" || exit 4 ;;
     profb5) (cd /tmp && run profb5 600 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_profb5" -o prof -- $B --beam 5 --lanes 1 --steps 1 --warmup 1 --no-cpu-baseline) || exit 4; python3 scripts/prof_box.py "$O/${TAG}_profb5" || exit 4 ;;
+    profsvc) (cd /tmp && run profsvc 600 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_profsvc" -o prof -- $B --service-defaults --lanes 1 --steps 1 --warmup 0 --no-cpu-baseline) || exit 4; python3 scripts/prof_box.py "$O/${TAG}_profsvc" || exit 4 ;;
     profc5) (cd /tmp && run profc5 700 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_profc5" -o prof -- $B --fp8 --beam 5 --clip-seconds 60 --lanes 1 --steps 1 --warmup 0 --no-cpu-baseline) || exit 4; python3 scripts/prof_box.py "$O/${TAG}_profc5" || exit 4 ;;
     pmcb5)  # instruction mix / stall counters of the beam-5 (and fp8) kernels
       (cd /tmp && run pmcb5 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d "$O/${TAG}_pmcb5" -o pmc -- $B --beam 5 --lanes 1 --steps 1 --warmup 0 --decode-steps 8 --no-cpu-baseline) || exit 5

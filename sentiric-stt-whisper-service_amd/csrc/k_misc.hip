@@ -647,10 +647,14 @@ __device__ __forceinline__ RowCtl next_inputs(const RowRun& w, const RunConst& C
   return n;
 }
 
-// Run-ahead greedy decoding: applies the token rules to the step just run and
-// writes the next step's inputs. One workgroup; every row is independent. The
-// step's token records and the inputs chosen for the next step go straight to
-// the pinned host ring slot `*run_step % nslot`.
+// Run-ahead greedy decoding and temperature sampling: applies the token rules
+// to the step just run and writes the next step's inputs. One workgroup; every
+// row is independent. The step's token records and the inputs chosen for the
+// next step go straight to the pinned host ring slot `*run_step % nslot`.
+// Sampling (B.draws set): a sampling row's token is its std::discrete_distribution
+// draw of this step (sample_draws, earlier in the same graph); the next step's
+// uniform is the row's next one in the host-filled ring, and the step's draws
+// are reported for the host replay.
 __global__ __launch_bounds__(256) void row_advance_kernel(RowRun* __restrict__ run,
                                                           int* __restrict__ run_step,
                                                           const int* __restrict__ prompt,
@@ -658,10 +662,11 @@ __global__ __launch_bounds__(256) void row_advance_kernel(RowRun* __restrict__ r
                                                           RowCtl* __restrict__ ctl,
                                                           TokOut* __restrict__ out,
                                                           RunReport* __restrict__ rep, RunConst C,
-                                                          PickIn pk) {
+                                                          BeamRun B, PickIn pk) {
   const int step = *run_step;
   const int R = C.R;
-  RunReport* slot = rep + (long)(step % C.nslot) * R;
+  const int sl = step % C.nslot;
+  RunReport* slot = rep + (long)sl * R;
   for (int r = threadIdx.x; r < R; r += blockDim.x) {
     RowRun w = run[r];
     const RowCtl k = ctl[r];
@@ -671,11 +676,20 @@ __global__ __launch_bounds__(256) void row_advance_kernel(RowRun* __restrict__ r
       out[r] = t;
     }
     if (!w.stopped) {
-      if (k.sample) token_rules(w, t.id, C);
+      if (k.sample) token_rules(w, B.draws ? B.draws[(long)r * B.KD].id : t.id, C);
       if (!w.stopped) w.fed++;
     }
     int tok;
     const RowCtl n = next_inputs(w, C, prompt + (long)r * C.prompt_stride, tok);
+    if (B.draws) {
+      const int nd = (!w.stopped && n.sample) ? B.KD : 0;
+      for (int d = 0; d < nd; ++d)
+        B.du[(long)r * B.KD + d] = B.uring[(long)r * B.ring_n + (w.used + d) % B.ring_n];
+      w.used += nd;
+      B.dnd[r] = nd;
+      for (int d = 0; d < B.KD; ++d)
+        B.drep[((long)sl * R + r) * B.KD + d] = B.draws[(long)r * B.KD + d];
+    }
     si[r] = tok;
     si[R + r] = w.fed;
     si[2 * R + r] = n.active;
@@ -885,9 +899,9 @@ __global__ __launch_bounds__(64) void perf_empty_kernel() {}
 void launch_perf_empty(hipStream_t st) { perf_empty_kernel<<<1, 64, 0, st>>>(); }
 
 void row_advance(RowRun* run, int* run_step, const int* prompt, int* stepin, RowCtl* ctl,
-                 TokOut* out, RunReport* rep, const RunConst& C, const PickIn& pk,
-                 hipStream_t st) {
-  row_advance_kernel<<<1, 256, 0, st>>>(run, run_step, prompt, stepin, ctl, out, rep, C, pk);
+                 TokOut* out, RunReport* rep, const RunConst& C, const BeamRun& B,
+                 const PickIn& pk, hipStream_t st) {
+  row_advance_kernel<<<1, 256, 0, st>>>(run, run_step, prompt, stepin, ctl, out, rep, C, B, pk);
 }
 
 void beam_advance(RowRun* run, int* run_step, const int* prompt, int* stepin, RowCtl* ctl,

@@ -325,10 +325,6 @@ struct PickIn {
   const LPRes* res = nullptr;
   LogitsConst C{};
 };
-void row_advance(RowRun* run, int* run_step, const int* prompt, int* stepin, RowCtl* ctl,
-                 TokOut* out, RunReport* rep, const RunConst& C, const PickIn& pk,
-                 hipStream_t st);
-
 struct Draw;
 // Run-ahead beam search: per clip (n decoders = rows r0 .. r0+n-1), the
 // beam step of whisper.cpp's decoder loop on the device (driver.inc
@@ -357,6 +353,13 @@ struct BeamRun {
 void beam_advance(RowRun* run, int* run_step, const int* prompt, int* stepin, RowCtl* ctl,
                   TokOut* out, RunReport* rep, const RunConst& C, const BeamRun& B,
                   const PickIn& pk, hipStream_t st);
+// Run-ahead greedy decoding and temperature sampling (best-of): B.draws ==
+// nullptr: the step's argmax; else each sampling row takes its draw
+// B.draws[r][0] and the next step's uniform comes from the ring as in
+// beam_advance (B.n, kvmap, kvown, Tctx and brep unused)
+void row_advance(RowRun* run, int* run_step, const int* prompt, int* stepin, RowCtl* ctl,
+                 TokOut* out, RunReport* rep, const RunConst& C, const BeamRun& B,
+                 const PickIn& pk, hipStream_t st);
 
 // Logits processing is split over LP_G chunks of LP_CHUNK vocabulary entries
 // per row (LP_G * LP_CHUNK >= n_vocab for every Whisper vocabulary).

@@ -49,6 +49,7 @@ class FollowReport:
     eps_max: float
     rows: int
     tokens: List[int] = field(default_factory=list)
+    kinds: Dict[str, int] = field(default_factory=dict)  # decisions checked per kind
 
     def summary(self, label: str) -> str:
         kinds: Dict[str, int] = {}
@@ -117,4 +118,7 @@ def follow_compare(o: orc.Oracle, pcm, opt: orc.FullOptions, guide: List[orc.Tra
         forced.append((e, dist, bound))
     eps_max = max((err for rows in errs.values() for _, err in rows), default=0.0)
     toks = [t.id for s in segs for t in s.tokens]
-    return FollowReport(len(ta), forced, eps_max, sum(len(r) for r in errs.values()), toks)
+    kinds: Dict[str, int] = {}
+    for e in ta:
+        kinds[e.kind] = kinds.get(e.kind, 0) + 1
+    return FollowReport(len(ta), forced, eps_max, sum(len(r) for r in errs.values()), toks, kinds)

@@ -99,6 +99,26 @@ def test_beam5_vs_oracle_arithmetic(rich, temperature_inc):
         print(r.summary(f"clip {k} (temperature_inc {temperature_inc})"))
 
 
+@pytest.mark.parametrize("best_of", [-1, 5])
+def test_beam5_temperature_ladder_vs_oracle_arithmetic(rich, best_of):
+    """The attempts at t > 0 of beam search (beam_size candidates drawn per
+    decoder from the temperature-scaled probs, best_of decoders: -1 -> one, as
+    the service runs it, and 5), run ahead on the device: logprob_thold above
+    any average log-probability makes every window walk the whole ladder
+    0.0 -> 1.0 (the clips of test_beam5_vs_oracle_arithmetic pass at t = 0).
+    Every decision checked as there, the noise bounds scaled by 1/t."""
+    ctx, o = rich
+    p, opt = beam_params(ctx, 0.2), beam_opt(0.2)
+    p.greedy.best_of = opt.best_of = best_of
+    p.logprob_thold = opt.logprob_thold = 0.5
+    for k in (0, 2):
+        pcm = pcm_clip(50 + k, 14.0 + 4 * k)
+        r = compare(ctx, o, pcm, p, opt, "micro-rich")
+        print(r.summary(f"clip {k} (ladder, best_of {best_of})"))
+        print("decisions per kind:", r.kinds)
+        assert r.kinds.get("fallback", 0) >= 5, r.kinds  # the ladder ran
+
+
 def full_depth(path, compute, model, steps=FULL_DEPTH_STEPS, mxfp8=False):
     o = orc.Oracle(path, mxfp8=mxfp8)
     with mwx.Context.open(path, compute=compute) as ctx:

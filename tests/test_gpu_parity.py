@@ -108,7 +108,8 @@ def service_params(ctx, beam=1, temperature_inc=0.2, language=b"auto"):
     p.logprob_thold = -0.7
     p.temperature = 0.0
     p.temperature_inc = temperature_inc
-    p.greedy.best_of = 5
+    # (the service sets best_of for greedy only, src/stt_engine.cpp:235-238)
+    p.greedy.best_of = 5 if beam <= 1 else -1
     p.language = language
     return p
 
@@ -760,7 +761,7 @@ pcms = [mwx.pcm16_to_f32(mwx.synth_pcm16(k, int(s * 16000))) for k, s in enumera
 assert ctx.full_batch(pcms, p) == 0
 out = [[[s.t0, s.t1, s.text, [(t.id, t.tid, t.p, t.t0, t.t1) for t in s.tokens]]
         for s in ctx.segments(i)] for i in range(len(pcms))]
-print(json.dumps(out))
+print(json.dumps([out, ctx.window_counters(0)[:2], ctx.runahead_fallbacks(0)]))
 '''
 
 
@@ -770,7 +771,9 @@ def test_runahead_decode_equals_synchronous_loop(make_model, max_tokens, inc):
     next-input rules after each step, the host reads step k while step k+1
     runs) gives exactly the host-driven loop's results (MWX_NO_RUNAHEAD=1):
     six clips of 3-75 s (long-form seeks, timestamps, EOT), the fallback
-    re-decodes (temperature > 0 runs the host loop), and the max_tokens stop."""
+    re-decodes (best-of-5 temperature sampling, run ahead too since round 6:
+    each row's token is its device draw, its uniforms come from the ring the
+    host fills from a copy of its RNG), and the max_tokens stop."""
     import json
     import os
     import subprocess
@@ -785,33 +788,50 @@ def test_runahead_decode_equals_synchronous_loop(make_model, max_tokens, inc):
                            cwd=root, env=env, capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-2000:]
         res.append(json.loads(r.stdout.strip().splitlines()[-1]))
-    assert res[0] == res[1]
-    assert sum(len(s[3]) for c in res[0] for s in c) > 40
+    (out_ra, (windows, attempts), redos), (out_host, _, _) = res
+    print("windows", windows, "attempts", attempts, "run-ahead redos", redos)
+    assert redos == 0  # (a redo would run the host loop: the comparison would be vacuous)
+    assert inc == 0.0 or attempts > windows  # temperature fallback attempts ran
+    assert out_ra == out_host
+    assert sum(len(s[3]) for c in out_ra for s in c) > 40
 
 
-@pytest.mark.parametrize("temperature_inc", [0.0, 0.2])
-def test_beam_runahead_equals_host_loop(rich, temperature_inc, monkeypatch):
+@pytest.mark.parametrize("temperature_inc,best_of", [(0.0, 5), (0.2, 5), (0.2, -1)])
+def test_beam_runahead_equals_host_loop(rich, temperature_inc, best_of, monkeypatch):
     """Beam search run ahead on the device (beam_advance_kernel: ranking,
     dedup, decoder hand-over and KV maps, the next step's inputs and uniforms)
     == the host loop (MWX_NO_RUNAHEAD: beam_step on the host, one round trip
     per step): every clip's token records bit for bit, 4 clips in one batch.
-    With fallback, the sampled decoders after a beam pass draw from RNG
-    streams the run-ahead consumed from its uniform ring."""
+    With fallback, the attempts at t > 0 (beam search over best_of decoders
+    drawing from the temperature-scaled probs; run ahead since round 6) draw
+    from RNG streams the earlier attempts consumed from their uniform rings.
+    best_of = -1 is what the service runs (src/stt_engine.cpp:235-238 sets
+    best_of for greedy only: one decoder at t > 0). These clips pass at t = 0,
+    so the t > 0 cases raise logprob_thold above any average log-probability:
+    every window walks the whole ladder 0.0 -> 1.0."""
     ctx, _, _ = rich
     p = beam_params(ctx, temperature_inc)
+    p.greedy.best_of = best_of
+    if temperature_inc > 0.0:
+        p.logprob_thold = 0.5
     pcms = [pcm_clip(40 + k, 10.0 + 7 * k) for k in range(4)]
 
     def run():
         base = len(ctx.states)
         for i in range(4):
             ctx.state(base + i)
+        ctx.window_counters(base)
+        ctx.runahead_fallbacks(base)
         assert ctx.full_batch_states(pcms, p, range(base, base + 4)) == 0
-        return [ctx.token_records(base + i) for i in range(4)]
+        return ([ctx.token_records(base + i) for i in range(4)], ctx.window_counters(base)[:2],
+                ctx.runahead_fallbacks(base))
 
-    ra = run()
+    ra, (windows, attempts), redos = run()
     monkeypatch.setenv("MWX_NO_RUNAHEAD", "1")
-    host = run()
-    print("tokens per clip:", [len(x) for x in ra])
+    host, _, _ = run()
+    print("tokens per clip:", [len(x) for x in ra], "windows", windows, "attempts", attempts)
+    assert redos == 0
+    assert temperature_inc == 0.0 or attempts > windows
     assert sum(len(x) for x in ra) > 20
     assert ra == host
 

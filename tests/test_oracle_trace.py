@@ -156,3 +156,24 @@ def test_follow_mode_stops_at_a_structural_difference(rich):
     _, tr2, brk2 = o.traced_follow(tr, pcm, beam_opt())  # its own trace: followed to the end
     assert brk2 is None and not [x for x in tr2 if x.forced]
     assert [x.key() for x in tr2] == [x.key() for x in tr]
+
+
+def test_best_decoder_id_persists_across_attempts(rich):
+    """whisper.cpp v1.8.2 declares best_decoder_id before the temperature loop
+    and resets only the decoders an attempt runs: beam search's fallbacks run
+    one decoder (best_of = -1, src/stt_engine.cpp:235-238), and when it fails
+    the window's best stays the earlier attempt's decoder — whose state that
+    attempt left. The oracle keeps that (the engine's driver does too, checked
+    on the GPU by test_beam5_temperature_ladder_vs_oracle_arithmetic): on this
+    clip, with every window walking the ladder, the t > 0 attempts' BEST events
+    name decoder 2 of the t = 0 beam pass although only decoder 0 ran."""
+    o = rich
+    pcm = mwx.pcm16_to_f32(mwx.synth_pcm16(50, 14 * 16000))
+    opt = beam_opt()
+    opt.temperature_inc = 0.2
+    opt.logprob_thold = 0.5
+    assert opt.best_of == -1
+    (_, segs, _, _), tr = o.traced(o.full, pcm, opt)
+    best = [(e.seek, e.it, e.a) for e in tr if e.kind == "best"]
+    stale = [b for b in best if b[1] > 0 and b[2] > 0]
+    assert stale, best
