@@ -342,13 +342,14 @@ def is_headline_config(args):
 
 
 def service_leg():
-    """What a DEFAULT request of the service costs, reported beside the headline (VERDICT r05
-    weak 9): one batch of 32 x 30-s clips at --service-defaults (language auto, beam 5, the
-    temperature ladder, token timestamps, '-rich' weights decoded to the model's stop), one lane,
-    after one warm-up batch. Run as a child process once this process has released its context;
-    its failure is reported, never fatal to the headline."""
-    cmd = [sys.executable, "-u", os.path.abspath(__file__), "--service-defaults", "--lanes", "1",
-           "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-one-lane"]
+    """What DEFAULT requests of the service cost, reported beside the headline (VERDICT r05
+    weak 9): batches of 32 x 30-s clips at --service-defaults (language auto, beam 5, the
+    temperature ladder, token timestamps, '-rich' weights decoded to the model's stop), two
+    lanes as the headline (the service's parallel_requests = 2, src/config.h:41): one batch per
+    lane timed after one warm-up batch per lane. Run as a child process once this process has
+    released its context; its failure is reported, never fatal to the headline."""
+    cmd = [sys.executable, "-u", os.path.abspath(__file__), "--service-defaults", "--lanes", "2",
+           "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-one-lane"]
     env = {k: v for k, v in os.environ.items()
            if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
     try:
@@ -362,9 +363,9 @@ def service_leg():
     except Exception as ex:
         return {"error": str(ex)}
     return {"value": rec["value"], "unit": rec["unit"], "ms_per_step": rec["ms_per_step"],
-            "steps": rec["steps"], "warmup": rec["warmup"], "lanes": 1,
+            "steps": rec["steps"], "warmup": rec["warmup"], "lanes": 2,
             "workload": rec["config"]["workload"], "decode_work": rec.get("decode_work"),
-            "cmd": "python bench.py --service-defaults --lanes 1 --steps 1 --warmup 1"}
+            "cmd": "python bench.py --service-defaults --lanes 2 --steps 2 --warmup 1"}
 
 
 def prosody_cpu_baseline(pcm, desc, budget_s=10.0):

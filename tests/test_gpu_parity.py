@@ -349,6 +349,35 @@ def test_rich_fallback_matches_oracle(rich):
     assert ids[:12] == oids[:12]
 
 
+@pytest.mark.parametrize("k", [3, 50])
+def test_rich_greedy_ladder_matches_oracle_replay(rich, k):
+    """Every window walks the whole temperature ladder (logprob_thold above
+    any average log-probability): greedy at t = 0, then best_of 5 sampled
+    decoders at t = 0.2 .. 1.0, all run ahead on the device since round 6, and
+    the window's result kept by whisper.cpp's best_decoder_id rule across the
+    attempts. Token for token identical to the oracle's loop on the device's
+    logits."""
+    ctx, o, _ = rich
+    pcm = pcm_clip(k, 14.0 if k == 50 else 30.0)
+    opt = orc.FullOptions.service_defaults()
+    opt.language = "en"
+    opt.logprob_thold = 0.5
+    p = service_params(ctx, language=b"en")
+    p.logprob_thold = 0.5
+    idx = len(ctx.states)
+    ctx.state(idx)
+    ctx.window_counters(idx)
+    ctx.runahead_fallbacks(idx)
+    assert ctx.full(pcm, p, state_index=idx) == 0
+    segs = ctx.segments(idx)
+    windows, attempts, _ = ctx.window_counters(idx)
+    assert attempts == 6 * windows and ctx.runahead_fallbacks(idx) == 0, (windows, attempts)
+    osegs = replay(ctx, o, pcm, opt)
+    assert_same(segs, osegs, p_tol=1e-4)
+    print(f"clip {k}: {windows} windows x 6 attempts, "
+          f"{sum(len(sg.tokens) for sg in segs)} tokens")
+
+
 def beam_params(ctx, temperature_inc):
     return service_params(ctx, beam=5, temperature_inc=temperature_inc, language=b"en")
 
