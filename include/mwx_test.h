@@ -119,6 +119,13 @@ int mwx_test_set_dec_shared(int on);
  * Returns the previous mode. */
 int mwx_test_set_gemm_8ph(int on);
 
+/* The decode LayerNorms before the QKV and cross-Q projections folded into
+ * those split-K GEMMs at one row (gemm_splitk_ln, bit-identical to the
+ * separate LayerNorm launch) on (1) / off (0) / back to the MWX_LN_FOLD
+ * environment default, on (-1). Read when a decode step is captured. Returns
+ * the previous mode. */
+int mwx_test_set_ln_fold(int on);
+
 
 /* The MX-fp8 cross K/V cache's widening of e4m3 codes to f16 as the
  * cross-attention kernels run it: n8 groups of 8 codes (codes[8 n8]), each

@@ -44,6 +44,22 @@ namespace mwx {
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// LayerNorm folded into the next split-K GEMM at one row (gemm_splitk_ln):
+// env MWX_LN_FOLD (default on) read once; mwx_test_set_ln_fold switches it
+// (read when a decode step is captured)
+inline std::atomic<int>& ln_fold_mode() {
+  static std::atomic<int> m{-1};
+  return m;
+}
+inline bool ln_fold_on() {
+  int v = ln_fold_mode().load();
+  if (v < 0) {
+    v = (getenv("MWX_LN_FOLD") && atoi(getenv("MWX_LN_FOLD")) == 0) ? 0 : 1;
+    ln_fold_mode().store(v);
+  }
+  return v != 0;
+}
+
 // Process-wide order between graph capture and (de)allocation: while any
 // thread captures a stream, HIP rejects legacy-stream operations such as
 // hipMemset ("would make the legacy stream depend on a capturing stream") and
@@ -204,7 +220,7 @@ struct State {
     return (RunReport*)rep_pin;
   }
   // decoder workspace (row-batched)
-  DBuf xd, hd, qd, od, ffd, logits, kself, vself, stepin, ctl, tokout, probs, logprobs, smask;
+  DBuf xd, xd2, hd, qd, od, ffd, logits, kself, vself, stepin, ctl, tokout, probs, logprobs, smask;
   DBuf pqkv, pres, pq;  // split-K partial slabs of the decode GEMMs
   // batched prompt prefill: virtual-row inputs [tok|pos|act|xidx|crow] and the
   // layer stack's activations / slabs for up to MWX_PREFILL_ROWS virtual rows
@@ -1041,6 +1057,7 @@ struct Driver {
     S.pres.get((size_t)ks_res() * R * d * 4);
     S.pq.get((size_t)ks_d() * R * d * 4);
     S.xd.get((size_t)R * d * 4, true);
+    S.xd2.get((size_t)R * d * 4, true);  // (the residual's other buffer: LayerNorm folded at R = 1)
     // decode-GEMM A operands (fragment tiles), rows padded to the 64-row block
     const size_t R64 = (size_t)(R + 63) / 64 * 64;
     S.hd.get(R64 * d * sizeof(T), true);
@@ -1130,6 +1147,7 @@ struct Driver {
     // prefill: the self-cache row of each virtual row (nullptr: row = its own)
     const int* crow = nullptr;
     float* xd = nullptr;
+    float* xd2 = nullptr;  // the residual's second buffer (nullptr: no LayerNorm folding)
     T *hd = nullptr, *od = nullptr, *ffd = nullptr;
     float *Pqkv = nullptr, *Pres = nullptr, *Pq = nullptr;
     _Float16 *kself = nullptr, *vself = nullptr;  // layer-0 self cache of row 0
@@ -1182,10 +1200,34 @@ struct Driver {
       emb.n_pos = Tctx;
       c.embed = false;
     }
-    layer_norm_dec<T>(c.xd, W.ln1_w, W.ln1_b, hd, n, d, rw.act, s, c.ks_prev ? rw.Pres : nullptr,
-                      c.ks_prev, c.bias_prev, emb);
-    { PerfScope ps(S, "dec_gemm", s);
-      c.k1 = gemm_splitk_partials<T>(hd, Dw(W.qkv), n, 3 * d, d, rw.Pqkv, s); }
+    // one row (C2, single-clip requests): the LayerNorms before the QKV and
+    // cross-Q projections are folded into those split-K GEMMs (gemm_splitk_ln:
+    // the same arithmetic, no launch of their own); the residual moves to the
+    // other buffer at each. MWX_LN_FOLD=0 keeps the separate launches (A/B).
+    const bool fold = n == 1 && rw.xd2 && !rw.prefill && ln_fold_on();
+    auto other = [&](float* x) { return x == rw.xd ? rw.xd2 : rw.xd; };
+    c.k1 = 0;
+    if (fold && !emb.te) {
+      LnFuse f;
+      f.x_in = c.xd;
+      f.x_out = other(c.xd);
+      f.P = c.ks_prev ? rw.Pres : nullptr;
+      f.KS = c.ks_prev;
+      f.pstride = (long)n * d;
+      f.pbias = c.bias_prev;
+      f.w = W.ln1_w;
+      f.b = W.ln1_b;
+      f.active = rw.act;
+      PerfScope ps(S, "dec_gemm", s);
+      c.k1 = gemm_splitk_ln<T>(f, Dw(W.qkv), 3 * d, d, rw.Pqkv, s);
+      if (c.k1) c.xd = f.x_out;
+    }
+    if (!c.k1) {
+      layer_norm_dec<T>(c.xd, W.ln1_w, W.ln1_b, hd, n, d, rw.act, s, c.ks_prev ? rw.Pres : nullptr,
+                        c.ks_prev, c.bias_prev, emb);
+      PerfScope ps(S, "dec_gemm", s);
+      c.k1 = gemm_splitk_partials<T>(hd, Dw(W.qkv), n, 3 * d, d, rw.Pqkv, s);
+    }
     static const int pf_selfwrite =
         getenv("MWX_PREFILL_SELFWRITE") ? atoi(getenv("MWX_PREFILL_SELFWRITE")) : 0;
     if (rw.prefill)
@@ -1197,9 +1239,27 @@ struct Driver {
                        rw.prefill ? 1 : rw.xgroup, pf_selfwrite || !rw.prefill); }
     { PerfScope ps(S, "dec_gemm", s);
       c.k2 = gemm_splitk_partials<T>(rw.od, Dw(W.o), n, d, d, rw.Pres, s); }
-    layer_norm_dec<T>(c.xd, W.lnc_w, W.lnc_b, hd, n, d, rw.act, s, rw.Pres, c.k2, W.o_b);
-    PerfScope ps(S, "dec_gemm", s);
-    c.k3 = gemm_splitk_partials<T>(hd, Dw(W.cq), n, d, d, rw.Pq, s);
+    c.k3 = 0;
+    if (fold) {
+      LnFuse f;
+      f.x_in = c.xd;
+      f.x_out = other(c.xd);
+      f.P = rw.Pres;
+      f.KS = c.k2;
+      f.pstride = (long)n * d;
+      f.pbias = W.o_b;
+      f.w = W.lnc_w;
+      f.b = W.lnc_b;
+      f.active = rw.act;
+      PerfScope ps(S, "dec_gemm", s);
+      c.k3 = gemm_splitk_ln<T>(f, Dw(W.cq), d, d, rw.Pq, s);
+      if (c.k3) c.xd = f.x_out;
+    }
+    if (!c.k3) {
+      layer_norm_dec<T>(c.xd, W.lnc_w, W.lnc_b, hd, n, d, rw.act, s, rw.Pres, c.k2, W.o_b);
+      PerfScope ps(S, "dec_gemm", s);
+      c.k3 = gemm_splitk_partials<T>(hd, Dw(W.cq), n, d, d, rw.Pq, s);
+    }
   }
   void layer_cross(const LayerRows& rw, LayerRun& c, int l, hipStream_t s) {
     const int n = rw.n;
@@ -1251,9 +1311,27 @@ struct Driver {
     e.c16 = rw.ffd;
     e.ldc = 4 * d;
     e.pack_out = true;
-    layer_norm_dec<T>(c.xd, W.ln2_w, W.ln2_b, rw.hd, n, d, rw.act, s, rw.Pres, c.k4, W.co_b);
-    { PerfScope ps(S, "dec_gemm", s);
-      c.k5 = gemm_decode<T>(EPI_GELU, rw.hd, Dw(W.fc1), n, 4 * d, d, e, s); }
+    c.k5 = false;
+    if (n == 1 && rw.xd2 && !rw.prefill && ln_fold_on()) {  // (as layer_pre)
+      LnFuse f;
+      f.x_in = c.xd;
+      f.x_out = c.xd == rw.xd ? rw.xd2 : rw.xd;
+      f.P = rw.Pres;
+      f.KS = c.k4;
+      f.pstride = (long)n * d;
+      f.pbias = W.co_b;
+      f.w = W.ln2_w;
+      f.b = W.ln2_b;
+      f.active = rw.act;
+      PerfScope ps(S, "dec_gemm", s);
+      c.k5 = gemm_decode_ln<T>(EPI_GELU, f, Dw(W.fc1), 4 * d, d, e, s);
+      if (c.k5) c.xd = f.x_out;
+    }
+    if (!c.k5) {
+      layer_norm_dec<T>(c.xd, W.ln2_w, W.ln2_b, rw.hd, n, d, rw.act, s, rw.Pres, c.k4, W.co_b);
+      PerfScope ps(S, "dec_gemm", s);
+      c.k5 = gemm_decode<T>(EPI_GELU, rw.hd, Dw(W.fc1), n, 4 * d, d, e, s);
+    }
     { PerfScope ps(S, "dec_gemm", s);
       c.ks_prev = gemm_splitk_partials<T>(rw.ffd, Dw(W.fc2), n, d, 4 * d, rw.Pres, s); }
     c.bias_prev = W.fc2_b;
@@ -1263,7 +1341,8 @@ struct Driver {
 
   // embedding + all decoder layers; returns the last FFN2's split-K factor
   // and bias (folded into the consumer: the final LayerNorm)
-  void run_layers(const LayerRows& rw, hipStream_t s, int& ks_prev, const float*& bias_prev) {
+  void run_layers(const LayerRows& rw, hipStream_t s, int& ks_prev, const float*& bias_prev,
+                  float** xd_out = nullptr) {
     LayerRun c;
     layers_begin(rw, c, s);
     for (int l = 0; l < L_dec; ++l) {
@@ -1273,6 +1352,7 @@ struct Driver {
     }
     ks_prev = c.ks_prev;
     bias_prev = c.bias_prev;
+    if (xd_out) *xd_out = c.xd;  // (the buffer holding the residual after the last layer)
   }
 
   // Batched prompt prefill (whisper.cpp decodes a window's prompt in one
@@ -1410,6 +1490,7 @@ struct Driver {
     rw.act = si + 2 * R;
     rw.xidx = si + 3 * R;
     rw.xd = (float*)S.xd.p;
+    rw.xd2 = (float*)S.xd2.p;
     rw.hd = (T*)S.hd.p;
     rw.od = (T*)S.od.p;
     rw.ffd = (T*)S.ffd.p;
@@ -1427,10 +1508,12 @@ struct Driver {
 
   // one decode step of all R rows on stream s
   void decode_rows(int R, bool want_probs, hipStream_t s) {
-    const LayerRows rw = step_rows(R);
+    LayerRows rw = step_rows(R);
     int ks_prev = 0;
     const float* bias_prev = nullptr;
-    run_layers(rw, s, ks_prev, bias_prev);
+    float* xd = rw.xd;
+    run_layers(rw, s, ks_prev, bias_prev, &xd);
+    rw.xd = xd;
     step_tail(R, rw, ks_prev, bias_prev, want_probs, s);
   }
 

@@ -25,6 +25,7 @@
 
 #include "kcommon.h"
 #include "kernels.h"
+#include "ln_core.h"
 
 namespace mwx {
 
@@ -814,11 +815,14 @@ __device__ __forceinline__ void skinny_store(const EpiParams& P, int m, int n, f
   epi_store<EPI, T, OUT16>(P, 0, m, n, v);
 }
 
-template <typename T, int MT, int KCH, bool W8 = false>
+// LNF (M = 1, MT = 1): the A operand is the folded LayerNorm of the row
+// (LnFuse, ln_core.h), as gemm_splitk LNF.
+template <typename T, int MT, int KCH, bool W8 = false, bool LNF = false>
 __global__ __launch_bounds__(1024) void gemm_skinny(int epi, const T* __restrict__ Ap,
                                                     const void* __restrict__ Wv,
                                                     const uint8_t* __restrict__ Ws, int KT, int M,
-                                                    int N, EpiParams P) {
+                                                    int N, EpiParams P, LnFuse ln) {
+  static_assert(!LNF || MT == 1, "the folded LayerNorm serves one row");
   using V8 = typename Elt<T>::v8;
   __shared__ f32x4 red[16][MT][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, NW = blockDim.x >> 6;
@@ -830,7 +834,6 @@ __global__ __launch_bounds__(1024) void gemm_skinny(int epi, const T* __restrict
   const int Mb = min(16 * MT, M - m_base);
   const int kt0 = wid * KCH;
   const long f0 = (long)bx * KT + kt0;  // first weight fragment of this wave
-  const T* at = Ap + ((long)(by * MT) * KT + kt0) * 512 + lane * 8;
   V8 bfr[KCH];
   V8 afr[MT][KCH];
   uint2 wraw[W8 ? KCH : 1];
@@ -847,10 +850,19 @@ __global__ __launch_bounds__(1024) void gemm_skinny(int epi, const T* __restrict
 #pragma unroll
     for (int c = 0; c < KCH; ++c) bfr[c] = ld8(wt + c * 512);
   }
+  if constexpr (LNF) {
+    __shared__ double lnred[2][4];
+    __shared__ __attribute__((aligned(16))) T srow[2048];
+    ln_fold_prologue<T>(ln, KT * 32, bx == 0 && by == 0, srow, lnred);
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
+    for (int c = 0; c < KCH; ++c) afr[0][c] = ln_fold_frag<T>(srow, kt0 + c, lane);
+  } else {
+    const T* at = Ap + ((long)(by * MT) * KT + kt0) * 512 + lane * 8;
 #pragma unroll
-    for (int c = 0; c < KCH; ++c) afr[mt][c] = ld8(at + ((long)mt * KT + c) * 512);
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int c = 0; c < KCH; ++c) afr[mt][c] = ld8(at + ((long)mt * KT + c) * 512);
+  }
   if constexpr (W8) {
 #pragma unroll
     for (int c = 0; c < KCH; ++c) bfr[c] = dequant8<T>(wraw[c], e8m0_to_f32(wsc[c]));
@@ -1106,7 +1118,7 @@ static bool skinny_launch(int epi, const T* Ap, const void* Wp, const uint8_t* W
   const dim3 g(nx, nrb), b(64 * nw);
   switch (kch) {
 #define SK(C) \
-  case C: gemm_skinny<T, MT, C, W8><<<g, b, 0, st>>>(epi, Ap, Wp, Ws, K / 32, M, N, P); return true;
+  case C: gemm_skinny<T, MT, C, W8><<<g, b, 0, st>>>(epi, Ap, Wp, Ws, K / 32, M, N, P, LnFuse{}); return true;
     SK(1) SK(2) SK(3) SK(4) SK(6) SK(8) SK(10)
 #undef SK
     default: return false;
@@ -1121,12 +1133,17 @@ static bool skinny_launch(int epi, const T* Ap, const void* Wp, const uint8_t* W
 // order) by the consumer kernel together with the epilogue ggml applies
 // (bias, residual, scale, f16 rounding), so the reduction costs no launch.
 // ---------------------------------------------------------------------------
-template <typename T, int MT, int KCH, bool W8 = false>
+// LNF (M = 1, MT = 1): the A operand is the LayerNorm of the row formed in the
+// prologue (LnFuse, kernels.h), staged through LDS in natural order; the
+// weight loads are issued first so they overlap the LayerNorm's reductions.
+template <typename T, int MT, int KCH, bool W8 = false, bool LNF = false>
 __global__ __launch_bounds__(256) void gemm_splitk(const T* __restrict__ Ap,
                                                    const void* __restrict__ Wv,
                                                    const uint8_t* __restrict__ Ws, int KT, int M,
-                                                   int N, int kslice, float* __restrict__ P) {
+                                                   int N, int kslice, float* __restrict__ P,
+                                                   LnFuse ln) {
   using V8 = typename Elt<T>::v8;
+  static_assert(!LNF || MT == 1, "the folded LayerNorm serves one row");
   __shared__ f32x4 red[4][MT][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int bx = blockIdx.x, ks = blockIdx.y, bz = blockIdx.z;
@@ -1135,7 +1152,6 @@ __global__ __launch_bounds__(256) void gemm_splitk(const T* __restrict__ Ap,
   const int Mb = min(16 * MT, M - m_base);
   const int kt0 = (ks * kslice >> 5) + wid * KCH;
   const long f0 = (long)bx * KT + kt0;
-  const T* at = Ap + ((long)(bz * MT) * KT + kt0) * 512 + lane * 8;
   V8 bfr[KCH];
   V8 afr[MT][KCH];
   uint2 wraw[W8 ? KCH : 1];
@@ -1152,10 +1168,19 @@ __global__ __launch_bounds__(256) void gemm_splitk(const T* __restrict__ Ap,
 #pragma unroll
     for (int c = 0; c < KCH; ++c) bfr[c] = ld8(wt + c * 512);
   }
+  if constexpr (LNF) {
+    __shared__ double lnred[2][4];
+    __shared__ __attribute__((aligned(16))) T srow[2048];
+    ln_fold_prologue<T>(ln, KT * 32, bx == 0 && ks == 0 && bz == 0, srow, lnred);
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
+    for (int c = 0; c < KCH; ++c) afr[0][c] = ln_fold_frag<T>(srow, kt0 + c, lane);
+  } else {
+    const T* at = Ap + ((long)(bz * MT) * KT + kt0) * 512 + lane * 8;
 #pragma unroll
-    for (int c = 0; c < KCH; ++c) afr[mt][c] = ld8(at + ((long)mt * KT + c) * 512);
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int c = 0; c < KCH; ++c) afr[mt][c] = ld8(at + ((long)mt * KT + c) * 512);
+  }
   if constexpr (W8) {
 #pragma unroll
     for (int c = 0; c < KCH; ++c) bfr[c] = dequant8<T>(wraw[c], e8m0_to_f32(wsc[c]));
@@ -1229,9 +1254,11 @@ int gemm_splitk_partials(const T* Ap, const DecW<T>& Wd, int M, int N, int K, fl
 #define SKL(MTV, C)                                                                         \
   if (MT == MTV && kch == C) {                                                              \
     if (w8)                                                                                 \
-      gemm_splitk<T, MTV, C, true><<<g, 256, 0, st>>>(Ap, Wp, Ws, K / 32, M, N, kslice, P);  \
+      gemm_splitk<T, MTV, C, true><<<g, 256, 0, st>>>(Ap, Wp, Ws, K / 32, M, N, kslice, P,   \
+                                                      LnFuse{});                            \
     else                                                                                    \
-      gemm_splitk<T, MTV, C, false><<<g, 256, 0, st>>>(Ap, Wp, Ws, K / 32, M, N, kslice, P); \
+      gemm_splitk<T, MTV, C, false><<<g, 256, 0, st>>>(Ap, Wp, Ws, K / 32, M, N, kslice, P,  \
+                                                       LnFuse{});                           \
     return ks;                                                                              \
   }
 #define SKM(MTV) SKL(MTV, 1) SKL(MTV, 2) SKL(MTV, 3) SKL(MTV, 4) SKL(MTV, 5)
@@ -1240,6 +1267,34 @@ int gemm_splitk_partials(const T* Ap, const DecW<T>& Wd, int M, int N, int K, fl
 #undef SKL
   return 0;
 }
+
+template <typename T>
+int gemm_splitk_ln(const LnFuse& ln, const DecW<T>& Wd, int N, int K, float* P, hipStream_t st) {
+  if (K > 2048 || K % 8) return 0;
+  const void* Wp = Wd.q ? (const void*)Wd.q : (const void*)Wd.w;
+  const int ks = splitk_factor(K);
+  if (ks == 0) return 0;
+  const int kslice = K / ks;
+  const int kch = kslice / 128;
+  const dim3 g((N + 15) / 16, ks, 1);
+#define SKL(C)                                                                                 \
+  if (kch == C) {                                                                              \
+    if (Wd.q)                                                                                  \
+      gemm_splitk<T, 1, C, true, true><<<g, 256, 0, st>>>(nullptr, Wp, Wd.s, K / 32, 1, N,     \
+                                                          kslice, P, ln);                      \
+    else                                                                                       \
+      gemm_splitk<T, 1, C, false, true><<<g, 256, 0, st>>>(nullptr, Wp, Wd.s, K / 32, 1, N,    \
+                                                           kslice, P, ln);                     \
+    return ks;                                                                                 \
+  }
+  SKL(1) SKL(2) SKL(3) SKL(4) SKL(5)
+#undef SKL
+  return 0;
+}
+template int gemm_splitk_ln<_Float16>(const LnFuse&, const DecW<_Float16>&, int, int, float*,
+                                      hipStream_t);
+template int gemm_splitk_ln<__bf16>(const LnFuse&, const DecW<__bf16>&, int, int, float*,
+                                    hipStream_t);
 
 template int gemm_splitk_partials<_Float16>(const _Float16*, const DecW<_Float16>&, int, int, int,
                                             float*, hipStream_t);
@@ -1268,6 +1323,33 @@ bool gemm_decode(int epi, const T* Ap, const DecW<T>& Wd, int M, int N, int K, c
 #undef SKM
   return false;
 }
+template <typename T>
+bool gemm_decode_ln(int epi, const LnFuse& ln, const DecW<T>& Wd, int N, int K,
+                    const EpiParams& P, hipStream_t st) {
+  int nw = 0, kch = 0;
+  if (K > 2048 || K % 8 || !skinny_split(K, nw, kch, P.nw) || nw < 4) return false;
+  const void* Wp = Wd.q ? (const void*)Wd.q : (const void*)Wd.w;
+  const dim3 g((N + 15) / 16, 1), b(64 * nw);
+  switch (kch) {
+#define SK(C)                                                                                     \
+  case C:                                                                                         \
+    if (Wd.q)                                                                                     \
+      gemm_skinny<T, 1, C, true, true><<<g, b, 0, st>>>(epi, nullptr, Wp, Wd.s, K / 32, 1, N, P,  \
+                                                         ln);                                     \
+    else                                                                                          \
+      gemm_skinny<T, 1, C, false, true><<<g, b, 0, st>>>(epi, nullptr, Wp, Wd.s, K / 32, 1, N, P, \
+                                                          ln);                                    \
+    return true;
+    SK(1) SK(2) SK(3) SK(4) SK(6) SK(8) SK(10)
+#undef SK
+    default: return false;
+  }
+}
+template bool gemm_decode_ln<_Float16>(int, const LnFuse&, const DecW<_Float16>&, int, int,
+                                       const EpiParams&, hipStream_t);
+template bool gemm_decode_ln<__bf16>(int, const LnFuse&, const DecW<__bf16>&, int, int,
+                                     const EpiParams&, hipStream_t);
+
 template bool gemm_decode<_Float16>(int, const _Float16*, const DecW<_Float16>&, int, int, int,
                                     const EpiParams&, hipStream_t);
 template bool gemm_decode<__bf16>(int, const __bf16*, const DecW<__bf16>&, int, int, int,

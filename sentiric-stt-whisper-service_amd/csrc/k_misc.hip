@@ -12,6 +12,7 @@
 
 #include "kcommon.h"
 #include "kernels.h"
+#include "ln_core.h"
 
 namespace mwx {
 
@@ -185,52 +186,18 @@ __global__ __launch_bounds__(256) void ln_dec_kernel(float* __restrict__ x,
     v[e] = xa[e];
     v[4 + e] = xc[e];
   }
-  if (P) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float acc = pk[0][e >> 2][e & 3];
-#pragma unroll
-      for (int k = 1; k < 8; ++k)
-        if (k < KS) acc += pk[k][e >> 2][e & 3];
-      v[e] = (acc + (e < 4 ? pb0[e] : pb1[e - 4])) + v[e];
-    }
-  }
+  if (P) ln_fold8(v, pk, KS, pb0, pb1);
   if (P || emb.te) {
     if (own) {
       *reinterpret_cast<f32x4*>(xr) = f32x4{v[0], v[1], v[2], v[3]};
       *reinterpret_cast<f32x4*>(xr + 4) = f32x4{v[4], v[5], v[6], v[7]};
     }
   }
-  double s = 0.0;
-  if (own) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) s += (double)v[e];
-  }
-  s = wave_sum_d_dpp(s);
-  if (lane == 0) red[0][wid] = s;
-  __syncthreads();
-  s = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
-  const float mean = (float)(s / N);
-  double s2 = 0.0;
-  if (own) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float d = v[e] - mean;
-      s2 += (double)(d * d);
-    }
-  }
-  s2 = wave_sum_d_dpp(s2);
-  if (lane == 0) red[1][wid] = s2;
-  __syncthreads();
+  float mean, scale;
+  ln_stats(v, own, N, red, lane, wid, mean, scale);
   if (!own) return;
-  s2 = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
-  const float variance = (float)(s2 / N);
-  const float scale = 1.0f / sqrtf(variance + 1e-5f);
-  typename Elt<T>::v8 o;
-#pragma unroll
-  for (int e = 0; e < 8; ++e)
-    o[e] = to_t<T>(((v[e] - mean) * scale) * (e < 4 ? w0[e] : w1[e - 4]) + (e < 4 ? b0[e] : b1[e - 4]));
-  *reinterpret_cast<typename Elt<T>::v8*>(y + pack_index(row, i0, N)) = o;
+  *reinterpret_cast<typename Elt<T>::v8*>(y + pack_index(row, i0, N)) =
+      ln_out8<T>(v, mean, scale, w0, w1, b0, b1);
 }
 
 template <typename T>

@@ -122,6 +122,31 @@ struct DecW {
 template <typename T>
 int gemm_splitk_partials(const T* Ap, const DecW<T>& W, int M, int N, int K, float* P,
                          hipStream_t st);
+// The decode LayerNorm folded into the split-K GEMM that consumes it, at one
+// row (M = 1: C2, the service's single-clip requests): every workgroup forms
+// the row's residual x_in + (sum P + pbias) and its LayerNorm as its A operand
+// (ln_core.h: ln_dec_kernel's arithmetic, bit-identical) instead of reading a
+// packed LayerNorm output, so the LayerNorm costs no launch of its own.
+// Workgroup (0, 0) writes the residual to x_out, a buffer other than x_in (the
+// other workgroups still read x_in); an inactive row's x_in is copied.
+struct LnFuse {
+  const float* x_in = nullptr;
+  float* x_out = nullptr;
+  const float* P = nullptr;  // the producer's KS split-K slabs (nullptr: none)
+  int KS = 0;
+  long pstride = 0;
+  const float* pbias = nullptr;
+  const float* w = nullptr;  // LayerNorm weight / bias
+  const float* b = nullptr;
+  const int* active = nullptr;
+};
+template <typename T>
+int gemm_splitk_ln(const LnFuse& ln, const DecW<T>& W, int N, int K, float* P, hipStream_t st);
+// The same fold into a full-K decode GEMM with its epilogue (FFN1 + GELU at one
+// row); false if the shape is unsupported (the caller launches the two kernels).
+template <typename T>
+bool gemm_decode_ln(int epi, const LnFuse& ln, const DecW<T>& W, int N, int K, const EpiParams& P,
+                    hipStream_t st);
 // Decode full-K GEMM over fragment-tiled weights with a fused epilogue
 // (EPI_GELU / EPI_RES / EPI_F32 / EPI_STORE16 / EPI_DEC_QKV), rows in blocks of
 // 64 so a row's arithmetic does not depend on the batch. Returns false if K is

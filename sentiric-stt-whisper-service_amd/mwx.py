@@ -226,6 +226,8 @@ def lib() -> C.CDLL:
     L.mwx_test_set_dec_shared.restype = C.c_int
     L.mwx_test_set_dec_shared.argtypes = [C.c_int]
     L.mwx_test_set_gemm_8ph.restype = C.c_int
+    L.mwx_test_set_ln_fold.restype = C.c_int
+    L.mwx_test_set_ln_fold.argtypes = [C.c_int]
     L.mwx_test_mx_widen.restype = C.c_int
     L.mwx_test_mx_widen.argtypes = [P, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
     L.mwx_test_set_gemm_8ph.argtypes = [C.c_int]
@@ -301,6 +303,13 @@ def set_gemm_8ph(on: Optional[bool]) -> int:
     """mwx_test_set_gemm_8ph: the encoder GEMM's 8-phase main loop (True) or
     the 2-stage ring (False); None: the MWX_GEMM_8PH default."""
     return lib().mwx_test_set_gemm_8ph(-1 if on is None else int(bool(on)))
+
+
+def set_ln_fold(on: Optional[bool]) -> int:
+    """mwx_test_set_ln_fold: the decode LayerNorms folded into the next
+    split-K GEMM at one row (True) or launched separately (False); None: the
+    MWX_LN_FOLD default (on)."""
+    return lib().mwx_test_set_ln_fold(-1 if on is None else int(bool(on)))
 
 
 def set_ra_mismatch(step: Optional[int]) -> int:

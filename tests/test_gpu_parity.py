@@ -1103,3 +1103,32 @@ def test_encoder_8phase_gemm_bit_identical(make_model, arch, wt):
             mwx.set_gemm_8ph(None)
     for x, y in ((e0, e1), (k0, k1), (v0, v1)):
         assert np.array_equal(x.view(np.uint32), y.view(np.uint32)), float(np.abs(x - y).max())
+
+
+@pytest.mark.parametrize("arch,wt", [("micro-rich", mwx.GGML_F16), ("base", mwx.GGML_F16),
+                                     ("large-v3-l2", mwx.GGML_BF16)])
+def test_ln_fold_bit_identical(make_model, arch, wt):
+    """The decode LayerNorms before the QKV and cross-Q projections folded
+    into those split-K GEMMs at one row (gemm_splitk_ln, the default for
+    single-row steps: C2 and the replays' test decodes) against the separate
+    LayerNorm launches (ln_dec_kernel): the logits of every position of a
+    48-token prefix bit for bit, and a whole single-clip service-default run
+    (greedy, temperature fallback, token timestamps) record for record."""
+    path = make_model(arch, wt)
+    pcm = pcm_clip(5, 30.0)
+    toks = [int(t) for t in np.random.default_rng(7).integers(0, 50000, 48)]
+    with mwx.Context.open(path) as ctx:
+        logits, recs = [], []
+        try:
+            for fold in (False, True):
+                mwx.set_ln_fold(fold)
+                ctx.test_encode(pcm, cross=False, state_index=0)
+                logits.append(ctx.test_decode(toks))
+                idx = len(ctx.states)
+                assert ctx.full(pcm, service_params(ctx, language=b"en"), state_index=idx) == 0
+                recs.append(ctx.token_records(idx))
+        finally:
+            mwx.set_ln_fold(None)
+    assert np.array_equal(logits[0].view(np.uint32), logits[1].view(np.uint32)), \
+        float(np.abs(logits[0] - logits[1]).max())
+    assert recs[0] == recs[1] and len(recs[0]) > 0
