@@ -865,15 +865,22 @@ def test_beam_runahead_equals_host_loop(rich, temperature_inc, best_of, monkeypa
     assert ra == host
 
 
-@pytest.mark.parametrize("beam,fault_step", [(5, 0), (5, 3), (1, 2)])
-def test_runahead_mismatch_falls_back_to_host_loop(rich, beam, fault_step, monkeypatch):
+@pytest.mark.parametrize("beam,fault_step,ladder", [(5, 0, False), (5, 3, False), (1, 2, False),
+                                                    (5, 2, True), (1, 2, True)])
+def test_runahead_mismatch_falls_back_to_host_loop(rich, beam, fault_step, ladder, monkeypatch):
     """A disagreement between the device's run-ahead advance and the host's
     replay (forced at run-ahead step `fault_step` by mwx_test_set_ra_mismatch)
     does not fail the request: the attempt is redone on the host-driven loop
     and the batch's token records equal a run on the host loop throughout
-    (beam 5, the service default, and greedy)."""
+    (beam 5, the service default, and greedy). `ladder`: every window walks
+    the whole temperature ladder (logprob_thold raised), so the faulted
+    attempts include the sampling ones, whose redo must draw the uniforms the
+    run-ahead did not consume (the rows' RNGs advance only once an attempt's
+    loop has finished)."""
     ctx, _, _ = rich
-    p = service_params(ctx, beam=beam, temperature_inc=0.0, language=b"en")
+    p = service_params(ctx, beam=beam, temperature_inc=0.2 if ladder else 0.0, language=b"en")
+    if ladder:
+        p.logprob_thold = 0.5
     pcms = [pcm_clip(60 + k, 11.0 + 6 * k) for k in range(3)]
 
     def run():
