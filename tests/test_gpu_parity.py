@@ -1112,19 +1112,22 @@ def test_encoder_8phase_gemm_bit_identical(make_model, arch, wt):
         assert np.array_equal(x.view(np.uint32), y.view(np.uint32)), float(np.abs(x - y).max())
 
 
-@pytest.mark.parametrize("arch,wt", [("micro-rich", mwx.GGML_F16), ("base", mwx.GGML_F16),
-                                     ("large-v3-l2", mwx.GGML_BF16)])
-def test_ln_fold_bit_identical(make_model, arch, wt):
+@pytest.mark.parametrize("arch,wt,mx", [("micro-rich", mwx.GGML_F16, False),
+                                        ("base", mwx.GGML_F16, False),
+                                        ("large-v3-l2", mwx.GGML_BF16, False),
+                                        ("large-v3-l2", mwx.GGML_BF16, True)])
+def test_ln_fold_bit_identical(make_model, arch, wt, mx):
     """The decode LayerNorms before the QKV and cross-Q projections folded
     into those split-K GEMMs at one row (gemm_splitk_ln, the default for
     single-row steps: C2 and the replays' test decodes) against the separate
     LayerNorm launches (ln_dec_kernel): the logits of every position of a
     48-token prefix bit for bit, and a whole single-clip service-default run
-    (greedy, temperature fallback, token timestamps) record for record."""
+    (greedy, temperature fallback, token timestamps) record for record. mx:
+    MX-fp8 compute (the fold's fp8-weight GEMM variants)."""
     path = make_model(arch, wt)
     pcm = pcm_clip(5, 30.0)
     toks = [int(t) for t in np.random.default_rng(7).integers(0, 50000, 48)]
-    with mwx.Context.open(path) as ctx:
+    with mwx.Context.open(path, compute=mwx.COMPUTE_MXFP8 if mx else mwx.COMPUTE_MODEL) as ctx:
         logits, recs = [], []
         try:
             for fold in (False, True):
