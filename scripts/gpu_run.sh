@@ -90,6 +90,8 @@ for s in "$@"; do
     c2f*) run "$s" 300 python -u bench.py --arch base --wtype f16 --clips 1 --lanes 1 --steps 20 --warmup 3 --no-cpu-baseline ;;
     streamrnf) run streamrnf 300 env MWX_LN_FOLD=0 python -u bench.py --stream --rich --arch base --wtype f16 --steps 3 --warmup 1 ;;
     ramm) run ramm 400 python -u -m pytest tests/test_gpu_parity.py -k "runahead_mismatch or ln_fold" -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
+    mrdiag) run mrdiag 500 python -u scripts/probe/multirank_diag.py ;;
+    mrtests) run mrtests 600 python -u -m pytest tests/test_multi_rank.py -m gpu -v -s -rf --timeout 500 --timeout-method thread ;;
     newtests) run newtests 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shapes.py -k "extreme_scales or widening or runahead_mismatch or grouped_self or beam_search" -m gpu -v -s -rf --timeout 300 --timeout-method thread ;;
     pmcbs)  # beam 5 bf16 at the benched 220 steps: FETCH and LDS / MFMA passes (the self-attention's history reads)
       for x in "fetch:FETCH_SIZE" "lds:SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE"; do

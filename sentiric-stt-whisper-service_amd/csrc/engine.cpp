@@ -84,7 +84,16 @@ struct DBuf {
       n = 0;
       HIPC(hipMalloc(&p, bytes));
       n = bytes;
-      if (zero) HIPC(hipMemset(p, 0, bytes));
+      if (zero) {
+        // the fill is queued on the null stream, which the states' non-blocking
+        // streams do not wait for: wait for it here, or the first kernels on a
+        // fresh buffer can run before (or under) it -- seen as run-to-run
+        // differences of a fresh context's first batch with another process
+        // on the GPU (zero-padded encoder inputs overwritten after the
+        // producer wrote them)
+        HIPC(hipMemset(p, 0, bytes));
+        HIPC(hipStreamSynchronize(nullptr));
+      }
     }
     return p;
   }
