@@ -1191,6 +1191,25 @@ struct Driver {
   // The d- and 3d-wide projections run as split-K GEMMs writing f32 partial
   // slabs; each consumer (LN: bias + residual, attention: bias/scale/f16 and
   // the KV-cache append) folds the slabs in, so no launch is added.
+  // the LayerNorm fold at one row (layer_pre): x = the residual now (c.xd),
+  // moving to the other buffer; P / KS / pbias the producer's slabs and bias
+  bool ln_folds(const LayerRows& rw) const {
+    return rw.n == 1 && rw.xd2 && !rw.prefill && ln_fold_on();
+  }
+  LnFuse ln_fuse(const LayerRows& rw, const LayerRun& c, const float* P, int KS,
+                 const float* pbias, const float* w, const float* b) const {
+    LnFuse f;
+    f.x_in = c.xd;
+    f.x_out = c.xd == rw.xd ? rw.xd2 : rw.xd;
+    f.P = P;
+    f.KS = KS;
+    f.pstride = (long)rw.n * d;
+    f.pbias = pbias;
+    f.w = w;
+    f.b = b;
+    f.active = rw.act;
+    return f;
+  }
   void layer_pre(const LayerRows& rw, LayerRun& c, int l, hipStream_t s) {
     const int n = rw.n;
     const float kqs = powf(64.0f, -0.25f);
@@ -1209,24 +1228,16 @@ struct Driver {
       emb.n_pos = Tctx;
       c.embed = false;
     }
-    // one row (C2, single-clip requests): the LayerNorms before the QKV and
-    // cross-Q projections are folded into those split-K GEMMs (gemm_splitk_ln:
-    // the same arithmetic, no launch of their own); the residual moves to the
-    // other buffer at each. MWX_LN_FOLD=0 keeps the separate launches (A/B).
-    const bool fold = n == 1 && rw.xd2 && !rw.prefill && ln_fold_on();
-    auto other = [&](float* x) { return x == rw.xd ? rw.xd2 : rw.xd; };
+    // one row (C2, single-clip requests): the LayerNorms before the QKV,
+    // cross-Q and FFN1 projections are folded into those GEMMs
+    // (gemm_splitk_ln / gemm_decode_ln: the same arithmetic, no launch of
+    // their own); the residual moves to the other buffer at each.
+    // MWX_LN_FOLD=0 keeps the separate launches (A/B).
+    const bool fold = ln_folds(rw);
     c.k1 = 0;
     if (fold && !emb.te) {
-      LnFuse f;
-      f.x_in = c.xd;
-      f.x_out = other(c.xd);
-      f.P = c.ks_prev ? rw.Pres : nullptr;
-      f.KS = c.ks_prev;
-      f.pstride = (long)n * d;
-      f.pbias = c.bias_prev;
-      f.w = W.ln1_w;
-      f.b = W.ln1_b;
-      f.active = rw.act;
+      const LnFuse f = ln_fuse(rw, c, c.ks_prev ? rw.Pres : nullptr, c.ks_prev, c.bias_prev,
+                               W.ln1_w, W.ln1_b);
       PerfScope ps(S, "dec_gemm", s);
       c.k1 = gemm_splitk_ln<T>(f, Dw(W.qkv), 3 * d, d, rw.Pqkv, s);
       if (c.k1) c.xd = f.x_out;
@@ -1250,16 +1261,7 @@ struct Driver {
       c.k2 = gemm_splitk_partials<T>(rw.od, Dw(W.o), n, d, d, rw.Pres, s); }
     c.k3 = 0;
     if (fold) {
-      LnFuse f;
-      f.x_in = c.xd;
-      f.x_out = other(c.xd);
-      f.P = rw.Pres;
-      f.KS = c.k2;
-      f.pstride = (long)n * d;
-      f.pbias = W.o_b;
-      f.w = W.lnc_w;
-      f.b = W.lnc_b;
-      f.active = rw.act;
+      const LnFuse f = ln_fuse(rw, c, rw.Pres, c.k2, W.o_b, W.lnc_w, W.lnc_b);
       PerfScope ps(S, "dec_gemm", s);
       c.k3 = gemm_splitk_ln<T>(f, Dw(W.cq), d, d, rw.Pq, s);
       if (c.k3) c.xd = f.x_out;
@@ -1321,17 +1323,8 @@ struct Driver {
     e.ldc = 4 * d;
     e.pack_out = true;
     c.k5 = false;
-    if (n == 1 && rw.xd2 && !rw.prefill && ln_fold_on()) {  // (as layer_pre)
-      LnFuse f;
-      f.x_in = c.xd;
-      f.x_out = c.xd == rw.xd ? rw.xd2 : rw.xd;
-      f.P = rw.Pres;
-      f.KS = c.k4;
-      f.pstride = (long)n * d;
-      f.pbias = W.co_b;
-      f.w = W.ln2_w;
-      f.b = W.ln2_b;
-      f.active = rw.act;
+    if (ln_folds(rw)) {  // (as layer_pre)
+      const LnFuse f = ln_fuse(rw, c, rw.Pres, c.k4, W.co_b, W.ln2_w, W.ln2_b);
       PerfScope ps(S, "dec_gemm", s);
       c.k5 = gemm_decode_ln<T>(EPI_GELU, f, Dw(W.fc1), 4 * d, d, e, s);
       if (c.k5) c.xd = f.x_out;
