@@ -401,10 +401,15 @@ def gather_summary(block, clips, per_clip):
     import shard
     if block is None:
         return None
+    import zlib
     recs = shard.unpack_records(block)
     full = (lambda r: len(r) == per_clip) if per_clip else (lambda r: len(r) > 0)
+    # crc32 of the records (id, t0, t1, p bits): equal across runs and boxes
+    # for the same build and workload (the decode is deterministic)
+    crc = zlib.crc32(repr(recs).encode())
     return {"clips": len(recs), "tokens": sum(len(r) for r in recs),
-            "complete": len(recs) == clips and all(full(r) for r in recs)}
+            "complete": len(recs) == clips and all(full(r) for r in recs),
+            "records_crc32": f"{crc:08x}"}
 
 
 def launch_ranks(n):
